@@ -1,0 +1,203 @@
+"""bench.py -- TileSpGEMM on MI355X: SpGEMM GFLOPS (fp64, C = A^2) + HBM roofline.
+
+One "step" = one full device pass of the hot path on one matrix, device CSR in ->
+device CSR out: GPU csr2tile(A) + csr2tile(B) + step 1 + step 2 (+ scan) +
+step 3 + GPU tile2csr (SURVEY.md §8d t_e2e).  Inputs are resident in HBM
+(torch tensors) before the timed region.  GFLOPS = 2*nnzCub/t
+(src/tilespgemm-cuda.h:2808).
+
+  python bench.py                       # N=1, webbase-1M synthetic stand-in
+  python bench.py --gpus N ...          # under torch.distributed.run: A split by
+                                        # tile-row blocks of equal work, B
+                                        # replicated, C gathered to rank 0 (RCCL)
+Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "SpGEMM GFLOPS (fp64, C=A^2) + achieved HBM GB/s fraction, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def load_matrix(args):
+    from spgemm_amd import synth
+    if args.mtx:
+        from spgemm_amd import tilespgemm as T
+        A = T.mmio_allinone(args.mtx)
+        T.values_pos_mod10(A)
+        m, n, rp, ci, vv = A.csr()
+        return m, n, rp, ci, vv, os.path.basename(args.mtx), "real"
+    m, n, rp, ci, vv = synth.GENERATORS[args.matrix]()
+    return m, n, rp, ci, vv, args.matrix + "-synthetic", "synthetic"
+
+
+def transpose_host(m, n, rp, ci, vv):
+    import scipy.sparse as sp
+    T = sp.csr_matrix((vv, ci, rp), shape=(m, n)).T.tocsr()
+    T.sort_indices()
+    return n, m, T.indptr.astype(np.int32), T.indices.astype(np.int32), T.data
+
+
+def nnzcub_rows(rp_a, ci_a, rp_b, r0, r1):
+    blen = np.diff(rp_b.astype(np.int64))
+    s, e = int(rp_a[r0]), int(rp_a[r1])
+    return int(blen[ci_a[s:e]].sum())
+
+
+def cpu_baseline(m, n, rp, ci, vv, mb, nb, rpb, cib, vvb, budget_s):
+    """The reference's CPU SPA (spgemm_serialref_spa_new.h, clean-room oracle
+    restatement, both passes) on a bounded row prefix of the same workload."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import _oracle as O
+    A = O.OMat.from_csr(m, n, rp, ci, vv)
+    B = O.OMat.from_csr(mb, nb, rpb, cib, vvb)
+    rows = min(m, 2000)
+    t0 = time.perf_counter()
+    O.spa(A, B, 0, rows)
+    t = time.perf_counter() - t0
+    rows2 = int(min(m, max(rows, rows * budget_s / max(t, 1e-6))))
+    t0 = time.perf_counter()
+    O.spa(A, B, 0, rows2)
+    t = time.perf_counter() - t0
+    cub = nnzcub_rows(rp, ci, rpb, 0, rows2)
+    return {"value": round(2.0 * cub / t / 1e9, 4), "unit": "GFLOPS", "cores": O.num_threads(),
+            "kind": "port",
+            "sample": f"spgemm_spa restatement (count+fill passes), rows [0,{rows2}) of {m} "
+                      f"({cub} of the intermediate products), {t:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--matrix", default="webbase", choices=["webbase", "cant", "mc2depi", "lj"])
+    ap.add_argument("--mtx", default=os.environ.get("TSG_MTX"))
+    ap.add_argument("--aat", type=int, default=None)
+    ap.add_argument("--tile", type=int, default=16)
+    ap.add_argument("--cpu-budget-s", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from spgemm_amd.device import Context, DeviceCSR
+    from spgemm_amd import dist as tdist
+
+    m, n, rp, ci, vv, name, data_kind = load_matrix(args)
+    aat = args.aat if args.aat is not None else (1 if args.matrix == "mc2depi" and not args.mtx else 0)
+    if aat:
+        mb, nb, rpb, cib, vvb = transpose_host(m, n, rp, ci, vv)
+    else:
+        mb, nb, rpb, cib, vvb = m, n, rp, ci, vv
+    tm = args.tile
+    nnzcub_total = nnzcub_rows(rp, ci, rpb, 0, m)
+    if world > 1:
+        work = tdist.tile_row_work(rp, ci, rpb, m, tm)
+        parts = tdist.partition_tile_rows(work, world)
+        t0r, t1r = parts[rank]
+        mblk, rpblk, ciblk, vvblk = tdist.slice_rows(m, rp, ci, vv, t0r * tm, t1r * tm)
+    else:
+        mblk, rpblk, ciblk, vvblk = m, rp, ci, vv
+    dA = DeviceCSR.from_host(mblk, n, rpblk, ciblk, vvblk)
+    dB = dA if (not aat and world == 1) else DeviceCSR.from_host(mb, nb, rpb, cib, vvb)
+    ctx = Context(local)
+    torch.cuda.synchronize()
+
+    def one_step():
+        ctx.reset()
+        c, st = ctx.spgemm(dA, dB, tm, tm)
+        if world > 1:
+            cblk = ctx.to_torch(c)
+            tdist.gather_csr_blocks(cblk.rowptr, cblk.col, cblk.val, rank, world)
+        return c, st
+
+    for _ in range(args.warmup):
+        one_step()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    stats = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        c, st = one_step()
+        stats.append(st)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        nz = torch.tensor([c.nnz], dtype=torch.int64, device="cuda")
+        dist.all_reduce(nz)
+        nnzC = int(nz.item())
+    else:
+        nnzC = c.nnz
+    ms_per_step = elapsed * 1e3 / args.steps
+    gflops = 2.0 * nnzcub_total * args.steps / elapsed / 1e9
+
+    med = {k: float(np.median([s[k] for s in stats])) for k in stats[0]}
+    dev_ms = med["t_csr2tile_ms"] + med["t_step1_ms"] + med["t_step2_ms"] + med["t_step3_ms"] + med["t_tile2csr_ms"]
+    # SURVEY §8d algorithmic bytes (src/external/cusparse/main.cu:205-208), this rank's share
+    b_alg = 4.0 * (mblk + 1) + 12.0 * len(ciblk) + 4.0 * (mb + 1) + 12.0 * len(cib) + 4.0 * (mblk + 1) + 12.0 * c.nnz
+    achieved = b_alg / (dev_ms * 1e-3) / 1e9
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            try:
+                cpu = cpu_baseline(m, n, rp, ci, vv, mb, nb, rpb, cib, vvb, args.cpu_budget_s)
+            except Exception as e:  # the baseline is reported, never required
+                log(f"cpu baseline failed: {e!r}")
+        out = {
+            "metric": METRIC, "value": round(gflops, 3), "unit": "GFLOPS", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True, "scaling": "strong" if world > 1 else "weak",
+            "vs_baseline": None, "dtype": "f64", "data": data_kind,
+            "config": {"workload": f"{name} C=A{'*A^T' if aat else '^2'} fp64, {tm}x{tm} tiles, "
+                                   "csr2tile+steps1-3+tile2csr (device CSR in -> device CSR out)",
+                       "m": m, "nnzA": int(len(ci)), "nnzCub": nnzcub_total, "nnzC": nnzC,
+                       "numtileA": int(med["numtileA"]), "numblkC": int(med["numblkC"]),
+                       "parallelism": f"row-block{world}" if world > 1 else "single"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "kernel": "device pipeline per step (B_alg of SURVEY §8d / HIP-event device time)",
+                         "algorithmic_bytes": int(b_alg), "device_ms": round(dev_ms, 4)},
+            "stage_ms": {k: round(med[k], 4) for k in ("t_csr2tile_ms", "t_step1_ms", "t_step2_ms",
+                                                        "t_step3_ms", "t_tile2csr_ms", "t_malloc_ms",
+                                                        "t_kern_ms", "t_e2e_ms")},
+            "gflops_kern": round(2.0 * nnzcub_total / (med["t_kern_ms"] * 1e-3) / 1e9, 3) if world == 1 else None,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

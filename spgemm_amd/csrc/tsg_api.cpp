@@ -1,0 +1,680 @@
+// tsg_api.cpp -- C ABI of libtsg.so (include/tsg.h): context + caching device
+// allocator, the reference-named host functions, and the Matrix-Market reader.
+// All arithmetic of the hot path runs in the HIP kernels of tsg_device.hip; the
+// host functions only move data and orchestrate.
+#include <hip/hip_runtime.h>
+
+#include <cctype>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "tsg_internal.h"
+
+namespace tsg {
+int dev_tiles_finalize_c(Context &cx, tsg_dev_tiles &C, hipStream_t s);
+int dev_rm2csc_from_structs(Context &cx, tsg_dev_tiles &B, hipStream_t s);
+
+void report_hip_error(hipError_t e, const char *what, const char *file, int line) {
+    if (!getenv("TSG_QUIET_ERRORS"))
+        fprintf(stderr, "[tsg] HIP error %d (%s) at %s:%d: %s\n", (int)e, hipGetErrorString(e), file, line, what);
+}
+
+// ------------------------------------------------------------------ pool
+static size_t size_class(size_t b) {
+    size_t c = 256;
+    while (c < b) c <<= 1;
+    return c;
+}
+
+DevicePool::~DevicePool() { trim(); }
+
+int DevicePool::alloc(void **p, size_t bytes) {
+    size_t c = size_class(bytes ? bytes : 1);
+    auto it = free_.find(c);
+    if (it != free_.end()) {
+        *p = it->second;
+        free_.erase(it);
+        live_[*p] = c;
+        return TSG_OK;
+    }
+    void *q = nullptr;
+    hipError_t e = hipMalloc(&q, c);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        trim();  // give cached blocks back and retry once
+        e = hipMalloc(&q, c);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            *p = nullptr;
+            return TSG_ERR_OOM;
+        }
+    }
+    reserved_ += c;
+    live_[q] = c;
+    *p = q;
+    return TSG_OK;
+}
+
+void DevicePool::release(void *p) {
+    auto it = live_.find(p);
+    if (it == live_.end()) return;
+    free_.emplace(it->second, p);
+    live_.erase(it);
+}
+
+void DevicePool::release_all_live() {
+    for (auto &kv : live_) free_.emplace(kv.second, kv.first);
+    live_.clear();
+}
+
+void DevicePool::trim() {
+    for (auto &kv : free_) {
+        (void)hipFree(kv.second);
+        reserved_ -= kv.first;
+    }
+    free_.clear();
+}
+
+int Context::init(int dev) {
+    device = dev;
+    TSG_HIP(hipSetDevice(dev));
+    TSG_HIP(hipHostMalloc((void **)&pinned, 64, hipHostMallocDefault));
+    TSG_HIP(hipHostMalloc((void **)&pinned64, 64, hipHostMallocDefault));
+    for (auto &e : ev) TSG_HIP(hipEventCreate(&e));
+    ev_ready = true;
+    return TSG_OK;
+}
+
+void Context::destroy() {
+    (void)hipSetDevice(device);
+    (void)hipDeviceSynchronize();
+    pool.release_all_live();
+    pool.trim();
+    if (pinned) (void)hipHostFree(pinned);
+    if (pinned64) (void)hipHostFree(pinned64);
+    pinned = nullptr;
+    pinned64 = nullptr;
+    if (ev_ready)
+        for (auto &e : ev) (void)hipEventDestroy(e);
+    ev_ready = false;
+}
+
+static double ev_ms(hipEvent_t a, hipEvent_t b) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0.0;
+    }
+    return (double)ms;
+}
+
+}  // namespace tsg
+
+using namespace tsg;
+
+struct tsg_context {
+    Context cx;
+};
+
+// ------------------------------------------------------------------ helpers
+static int g_have_device = -1;
+
+static int check_device() {
+    if (g_have_device < 0) {
+        int n = 0;
+        hipError_t e = hipGetDeviceCount(&n);
+        if (e != hipSuccess) (void)hipGetLastError();
+        g_have_device = (e == hipSuccess && n > 0) ? 1 : 0;
+    }
+    return g_have_device ? TSG_OK : TSG_ERR_NO_DEVICE;
+}
+
+static tsg_context *g_default = nullptr;
+
+static int default_ctx(tsg_context **out) {
+    TSG_TRY(check_device());
+    if (!g_default) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess) {
+            (void)hipGetLastError();
+            dev = 0;
+        }
+        tsg_context *c = new tsg_context();
+        int rc = c->cx.init(dev);
+        if (rc != TSG_OK) {
+            delete c;
+            return rc;
+        }
+        g_default = c;
+    }
+    *out = g_default;
+    return TSG_OK;
+}
+
+template <class T> static int upload(Context &cx, T **d, const T *h, size_t n, hipStream_t s) {
+    TSG_TRY(cx.get(d, n ? n : 1));
+    if (n) TSG_HIP(hipMemcpyAsync(*d, h, n * sizeof(T), hipMemcpyHostToDevice, s));
+    return TSG_OK;
+}
+
+template <class T> static int download(T **h, const T *d, size_t n, hipStream_t s) {
+    *h = (T *)malloc((n ? n : 1) * sizeof(T));
+    if (!*h) return TSG_ERR_OOM;
+    if (n) TSG_HIP(hipMemcpyAsync(*h, d, n * sizeof(T), hipMemcpyDeviceToHost, s));
+    return TSG_OK;
+}
+
+static bool valid_tiles(int tm, int tn) {
+    return tm > 0 && tn > 0 && tm % 16 == 0 && tn % 16 == 0 && tm <= 64 && tn <= 64 && (long)tm * tn <= 65536;
+}
+
+static int upload_csr(Context &cx, const tsg_smatrix *A, tsg_dev_csr &d, hipStream_t s) {
+    d.m = A->m;
+    d.n = A->n;
+    d.nnz = A->nnz;
+    TSG_TRY(upload(cx, &d.rowpointer, A->rowpointer, (size_t)A->m + 1, s));
+    TSG_TRY(upload(cx, &d.columnindex, A->columnindex, (size_t)A->nnz, s));
+    TSG_TRY(upload(cx, &d.value, A->value, (size_t)A->nnz, s));
+    return TSG_OK;
+}
+
+static void free_tile_fields(tsg_smatrix *M) {
+    free(M->tile_ptr); free(M->tile_columnidx); free(M->tile_rowidx); free(M->tile_nnz);
+    free(M->tile_csr_Value); free(M->tile_csr_Col); free(M->tile_csr_Ptr); free(M->mask);
+    free(M->csc_tile_ptr); free(M->csc_tile_rowidx);
+    M->tile_ptr = M->tile_columnidx = M->tile_rowidx = M->tile_nnz = nullptr;
+    M->tile_csr_Value = nullptr;
+    M->tile_csr_Col = M->tile_csr_Ptr = M->mask = nullptr;
+    M->csc_tile_ptr = M->csc_tile_rowidx = nullptr;
+}
+
+static int download_tiles(const tsg_dev_tiles &t, tsg_smatrix *M, bool csc, hipStream_t s) {
+    free_tile_fields(M);
+    const size_t nt = (size_t)t.numtile;
+    M->tilem = t.tilem;
+    M->tilen = t.tilen;
+    M->numtile = t.numtile;
+    TSG_TRY(download(&M->tile_ptr, t.tile_ptr, (size_t)t.tilem + 1, s));
+    TSG_TRY(download(&M->tile_columnidx, t.tile_columnidx, nt, s));
+    if (t.tile_rowidx) TSG_TRY(download(&M->tile_rowidx, t.tile_rowidx, nt, s));
+    TSG_TRY(download(&M->tile_nnz, t.tile_nnz, nt + 1, s));
+    TSG_TRY(download(&M->tile_csr_Ptr, t.tile_csr_Ptr, nt * t.tile_m, s));
+    TSG_TRY(download(&M->tile_csr_Col, t.tile_csr_Col, (size_t)t.nnz, s));
+    TSG_TRY(download(&M->tile_csr_Value, t.tile_csr_Value, (size_t)t.nnz, s));
+    TSG_TRY(download(&M->mask, t.mask, nt * t.tile_m * (t.tile_n / 16), s));
+    if (csc) {
+        TSG_TRY(download(&M->csc_tile_ptr, t.csc_tile_ptr, (size_t)t.tilen + 1, s));
+        TSG_TRY(download(&M->csc_tile_rowidx, t.csc_tile_rowidx, nt, s));
+    }
+    TSG_HIP(hipStreamSynchronize(s));
+    return TSG_OK;
+}
+
+static int upload_tiles(Context &cx, const tsg_smatrix *M, int tile_m, int tile_n, bool csc, tsg_dev_tiles &t,
+                        hipStream_t s) {
+    t = tsg_dev_tiles{};
+    t.m = M->m; t.n = M->n; t.nnz = M->nnz;
+    t.tile_m = tile_m; t.tile_n = tile_n;
+    t.tilem = M->tilem; t.tilen = M->tilen; t.numtile = M->numtile;
+    const size_t nt = (size_t)M->numtile;
+    TSG_TRY(upload(cx, &t.tile_ptr, M->tile_ptr, (size_t)M->tilem + 1, s));
+    TSG_TRY(upload(cx, &t.tile_columnidx, M->tile_columnidx, nt, s));
+    TSG_TRY(upload(cx, &t.tile_nnz, M->tile_nnz, nt + 1, s));
+    TSG_TRY(upload(cx, &t.tile_csr_Ptr, M->tile_csr_Ptr, nt * tile_m, s));
+    TSG_TRY(upload(cx, &t.tile_csr_Col, M->tile_csr_Col, (size_t)M->nnz, s));
+    TSG_TRY(upload(cx, &t.tile_csr_Value, M->tile_csr_Value, (size_t)M->nnz, s));
+    TSG_TRY(upload(cx, &t.mask, M->mask, nt * tile_m * (tile_n / 16), s));
+    if (csc) {
+        if (!M->csc_tile_ptr || !M->csc_tile_rowidx) return TSG_ERR_INVALID;
+        TSG_TRY(upload(cx, &t.csc_tile_ptr, M->csc_tile_ptr, (size_t)M->tilen + 1, s));
+        TSG_TRY(upload(cx, &t.csc_tile_rowidx, M->csc_tile_rowidx, nt, s));
+        TSG_TRY(dev_rm2csc_from_structs(cx, t, s));
+    }
+    return TSG_OK;
+}
+
+static bool quiet() { return getenv("TSG_QUIET") != nullptr; }
+
+// ------------------------------------------------------------------ C ABI
+extern "C" {
+
+const char *tsg_version(void) { return "tsg-mi355x 0.1 (gfx950)"; }
+
+int tsg_device_count(int *count) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        n = 0;
+    }
+    *count = n;
+    return TSG_OK;
+}
+
+const char *tsg_status_string(int st) {
+    switch (st) {
+        case TSG_OK: return "ok";
+        case TSG_ERR_INVALID: return "invalid argument";
+        case TSG_ERR_HIP: return "HIP runtime error";
+        case TSG_ERR_OOM: return "out of memory";
+        case TSG_ERR_OVERFLOW: return "count overflows the int32 layout";
+        case TSG_ERR_NO_DEVICE: return "no HIP device";
+        case TSG_ERR_UNSUPPORTED: return "unsupported tile size / shape";
+        case TSG_ERR_IO: return "Matrix-Market read error";
+        default: return "unknown";
+    }
+}
+
+// ---- Matrix-Market reader: same CSR order as mmio_allinone
+// (src/mmio_highlevel.h:593-759).  Whole-file read + hand-rolled tokenizer.
+int tsg_mmio_allinone(const char *filename, tsg_smatrix *A) {
+    if (!filename || !A) return TSG_ERR_INVALID;
+    memset(A, 0, sizeof(*A));
+    FILE *f = fopen(filename, "rb");
+    if (!f) return TSG_ERR_IO;
+    fseek(f, 0, SEEK_END);
+    long sz = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    std::vector<char> buf((size_t)sz + 1);
+    if (sz > 0 && fread(buf.data(), 1, (size_t)sz, f) != (size_t)sz) {
+        fclose(f);
+        return TSG_ERR_IO;
+    }
+    fclose(f);
+    buf[sz] = 0;
+    char *p = buf.data(), *end = buf.data() + sz;
+    // banner
+    char *eol = (char *)memchr(p, '\n', end - p);
+    if (!eol) eol = end;
+    std::string banner(p, eol);
+    for (auto &ch : banner) ch = (char)tolower(ch);
+    char t0[64] = {0}, t1[64] = {0}, t2[64] = {0}, t3[64] = {0}, t4[64] = {0};
+    if (sscanf(banner.c_str(), "%63s %63s %63s %63s %63s", t0, t1, t2, t3, t4) != 5) return TSG_ERR_IO;
+    if (strncmp(t0, "%%matrixmarket", 14) != 0 || strcmp(t1, "matrix") != 0) return TSG_ERR_IO;
+    if (strcmp(t2, "coordinate") != 0) return TSG_ERR_UNSUPPORTED;
+    const bool is_real = !strcmp(t3, "real"), is_cplx = !strcmp(t3, "complex");
+    const bool is_int = !strcmp(t3, "integer"), is_pat = !strcmp(t3, "pattern");
+    if (!(is_real || is_cplx || is_int || is_pat)) return TSG_ERR_UNSUPPORTED;
+    const bool sym = !strcmp(t4, "symmetric") || !strcmp(t4, "hermitian");
+    p = (eol < end) ? eol + 1 : end;
+    while (p < end && *p == '%') {  // comment lines
+        char *q = (char *)memchr(p, '\n', end - p);
+        p = q ? q + 1 : end;
+    }
+    char *q;
+    long m = strtol(p, &q, 10); p = q;
+    long n = strtol(p, &q, 10); p = q;
+    long nz = strtol(p, &q, 10); p = q;
+    if (m < 0 || n < 0 || nz < 0 || m > 0x7fffffff || n > 0x7fffffff) return TSG_ERR_IO;
+    std::vector<int> ri((size_t)nz), ci((size_t)nz);
+    std::vector<double> vv((size_t)nz);
+    std::vector<long long> cnt((size_t)m + 1, 0);
+    for (long k = 0; k < nz; ++k) {
+        long i = strtol(p, &q, 10);
+        if (q == p) return TSG_ERR_IO;
+        p = q;
+        long j = strtol(p, &q, 10);
+        if (q == p) return TSG_ERR_IO;
+        p = q;
+        double x = 1.0;
+        if (is_real || is_cplx) {
+            x = strtod(p, &q); p = q;
+            if (is_cplx) { (void)strtod(p, &q); p = q; }
+        } else if (is_int) {
+            x = (double)strtol(p, &q, 10); p = q;
+        }
+        if (i < 1 || j < 1 || i > m || j > n) return TSG_ERR_IO;
+        ri[k] = (int)(i - 1);
+        ci[k] = (int)(j - 1);
+        vv[k] = x;
+        cnt[i - 1]++;
+    }
+    if (sym)
+        for (long k = 0; k < nz; ++k)
+            if (ri[k] != ci[k]) cnt[ci[k]]++;
+    long long run = 0;
+    for (long r = 0; r <= m; ++r) {
+        long long v = cnt[r];
+        cnt[r] = run;
+        run += v;
+    }
+    if (run > 0x7fffffffLL) return TSG_ERR_OVERFLOW;
+    A->m = (int)m; A->n = (int)n; A->nnz = (int)run; A->isSymmetric = sym ? 1 : 0;
+    A->rowpointer = (int *)malloc(((size_t)m + 1) * sizeof(int));
+    A->columnindex = (int *)malloc((size_t)(run ? run : 1) * sizeof(int));
+    A->value = (double *)malloc((size_t)(run ? run : 1) * sizeof(double));
+    if (!A->rowpointer || !A->columnindex || !A->value) return TSG_ERR_OOM;
+    for (long r = 0; r <= m; ++r) A->rowpointer[r] = (int)cnt[r];
+    std::vector<int> fill((size_t)m + 1, 0);
+    for (long k = 0; k < nz; ++k) {
+        int r = ri[k], c = ci[k];
+        int d = A->rowpointer[r] + fill[r]++;
+        A->columnindex[d] = c;
+        A->value[d] = vv[k];
+        if (sym && r != c) {
+            d = A->rowpointer[c] + fill[c]++;
+            A->columnindex[d] = r;
+            A->value[d] = vv[k];
+        }
+    }
+    return TSG_OK;
+}
+
+void tsg_values_pos_mod10(tsg_smatrix *A) {
+    for (int k = 0; k < A->nnz; ++k) A->value[k] = (double)(k % 10);
+}
+
+void tsg_matrix_destroy(tsg_smatrix *M) {
+    if (!M) return;
+    free(M->value); free(M->columnindex); free(M->rowpointer);
+    free_tile_fields(M);
+    memset(M, 0, sizeof(*M));
+}
+
+int tsg_transpose(const tsg_smatrix *A, tsg_smatrix *B) {
+    if (!A || !B) return TSG_ERR_INVALID;
+    tsg_context *c;
+    TSG_TRY(default_ctx(&c));
+    Context &cx = c->cx;
+    hipStream_t s = 0;
+    tsg_dev_csr dA, dB;
+    TSG_TRY(upload_csr(cx, A, dA, s));
+    TSG_TRY(dev_transpose(cx, dA, dB, s));
+    memset(B, 0, sizeof(*B));
+    B->m = dB.m; B->n = dB.n; B->nnz = dB.nnz;
+    TSG_TRY(download(&B->rowpointer, dB.rowpointer, (size_t)dB.m + 1, s));
+    TSG_TRY(download(&B->columnindex, dB.columnindex, (size_t)dB.nnz, s));
+    TSG_TRY(download(&B->value, dB.value, (size_t)dB.nnz, s));
+    TSG_HIP(hipStreamSynchronize(s));
+    cx.pool.release_all_live();
+    return TSG_OK;
+}
+
+int tsg_nnzcub(const tsg_smatrix *A, const tsg_smatrix *B, unsigned long long *out) {
+    if (!A || !B || !out || A->n != B->m) return TSG_ERR_INVALID;
+    tsg_context *c;
+    TSG_TRY(default_ctx(&c));
+    Context &cx = c->cx;
+    hipStream_t s = 0;
+    tsg_dev_csr dA, dB;
+    TSG_TRY(upload_csr(cx, A, dA, s));
+    TSG_TRY(upload(cx, &dB.rowpointer, B->rowpointer, (size_t)B->m + 1, s));
+    unsigned long long *d = nullptr;
+    TSG_TRY(cx.get(&d, 1));
+    TSG_TRY(launch_nnzcub(cx, dA, dB, d, s));
+    TSG_HIP(hipMemcpyAsync(out, d, sizeof(*out), hipMemcpyDeviceToHost, s));
+    TSG_HIP(hipStreamSynchronize(s));
+    cx.pool.release_all_live();
+    return TSG_OK;
+}
+
+int tsg_csr2tile_row_major(tsg_smatrix *A, int tm, int tn) {
+    if (!A || !valid_tiles(tm, tn)) return TSG_ERR_INVALID;
+    if (!tile_size_supported(tm, tn)) return TSG_ERR_UNSUPPORTED;
+    tsg_context *c;
+    TSG_TRY(default_ctx(&c));
+    Context &cx = c->cx;
+    hipStream_t s = 0;
+    tsg_dev_csr d;
+    tsg_dev_tiles t;
+    TSG_TRY(upload_csr(cx, A, d, s));
+    int rc = dev_csr2tile_row_major(cx, d, tm, tn, t, s);
+    if (rc == TSG_OK) rc = download_tiles(t, A, false, s);
+    cx.pool.release_all_live();
+    return rc;
+}
+
+int tsg_csr2tile_col_major(tsg_smatrix *B, int tm, int tn) {
+    if (!B || !valid_tiles(tm, tn)) return TSG_ERR_INVALID;
+    if (!tile_size_supported(tm, tn)) return TSG_ERR_UNSUPPORTED;
+    tsg_context *c;
+    TSG_TRY(default_ctx(&c));
+    Context &cx = c->cx;
+    hipStream_t s = 0;
+    tsg_dev_csr d;
+    tsg_dev_tiles t;
+    TSG_TRY(upload_csr(cx, B, d, s));
+    int rc = dev_csr2tile_col_major(cx, d, tm, tn, t, s);
+    if (rc == TSG_OK) rc = download_tiles(t, B, true, s);
+    cx.pool.release_all_live();
+    return rc;
+}
+
+int tsg_tilespgemm(tsg_smatrix *A, tsg_smatrix *B, tsg_smatrix *C, unsigned int *bmA, unsigned int *bmB,
+                   int bmlen, double densityA, double densityB, unsigned long long nnzCub,
+                   unsigned long long *nnzC_computed, double *compression_rate, double *time_tile,
+                   double *gflops_tile, const char *filename, double *time_step1, double *time_step2,
+                   double *time_step3, double *time_malloc, int tm, int tn) {
+    (void)bmA; (void)bmB; (void)bmlen; (void)densityA; (void)densityB; (void)filename;
+    if (!A || !B || !C || !valid_tiles(tm, tn)) return TSG_ERR_INVALID;
+    if (!tile_size_supported(tm, tn)) return TSG_ERR_UNSUPPORTED;
+    if (A->n != B->m || !A->tile_ptr || !B->tile_ptr) return TSG_ERR_INVALID;
+    tsg_context *c;
+    TSG_TRY(default_ctx(&c));
+    Context &cx = c->cx;
+    hipStream_t s = 0;
+    tsg_dev_tiles dA, dB, dC;
+    TSG_TRY(upload_tiles(cx, A, tm, tn, false, dA, s));
+    TSG_TRY(upload_tiles(cx, B, tn, tm, true, dB, s));
+    TSG_HIP(hipStreamSynchronize(s));
+    tsg_stats st{};
+    auto h0 = std::chrono::steady_clock::now();
+    int rc = dev_tilespgemm(cx, dA, dB, dC, &st, s, cx.ev);
+    if (rc == TSG_OK) TSG_HIP(hipStreamSynchronize(s));
+    auto h1 = std::chrono::steady_clock::now();
+    if (rc == TSG_OK) rc = dev_tiles_finalize_c(cx, dC, s);
+    if (rc == TSG_OK) {
+        memset(C, 0, sizeof(*C));
+        C->m = dC.m; C->n = dC.n; C->nnz = dC.nnz;
+        rc = download_tiles(dC, C, false, s);
+    }
+    cx.pool.release_all_live();
+    if (rc != TSG_OK) return rc;
+    const double t1 = ev_ms(cx.ev[0], cx.ev[1]), t2 = ev_ms(cx.ev[1], cx.ev[2]), t3 = ev_ms(cx.ev[2], cx.ev[3]);
+    const double tk = std::chrono::duration<double, std::milli>(h1 - h0).count();
+    if (time_step1) *time_step1 = t1;
+    if (time_step2) *time_step2 = t2;
+    if (time_step3) *time_step3 = t3;
+    if (time_malloc) *time_malloc = tk - (t1 + t2 + t3) > 0 ? tk - (t1 + t2 + t3) : 0.0;
+    if (time_tile) *time_tile = tk;
+    if (nnzC_computed) *nnzC_computed = (unsigned long long)C->nnz;
+    if (compression_rate) *compression_rate = C->nnz ? (double)nnzCub / (double)C->nnz : 0.0;
+    if (gflops_tile) *gflops_tile = tk > 0 ? 2.0 * (double)nnzCub / (tk * 1e6) : 0.0;
+    if (!quiet()) {
+        printf("step1 ---------------------- Runtime is  %.2f ms-------------------------\n", t1);
+        printf("step2 ---------------------- Runtime is  %.2f ms-------------------------\n", t2);
+        printf("step3 ---------------------- Runtime is  %.2f ms------------------------\n", t3);
+        printf("Non-empty tiles of C = %i\n", C->numtile);
+        printf("nnzC = %i\n", C->nnz);
+        printf("CUDA  TileSpGEMM runtime is %4.2f ms, gflops = %4.2f\n", tk,
+               tk > 0 ? 2.0 * (double)nnzCub / (tk * 1e6) : 0.0);
+    }
+    return TSG_OK;
+}
+
+int tsg_tile2csr(tsg_smatrix *C, int tm, int tn) {
+    (void)tn;
+    if (!C || !C->tile_ptr || !valid_tiles(tm, tm)) return TSG_ERR_INVALID;
+    if (!tile_size_supported(tm, tm)) return TSG_ERR_UNSUPPORTED;
+    tsg_context *c;
+    TSG_TRY(default_ctx(&c));
+    Context &cx = c->cx;
+    hipStream_t s = 0;
+    tsg_dev_tiles t;
+    tsg_dev_csr d;
+    TSG_TRY(upload_tiles(cx, C, tm, tm, false, t, s));
+    int rc = dev_tile2csr(cx, t, d, s);
+    if (rc == TSG_OK) {
+        free(C->rowpointer); free(C->columnindex); free(C->value);
+        rc = download(&C->rowpointer, d.rowpointer, (size_t)C->m + 1, s);
+        if (rc == TSG_OK) rc = download(&C->columnindex, d.columnindex, (size_t)d.nnz, s);
+        if (rc == TSG_OK) rc = download(&C->value, d.value, (size_t)d.nnz, s);
+        if (rc == TSG_OK && hipStreamSynchronize(s) != hipSuccess) rc = TSG_ERR_HIP;
+        C->nnz = d.nnz;
+    }
+    cx.pool.release_all_live();
+    return rc;
+}
+
+// ---- device-resident API
+int tsg_context_create(int device, tsg_context **ctx) {
+    if (!ctx) return TSG_ERR_INVALID;
+    TSG_TRY(check_device());
+    tsg_context *c = new tsg_context();
+    int rc = c->cx.init(device);
+    if (rc != TSG_OK) {
+        delete c;
+        return rc;
+    }
+    *ctx = c;
+    return TSG_OK;
+}
+
+int tsg_context_destroy(tsg_context *ctx) {
+    if (!ctx) return TSG_ERR_INVALID;
+    ctx->cx.destroy();
+    delete ctx;
+    return TSG_OK;
+}
+
+int tsg_context_reset(tsg_context *ctx) {
+    if (!ctx) return TSG_ERR_INVALID;
+    ctx->cx.pool.release_all_live();
+    return TSG_OK;
+}
+
+int tsg_dev_malloc(tsg_context *ctx, void **ptr, size_t bytes) {
+    if (!ctx || !ptr) return TSG_ERR_INVALID;
+    return ctx->cx.pool.alloc(ptr, bytes);
+}
+
+int tsg_dev_free(tsg_context *ctx, void *ptr) {
+    if (!ctx) return TSG_ERR_INVALID;
+    ctx->cx.pool.release(ptr);
+    return TSG_OK;
+}
+
+int tsg_memcpy_h2d(tsg_context *ctx, void *dst, const void *src, size_t bytes, void *stream) {
+    (void)ctx;
+    TSG_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
+    TSG_HIP(hipStreamSynchronize((hipStream_t)stream));
+    return TSG_OK;
+}
+
+int tsg_memcpy_d2h(tsg_context *ctx, void *dst, const void *src, size_t bytes, void *stream) {
+    (void)ctx;
+    TSG_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
+    TSG_HIP(hipStreamSynchronize((hipStream_t)stream));
+    return TSG_OK;
+}
+
+int tsg_memcpy_d2d(tsg_context *ctx, void *dst, const void *src, size_t bytes, void *stream) {
+    (void)ctx;
+    TSG_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    TSG_HIP(hipStreamSynchronize((hipStream_t)stream));
+    return TSG_OK;
+}
+
+int tsg_dev_csr2tile_row_major(tsg_context *ctx, const tsg_dev_csr *A, int tm, int tn, void *stream,
+                               tsg_dev_tiles *out) {
+    if (!ctx || !A || !out || !valid_tiles(tm, tn)) return TSG_ERR_INVALID;
+    return dev_csr2tile_row_major(ctx->cx, *A, tm, tn, *out, (hipStream_t)stream);
+}
+
+int tsg_dev_csr2tile_col_major(tsg_context *ctx, const tsg_dev_csr *B, int tm, int tn, void *stream,
+                               tsg_dev_tiles *out) {
+    if (!ctx || !B || !out || !valid_tiles(tm, tn)) return TSG_ERR_INVALID;
+    return dev_csr2tile_col_major(ctx->cx, *B, tm, tn, *out, (hipStream_t)stream);
+}
+
+int tsg_dev_tilespgemm(tsg_context *ctx, const tsg_dev_tiles *A, const tsg_dev_tiles *B, void *stream,
+                       tsg_dev_tiles *C, tsg_stats *stats) {
+    if (!ctx || !A || !B || !C) return TSG_ERR_INVALID;
+    if (!B->tile_rm2csc) return TSG_ERR_INVALID;
+    return dev_tilespgemm(ctx->cx, *A, *B, *C, stats, (hipStream_t)stream, nullptr);
+}
+
+int tsg_dev_tile2csr(tsg_context *ctx, const tsg_dev_tiles *C, void *stream, tsg_dev_csr *out) {
+    if (!ctx || !C || !out) return TSG_ERR_INVALID;
+    return dev_tile2csr(ctx->cx, *C, *out, (hipStream_t)stream);
+}
+
+int tsg_dev_transpose(tsg_context *ctx, const tsg_dev_csr *A, void *stream, tsg_dev_csr *out) {
+    if (!ctx || !A || !out) return TSG_ERR_INVALID;
+    return dev_transpose(ctx->cx, *A, *out, (hipStream_t)stream);
+}
+
+static void release_tiles(Context &cx, tsg_dev_tiles &t) {
+    void *ps[] = {t.tile_ptr, t.tile_columnidx, t.tile_rowidx, t.tile_nnz, t.tile_csr_Ptr,
+                  t.tile_csr_Col, t.tile_csr_Value, t.mask, t.csc_tile_ptr, t.csc_tile_rowidx,
+                  t.tile_rm2csc};
+    for (void *p : ps) cx.put(p);
+    t = tsg_dev_tiles{};
+}
+
+int tsg_dev_spgemm(tsg_context *ctx, const tsg_dev_csr *A, const tsg_dev_csr *B, int tm, int tn,
+                   void *stream, tsg_dev_csr *C, tsg_stats *stats) {
+    if (!ctx || !A || !B || !C || !valid_tiles(tm, tn) || A->n != B->m) return TSG_ERR_INVALID;
+    if (!tile_size_supported(tm, tn)) return TSG_ERR_UNSUPPORTED;
+    Context &cx = ctx->cx;
+    hipStream_t s = (hipStream_t)stream;
+    tsg_stats st{};
+    tsg_dev_tiles tA, tB, tC;
+    auto h0 = std::chrono::steady_clock::now();
+    TSG_HIP(hipEventRecord(cx.ev[8], s));
+    TSG_TRY(dev_csr2tile_row_major(cx, *A, tm, tn, tA, s));
+    TSG_TRY(dev_csr2tile_col_major(cx, *B, tm, tn, tB, s));
+    TSG_HIP(hipEventRecord(cx.ev[9], s));
+    TSG_TRY(dev_tilespgemm(cx, tA, tB, tC, &st, s, cx.ev));
+    TSG_TRY(dev_tile2csr(cx, tC, *C, s));
+    TSG_HIP(hipEventRecord(cx.ev[10], s));
+    TSG_HIP(hipEventSynchronize(cx.ev[10]));
+    auto h1 = std::chrono::steady_clock::now();
+    st.numtileA = tA.numtile;
+    st.numtileB = tB.numtile;
+    st.t_csr2tile_ms = ev_ms(cx.ev[8], cx.ev[9]);
+    st.t_step1_ms = ev_ms(cx.ev[0], cx.ev[1]);
+    st.t_step2_ms = ev_ms(cx.ev[1], cx.ev[2]);
+    st.t_step3_ms = ev_ms(cx.ev[2], cx.ev[3]);
+    st.t_tile2csr_ms = ev_ms(cx.ev[3], cx.ev[10]);
+    st.t_kern_ms = ev_ms(cx.ev[0], cx.ev[3]);
+    st.t_e2e_ms = std::chrono::duration<double, std::milli>(h1 - h0).count();
+    st.t_malloc_ms = st.t_e2e_ms - ev_ms(cx.ev[8], cx.ev[10]);
+    if (st.t_malloc_ms < 0) st.t_malloc_ms = 0;
+    release_tiles(cx, tA);
+    release_tiles(cx, tB);
+    release_tiles(cx, tC);
+    if (stats) *stats = st;
+    return TSG_OK;
+}
+
+int tsg_spgemm_csr(const tsg_smatrix *A, const tsg_smatrix *B, tsg_smatrix *C, int tm, int tn,
+                   tsg_stats *stats) {
+    if (!A || !B || !C || A->n != B->m || !valid_tiles(tm, tn)) return TSG_ERR_INVALID;
+    if (!tile_size_supported(tm, tn)) return TSG_ERR_UNSUPPORTED;
+    tsg_context *c;
+    TSG_TRY(default_ctx(&c));
+    Context &cx = c->cx;
+    hipStream_t s = 0;
+    tsg_dev_csr dA, dB, dC;
+    TSG_TRY(upload_csr(cx, A, dA, s));
+    TSG_TRY(upload_csr(cx, B, dB, s));
+    TSG_HIP(hipStreamSynchronize(s));
+    int rc = tsg_dev_spgemm(c, &dA, &dB, tm, tn, s, &dC, stats);
+    if (rc == TSG_OK) {
+        memset(C, 0, sizeof(*C));
+        C->m = dC.m; C->n = dC.n; C->nnz = dC.nnz;
+        rc = download(&C->rowpointer, dC.rowpointer, (size_t)dC.m + 1, s);
+        if (rc == TSG_OK) rc = download(&C->columnindex, dC.columnindex, (size_t)dC.nnz, s);
+        if (rc == TSG_OK) rc = download(&C->value, dC.value, (size_t)dC.nnz, s);
+        if (rc == TSG_OK && hipStreamSynchronize(s) != hipSuccess) rc = TSG_ERR_HIP;
+    }
+    cx.pool.release_all_live();
+    return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,1282 @@
+// tsg_device.hip -- hand-written gfx950 (CDNA4, wave64) kernels of the TileSpGEMM
+// hot path, plus their stream-ordered host launchers.
+//
+// Pipeline (reference semantics in brackets, paths under /root/reference/src):
+//   csr2tile A     [csr2tile.h:205-277]   keys -> segmented sort per tile row -> count -> scan -> fill
+//   csr2tile B     [csr2tile.h:279-506]   same per B tile row + tile-level transpose into CSC tile order
+//   step 1         [tilespgemm-cuda.h:279-392, nsparse :1171-1438]
+//                  C tile structure: per (A tile row, column window) an LDS bitmask SPA
+//   step 2         [tilespgemm-cuda.h:394-773]
+//                  per C-tile-row chunk: LDS row masks OR-ed from B tile masks (ds_or_b32),
+//                  popcount -> tile nnz / Ptr; device-wide scan of tile nnz [:2598-2604]
+//   step 3         [tilespgemm-cuda.h:1273-2218]
+//                  per C-tile-row chunk: LDS fp64 accumulator addressed by mask popcount rank
+//                  (ds_add_f64), coalesced write of Val/Col
+//   tile2csr       [tile2csr.h:72-140]    wave per C tile row, 16 wave scans per 64 tiles
+//
+// Row-wise (Gustavson over tiles) instead of the reference's per-C-tile set
+// intersection: every (A tile, B tile) product of a C tile row is enumerated once
+// per chunk with a load-balanced expansion across the 256-thread workgroup.
+#include "tsg_internal.h"
+
+#include <cstdio>
+
+namespace tsg {
+
+typedef unsigned long long u64;
+typedef unsigned int u32;
+typedef unsigned short u16;
+
+constexpr int WG = 256;
+constexpr int WAVES = WG / 64;
+
+// ---------------------------------------------------------------------------
+// wave / workgroup primitives
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <class T> __device__ __forceinline__ T wave_incl_scan(T x) {
+    const int l = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        T y = __shfl_up(x, d, 64);
+        if (l >= d) x += y;
+    }
+    return x;
+}
+
+__device__ __forceinline__ int wave_incl_max(int x) {
+    const int l = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        int y = __shfl_up(x, d, 64);
+        if (l >= d) x = max(x, y);
+    }
+    return x;
+}
+
+template <class T> __device__ __forceinline__ T wave_sum(T x) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) x += __shfl_xor(x, d, 64);
+    return x;
+}
+
+// exclusive scan across the 256-thread workgroup; red needs WAVES entries
+template <class T> __device__ __forceinline__ T block_excl_scan(T x, T *total, T *red) {
+    T inc = wave_incl_scan(x);
+    if (lane_id() == 63) red[wave_id()] = inc;
+    __syncthreads();
+    T off = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) {
+        T v = red[w];
+        off += (w < wave_id()) ? v : T(0);
+        tot += v;
+    }
+    __syncthreads();
+    *total = tot;
+    return off + inc - x;
+}
+
+template <class T> __device__ __forceinline__ T block_sum(T x, T *red) {
+    x = wave_sum(x);
+    if (lane_id() == 0) red[wave_id()] = x;
+    __syncthreads();
+    T tot = 0;
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) tot += red[w];
+    __syncthreads();
+    return tot;
+}
+
+// first index in [lo,hi) with a[idx] >= key
+template <class T>
+__device__ __forceinline__ int lower_bound_dev(const T *a, int lo, int hi, T key) {
+    while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (a[mid] < key) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+static inline int grid_for(long work, int per_block, int cap) {
+    long g = (work + per_block - 1) / per_block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (int)g;
+}
+
+// ---------------------------------------------------------------------------
+// device-wide exclusive scan (reduce -> scan partials -> apply), in place
+// ---------------------------------------------------------------------------
+constexpr int SCAN_ITEMS = 16;
+constexpr int SCAN_TILE = WG * SCAN_ITEMS;  // 4096 elements per block
+__device__ __forceinline__ int scan_pad(int i) { return i + (i >> 4); }
+
+template <class T> __global__ __launch_bounds__(WG) void k_scan_reduce(const T *a, long n, T *part) {
+    __shared__ T red[WAVES];
+    long base = (long)blockIdx.x * SCAN_TILE;
+    T s = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        long i = base + k * WG + threadIdx.x;
+        if (i < n) s += a[i];
+    }
+    T tot = block_sum(s, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+template <class T>
+__global__ __launch_bounds__(WG) void k_scan_apply(T *a, long n, const T *part) {
+    __shared__ T tile[SCAN_TILE + SCAN_TILE / 16];
+    __shared__ T red[WAVES];
+    long base = (long)blockIdx.x * SCAN_TILE;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        int li = k * WG + threadIdx.x;
+        long i = base + li;
+        tile[scan_pad(li)] = (i < n) ? a[i] : T(0);
+    }
+    __syncthreads();
+    T s = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) s += tile[scan_pad(threadIdx.x * SCAN_ITEMS + k)];
+    T tot;
+    T off = block_excl_scan(s, &tot, red) + (part ? part[blockIdx.x] : T(0));
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        int li = scan_pad(threadIdx.x * SCAN_ITEMS + k);
+        T v = tile[li];
+        tile[li] = off;
+        off += v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        int li = k * WG + threadIdx.x;
+        long i = base + li;
+        if (i < n) a[i] = tile[scan_pad(li)];
+    }
+}
+
+template <class T> static int scan_exclusive(Context &cx, T *a, long n, hipStream_t s) {
+    if (n <= 0) return TSG_OK;
+    long nb = (n + SCAN_TILE - 1) / SCAN_TILE;
+    if (nb == 1) {
+        k_scan_apply<T><<<1, WG, 0, s>>>(a, n, nullptr);
+        TSG_HIP(hipGetLastError());
+        return TSG_OK;
+    }
+    T *part = nullptr;
+    TSG_TRY(cx.get(&part, nb));
+    k_scan_reduce<T><<<(unsigned)nb, WG, 0, s>>>(a, n, part);
+    TSG_HIP(hipGetLastError());
+    TSG_TRY(scan_exclusive(cx, part, nb, s));
+    k_scan_apply<T><<<(unsigned)nb, WG, 0, s>>>(a, n, part);
+    TSG_HIP(hipGetLastError());
+    cx.put(part);
+    return TSG_OK;
+}
+
+int scan_exclusive_i32(Context &cx, int *a, long n, hipStream_t s) { return scan_exclusive(cx, a, n, s); }
+int scan_exclusive_i64(Context &cx, long long *a, long n, hipStream_t s) {
+    return scan_exclusive(cx, a, n, s);
+}
+
+// ---------------------------------------------------------------------------
+// segmented sort of u64 keys (keys unique inside a segment for the >4096 tier)
+//   tier 1: len <= 16    one thread, insertion sort in LDS
+//   tier 2: len <= 512   one wave, bitonic network in its LDS slice
+//   tier 3: len <= 4096  one workgroup, bitonic network in LDS
+//   tier 4: len  > 4096  one workgroup: 4096-chunks sorted in LDS, then each key
+//                        placed by its rank (sum of lower_bounds over the chunks)
+// ---------------------------------------------------------------------------
+constexpr int SORT_T1 = 16, SORT_T2 = 512, SORT_T3 = 4096;
+
+__global__ __launch_bounds__(WG) void k_sort_classify(const int *seg, int nseg, int *lists, int *counts) {
+    for (int i = blockIdx.x * WG + threadIdx.x; i < nseg; i += gridDim.x * WG) {
+        int len = seg[i + 1] - seg[i];
+        if (len <= 1) continue;
+        int tier = len <= SORT_T1 ? 0 : len <= SORT_T2 ? 1 : len <= SORT_T3 ? 2 : 3;
+        int pos = atomicAdd(&counts[tier], 1);
+        lists[(long)tier * nseg + pos] = i;
+    }
+}
+
+__global__ __launch_bounds__(WG) void k_sort_t1(u64 *keys, const int *seg, const int *list, const int *count) {
+    __shared__ u64 buf[WG * SORT_T1];
+    const int n = *count;
+    u64 *my = buf + threadIdx.x * SORT_T1;
+    for (int j = blockIdx.x * WG + threadIdx.x; j < n; j += gridDim.x * WG) {
+        int i = list[j];
+        int s = seg[i], len = seg[i + 1] - s;
+        for (int q = 0; q < len; ++q) {
+            u64 k = keys[s + q];
+            int r = q - 1;
+            while (r >= 0 && my[r] > k) { my[r + 1] = my[r]; --r; }
+            my[r + 1] = k;
+        }
+        for (int q = 0; q < len; ++q) keys[s + q] = my[q];
+    }
+}
+
+__device__ __forceinline__ void bitonic_step(u64 *s, int P, int k, int j, int t0, int tstride) {
+    for (int t = t0; t < (P >> 1); t += tstride) {
+        int i = 2 * t - (t & (j - 1));
+        int l = i + j;
+        bool up = (i & k) == 0;
+        u64 a = s[i], b = s[l];
+        if ((a > b) == up) { s[i] = b; s[l] = a; }
+    }
+}
+
+__global__ __launch_bounds__(WG) void k_sort_t2(u64 *keys, const int *seg, const int *list, const int *count) {
+    __shared__ u64 buf[WAVES * SORT_T2];
+    const int n = *count;
+    const int lane = lane_id();
+    u64 *s = buf + wave_id() * SORT_T2;
+    const int gw = (blockIdx.x * WG + threadIdx.x) >> 6, nw = gridDim.x * WAVES;
+    for (int j = gw; j < n; j += nw) {
+        int i = list[j];
+        int st = seg[i], len = seg[i + 1] - st;
+        int P = 64;
+        while (P < len) P <<= 1;
+        for (int q = lane; q < P; q += 64) s[q] = q < len ? keys[st + q] : ~0ull;
+        wave_lds_sync();
+        for (int k = 2; k <= P; k <<= 1)
+            for (int jj = k >> 1; jj > 0; jj >>= 1) {
+                bitonic_step(s, P, k, jj, lane, 64);
+                wave_lds_sync();
+            }
+        for (int q = lane; q < len; q += 64) keys[st + q] = s[q];
+        wave_lds_sync();
+    }
+}
+
+__device__ void block_bitonic_sort(u64 *s, int P) {
+    for (int k = 2; k <= P; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            bitonic_step(s, P, k, j, threadIdx.x, WG);
+            __syncthreads();
+        }
+}
+
+__global__ __launch_bounds__(WG) void k_sort_t3(u64 *keys, const int *seg, const int *list, const int *count) {
+    __shared__ u64 s[SORT_T3];
+    const int n = *count;
+    for (int j = blockIdx.x; j < n; j += gridDim.x) {
+        int i = list[j];
+        int st = seg[i], len = seg[i + 1] - st;
+        int P = 64;
+        while (P < len) P <<= 1;
+        for (int q = threadIdx.x; q < P; q += WG) s[q] = q < len ? keys[st + q] : ~0ull;
+        __syncthreads();
+        block_bitonic_sort(s, P);
+        for (int q = threadIdx.x; q < len; q += WG) keys[st + q] = s[q];
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(WG) void k_sort_t4(u64 *keys, u64 *tmp, const int *seg, const int *list,
+                                                const int *count) {
+    __shared__ u64 s[SORT_T3];
+    const int n = *count;
+    for (int j = blockIdx.x; j < n; j += gridDim.x) {
+        int i = list[j];
+        int st = seg[i], len = seg[i + 1] - st;
+        int nch = (len + SORT_T3 - 1) / SORT_T3;
+        for (int c = 0; c < nch; ++c) {
+            int cs = st + c * SORT_T3, cl = min(SORT_T3, len - c * SORT_T3);
+            for (int q = threadIdx.x; q < SORT_T3; q += WG) s[q] = q < cl ? keys[cs + q] : ~0ull;
+            __syncthreads();
+            block_bitonic_sort(s, SORT_T3);
+            for (int q = threadIdx.x; q < cl; q += WG) keys[cs + q] = s[q];
+            __syncthreads();
+        }
+        __threadfence_block();
+        __syncthreads();
+        for (int q = threadIdx.x; q < len; q += WG) {
+            u64 k = keys[st + q];
+            int own = q / SORT_T3;
+            long rank = q - own * SORT_T3;
+            for (int c = 0; c < nch; ++c) {
+                if (c == own) continue;
+                int cs = st + c * SORT_T3, cl = min(SORT_T3, len - c * SORT_T3);
+                rank += lower_bound_dev(keys + cs, 0, cl, k);
+            }
+            tmp[st + rank] = k;
+        }
+        __syncthreads();
+        for (int q = threadIdx.x; q < len; q += WG) keys[st + q] = tmp[st + q];
+        __syncthreads();
+    }
+}
+
+int segmented_sort_u64(Context &cx, u64 *keys, const int *seg, int nseg, long total, hipStream_t s) {
+    if (nseg <= 0 || total <= 1) return TSG_OK;
+    int *lists = nullptr, *counts = nullptr;
+    u64 *tmp = nullptr;
+    TSG_TRY(cx.get(&lists, (size_t)4 * nseg));
+    TSG_TRY(cx.get(&counts, 4));
+    TSG_TRY(cx.get(&tmp, (size_t)total));
+    TSG_HIP(hipMemsetAsync(counts, 0, 4 * sizeof(int), s));
+    k_sort_classify<<<grid_for(nseg, WG, 4096), WG, 0, s>>>(seg, nseg, lists, counts);
+    k_sort_t1<<<grid_for(nseg, WG, 2048), WG, 0, s>>>(keys, seg, lists, counts);
+    k_sort_t2<<<grid_for(nseg, WAVES, 2048), WG, 0, s>>>(keys, seg, lists + nseg, counts + 1);
+    k_sort_t3<<<grid_for(nseg, 1, 1024), WG, 0, s>>>(keys, seg, lists + 2L * nseg, counts + 2);
+    k_sort_t4<<<grid_for(nseg, 1, 512), WG, 0, s>>>(keys, tmp, seg, lists + 3L * nseg, counts + 3);
+    TSG_HIP(hipGetLastError());
+    cx.put(lists);
+    cx.put(counts);
+    cx.put(tmp);
+    return TSG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// small utility kernels
+// ---------------------------------------------------------------------------
+__global__ void k_strided_starts(const int *rowptr, int m, int stride, int nseg, int *seg) {
+    for (int i = blockIdx.x * WG + threadIdx.x; i <= nseg; i += gridDim.x * WG)
+        seg[i] = rowptr[min((long)i * stride, (long)m)];
+}
+
+__global__ void k_set_i32(int *p, int v) { *p = v; }
+
+__global__ __launch_bounds__(WG) void k_nnzcub(const int *colA, long nnzA, const int *rowptrB,
+                                               u64 *out) {
+    __shared__ u64 red[WAVES];
+    u64 s = 0;
+    for (long p = (long)blockIdx.x * WG + threadIdx.x; p < nnzA; p += (long)gridDim.x * WG) {
+        int k = colA[p];
+        s += (u64)(rowptrB[k + 1] - rowptrB[k]);
+    }
+    s = block_sum(s, red);
+    if (threadIdx.x == 0 && s) atomicAdd(out, s);
+}
+
+int launch_nnzcub(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, u64 *d_out, hipStream_t s) {
+    (void)cx;
+    TSG_HIP(hipMemsetAsync(d_out, 0, sizeof(u64), s));
+    if (A.nnz > 0)
+        k_nnzcub<<<grid_for(A.nnz, WG * 8, 4096), WG, 0, s>>>(A.columnindex, A.nnz, B.rowpointer, d_out);
+    TSG_HIP(hipGetLastError());
+    return TSG_OK;
+}
+
+int read_i32(Context &cx, const int *d, int *h, hipStream_t s) {
+    TSG_HIP(hipMemcpyAsync(cx.pinned, d, sizeof(int), hipMemcpyDeviceToHost, s));
+    TSG_HIP(hipStreamSynchronize(s));
+    *h = cx.pinned[0];
+    return TSG_OK;
+}
+
+int read_i64(Context &cx, const long long *d, long long *h, hipStream_t s) {
+    TSG_HIP(hipMemcpyAsync(cx.pinned64, d, sizeof(long long), hipMemcpyDeviceToHost, s));
+    TSG_HIP(hipStreamSynchronize(s));
+    *h = cx.pinned64[0];
+    return TSG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// stable CSR transpose (matrix_transposition, src/utils.h:161-198):
+// column histogram -> scan -> unordered scatter of (row<<32 | pos) -> per-column
+// segmented sort restores the row-ordered (stable) insertion order.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(WG) void k_colcount(const int *col, long nnz, int *cnt) {
+    for (long p = (long)blockIdx.x * WG + threadIdx.x; p < nnz; p += (long)gridDim.x * WG)
+        atomicAdd(&cnt[col[p]], 1);
+}
+
+__global__ __launch_bounds__(WG) void k_scatter_rows(const int *rowptr, const int *col, int m,
+                                                     const int *colptr, int *fill, u64 *keys) {
+    for (int r = blockIdx.x * WG + threadIdx.x; r < m; r += gridDim.x * WG)
+        for (int p = rowptr[r]; p < rowptr[r + 1]; ++p) {
+            int c = col[p];
+            int slot = colptr[c] + atomicAdd(&fill[c], 1);
+            keys[slot] = ((u64)(u32)r << 32) | (u32)p;
+        }
+}
+
+__global__ __launch_bounds__(WG) void k_transpose_finish(const u64 *keys, long nnz, const double *val,
+                                                         int *rowidx, double *oval) {
+    for (long q = (long)blockIdx.x * WG + threadIdx.x; q < nnz; q += (long)gridDim.x * WG) {
+        u64 k = keys[q];
+        rowidx[q] = (int)(k >> 32);
+        if (val) oval[q] = val[(u32)k];
+    }
+}
+
+int dev_transpose(Context &cx, const tsg_dev_csr &A, tsg_dev_csr &out, hipStream_t s) {
+    out.m = A.n;
+    out.n = A.m;
+    out.nnz = A.nnz;
+    TSG_TRY(cx.get(&out.rowpointer, (size_t)A.n + 1));
+    TSG_TRY(cx.get(&out.columnindex, (size_t)A.nnz + 1));
+    TSG_TRY(cx.get(&out.value, (size_t)A.nnz + 1));
+    int *fill = nullptr;
+    u64 *keys = nullptr;
+    TSG_TRY(cx.get(&fill, (size_t)A.n + 1));
+    TSG_TRY(cx.get(&keys, (size_t)A.nnz + 1));
+    TSG_HIP(hipMemsetAsync(out.rowpointer, 0, ((size_t)A.n + 1) * sizeof(int), s));
+    TSG_HIP(hipMemsetAsync(fill, 0, ((size_t)A.n + 1) * sizeof(int), s));
+    if (A.nnz > 0)
+        k_colcount<<<grid_for(A.nnz, WG * 4, 8192), WG, 0, s>>>(A.columnindex, A.nnz, out.rowpointer);
+    TSG_TRY(scan_exclusive_i32(cx, out.rowpointer, (long)A.n + 1, s));
+    if (A.m > 0)
+        k_scatter_rows<<<grid_for(A.m, WG, 8192), WG, 0, s>>>(A.rowpointer, A.columnindex, A.m,
+                                                              out.rowpointer, fill, keys);
+    TSG_TRY(segmented_sort_u64(cx, keys, out.rowpointer, A.n, A.nnz, s));
+    if (A.nnz > 0)
+        k_transpose_finish<<<grid_for(A.nnz, WG * 4, 8192), WG, 0, s>>>(keys, A.nnz, A.value,
+                                                                        out.columnindex, out.value);
+    TSG_HIP(hipGetLastError());
+    cx.put(fill);
+    cx.put(keys);
+    return TSG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// csr2tile.  Sort key of an entry inside its tile row (TR CSR rows):
+//   tc:26 | lr:6 | lc:6 | lpos:26
+// A (row-major payload, csr2tile.h:152-192): lc = 0 -> order (tc, lr, CSR pos)
+// B (per-tile transposed payload, csr2tile.h:390-484): order (tc, lr, lc, CSR pos)
+// The sorted order IS the payload order inside each tile row.
+// ---------------------------------------------------------------------------
+constexpr int K_TC = 38, K_LR = 32, K_LC = 26;
+constexpr u64 LPOS_MASK = (1ull << 26) - 1;
+__device__ __forceinline__ u32 key_tc(u64 k) { return (u32)(k >> K_TC); }
+__device__ __forceinline__ int key_lr(u64 k) { return (int)((k >> K_LR) & 63); }
+__device__ __forceinline__ int key_lpos(u64 k) { return (int)(k & LPOS_MASK); }
+
+template <int TR, int TC, bool WITH_LC>
+__global__ __launch_bounds__(WG) void k_c2t_keys(const int *rowptr, const int *col, int m, u64 *keys) {
+    for (int R = blockIdx.x * WG + threadIdx.x; R < m; R += gridDim.x * WG) {
+        int i = R / TR;
+        int rs = rowptr[i * TR];
+        u64 lr = (u64)(R - i * TR);
+        for (int p = rowptr[R]; p < rowptr[R + 1]; ++p) {
+            int c = col[p];
+            u64 tc = (u64)(c / TC);
+            u64 lc = WITH_LC ? (u64)(c % TC) : 0ull;
+            keys[p] = (tc << K_TC) | (lr << K_LR) | (lc << K_LC) | (u64)(p - rs);
+        }
+    }
+}
+
+// number of distinct tile columns per tile row (wave per tile row)
+__global__ __launch_bounds__(WG) void k_c2t_count(const u64 *keys, const int *seg, int nseg, int *U) {
+    const int lane = lane_id();
+    const int gw = (blockIdx.x * WG + threadIdx.x) >> 6, nw = gridDim.x * WAVES;
+    for (int i = gw; i < nseg; i += nw) {
+        int s = seg[i], e = seg[i + 1];
+        int cnt = 0;
+        for (int base = s; base < e; base += 64) {
+            int p = base + lane;
+            bool in = p < e;
+            u32 tc = in ? key_tc(keys[p]) : 0u;
+            u32 tcp = (in && p > s) ? key_tc(keys[p - 1]) : 0xffffffffu;
+            cnt += __popcll(__ballot(in && tc != tcp));
+        }
+        if (lane == 0) U[i] = cnt;
+    }
+}
+
+enum { FILL_A = 0, FILL_B_STRUCT = 1, FILL_B_PAYLOAD = 2 };
+
+// Wave per tile row.  TR = rows per tile (Ptr entries per tile), TC = cols per
+// tile (TC/16 mask words per row).  Writes tiles of this tile row directly at
+// their final positions:
+//   FILL_A:         tile_columnidx/rowidx/nnz(start) + Ptr + Col(r*TC+c) + Val + mask
+//   FILL_B_STRUCT:  row-major tile_columnidx/rowidx + per-tile nnz (row-major order)
+//   FILL_B_PAYLOAD: CSC-ordered Ptr + Col(c) + Val + mask (tile id via rm2csc)
+template <int TR, int TC, int MODE>
+__global__ __launch_bounds__(WG) void k_c2t_fill(const u64 *keys, const int *seg, int nseg, const int *col,
+                                                 const double *val, const int *tile_ptr, int *tcol,
+                                                 int *trow, int *tnnz, u16 *Ptr, u16 *Col, double *Val,
+                                                 u16 *mask, const int *rm2csc, const int *csc_nnz) {
+    constexpr int MW = TC / 16;
+    const int lane = lane_id();
+    const int gw = (blockIdx.x * WG + threadIdx.x) >> 6, nw = gridDim.x * WAVES;
+    for (int i = gw; i < nseg; i += nw) {
+        const int s = seg[i], e = seg[i + 1];
+        const int tbase = tile_ptr[i];
+        int carry_u = -1, carry_first = -1;
+        for (int base = s; base < e; base += 64) {
+            const int p = base + lane;
+            const bool in = p < e;
+            u64 k = in ? keys[p] : 0ull;
+            u64 kp = (in && p > s) ? keys[p - 1] : 0ull;
+            u64 kn = (in && p + 1 < e) ? keys[p + 1] : 0ull;
+            const u32 tc = key_tc(k);
+            const int lr = key_lr(k);
+            const bool nt = in && (p == s || key_tc(kp) != tc);
+            const bool te = in && (p + 1 == e || key_tc(kn) != tc);
+            const bool gs = in && (nt || key_lr(kp) != lr);
+            int u = carry_u + wave_incl_scan(nt ? 1 : 0);
+            int f = max(wave_incl_max(nt ? p : -1), carry_first);
+            carry_u = __shfl(u, 63, 64);
+            carry_first = __shfl(f, 63, 64);
+            if (!in) continue;
+            const int trm = tbase + u;
+            if (MODE == FILL_B_STRUCT) {
+                if (nt) { tcol[trm] = (int)tc; trow[trm] = i; }
+                if (te) tnnz[trm] = p - f + 1;
+                continue;
+            }
+            const int t = (MODE == FILL_B_PAYLOAD) ? rm2csc[trm] : trm;
+            const int src = s + key_lpos(k);
+            const int c = col[src];
+            const int lc = c % TC;
+            const int dst = (MODE == FILL_B_PAYLOAD) ? csc_nnz[t] + (p - f) : p;
+            Col[dst] = (MODE == FILL_A) ? (u16)(lr * TC + lc) : (u16)lc;
+            Val[dst] = val[src];
+            if (MODE == FILL_A && nt) {
+                tcol[t] = (int)tc;
+                trow[t] = i;
+                tnnz[t] = p;
+            }
+            u16 *Pt = Ptr + (size_t)t * TR;
+            u16 *Mt = mask + (size_t)t * TR * MW;
+            if (gs) {
+                const int rprev = nt ? -1 : key_lr(kp);
+                for (int rr = rprev + 1; rr <= lr; ++rr) Pt[rr] = (u16)(p - f);
+                for (int rr = rprev + 1; rr < lr; ++rr)
+                    for (int w = 0; w < MW; ++w) Mt[rr * MW + w] = 0;
+                u16 mw[MW];
+                for (int w = 0; w < MW; ++w) mw[w] = 0;
+                for (int q = p; q < e; ++q) {
+                    u64 kq = keys[q];
+                    if (key_tc(kq) != tc || key_lr(kq) != lr) break;
+                    int lcq = col[s + key_lpos(kq)] % TC;
+                    mw[lcq >> 4] |= (u16)(1u << (15 - (lcq & 15)));
+                }
+                for (int w = 0; w < MW; ++w) Mt[lr * MW + w] = mw[w];
+            }
+            if (te) {
+                for (int rr = lr + 1; rr < TR; ++rr) {
+                    Pt[rr] = (u16)(p - f + 1);
+                    for (int w = 0; w < MW; ++w) Mt[rr * MW + w] = 0;
+                }
+            }
+        }
+    }
+}
+
+// tile-level transpose of B's row-major tiles into CSC tile order
+__global__ __launch_bounds__(WG) void k_tiles_colcount(const int *tcol, int numtile, int *cnt) {
+    for (int t = blockIdx.x * WG + threadIdx.x; t < numtile; t += gridDim.x * WG) atomicAdd(&cnt[tcol[t]], 1);
+}
+
+__global__ __launch_bounds__(WG) void k_tiles_scatter(const int *tcol, const int *trow, int numtile,
+                                                      const int *cptr, int *fill, u64 *keys) {
+    for (int t = blockIdx.x * WG + threadIdx.x; t < numtile; t += gridDim.x * WG) {
+        int c = tcol[t];
+        int slot = cptr[c] + atomicAdd(&fill[c], 1);
+        keys[slot] = ((u64)(u32)trow[t] << 32) | (u32)t;
+    }
+}
+
+__global__ __launch_bounds__(WG) void k_tiles_finish(const u64 *keys, int numtile, int *csc_rowidx,
+                                                     int *rm2csc, const int *nnz_rm, int *nnz_csc) {
+    for (int q = blockIdx.x * WG + threadIdx.x; q < numtile; q += gridDim.x * WG) {
+        u64 k = keys[q];
+        int t = (int)(u32)k;
+        csc_rowidx[q] = (int)(k >> 32);
+        rm2csc[t] = q;
+        nnz_csc[q] = nnz_rm[t];
+    }
+}
+
+template <int TR, int TC>
+static int csr2tile_impl(Context &cx, const tsg_dev_csr &M, bool colmajor, tsg_dev_tiles &out,
+                         hipStream_t s) {
+    const int m = M.m, n = M.n, nnz = M.nnz;
+    const int tilem = (m + TR - 1) / TR, tilen = (n + TC - 1) / TC;
+    if ((long)tilen >= (1L << 26)) return TSG_ERR_UNSUPPORTED;
+    out = tsg_dev_tiles{};
+    out.m = m; out.n = n; out.nnz = nnz;
+    out.tile_m = TR; out.tile_n = TC;
+    out.tilem = tilem; out.tilen = tilen;
+    int *seg = nullptr, *U = nullptr;
+    u64 *keys = nullptr;
+    TSG_TRY(cx.get(&seg, (size_t)tilem + 1));
+    TSG_TRY(cx.get(&keys, (size_t)nnz + 1));
+    TSG_TRY(cx.get(&out.tile_ptr, (size_t)tilem + 1));
+    k_strided_starts<<<grid_for(tilem + 1, WG, 4096), WG, 0, s>>>(M.rowpointer, m, TR, tilem, seg);
+    if (m > 0) {
+        if (colmajor)
+            k_c2t_keys<TR, TC, true><<<grid_for(m, WG, 8192), WG, 0, s>>>(M.rowpointer, M.columnindex, m, keys);
+        else
+            k_c2t_keys<TR, TC, false><<<grid_for(m, WG, 8192), WG, 0, s>>>(M.rowpointer, M.columnindex, m, keys);
+    }
+    TSG_HIP(hipGetLastError());
+    TSG_TRY(segmented_sort_u64(cx, keys, seg, tilem, nnz, s));
+    U = out.tile_ptr;
+    TSG_HIP(hipMemsetAsync(U, 0, ((size_t)tilem + 1) * sizeof(int), s));
+    k_c2t_count<<<grid_for(tilem, WAVES, 8192), WG, 0, s>>>(keys, seg, tilem, U);
+    TSG_HIP(hipGetLastError());
+    TSG_TRY(scan_exclusive_i32(cx, out.tile_ptr, (long)tilem + 1, s));
+    int numtile = 0;
+    TSG_TRY(read_i32(cx, out.tile_ptr + tilem, &numtile, s));
+    out.numtile = numtile;
+    const size_t nt1 = (size_t)numtile + 1;
+    TSG_TRY(cx.get(&out.tile_columnidx, nt1));
+    TSG_TRY(cx.get(&out.tile_rowidx, nt1));
+    TSG_TRY(cx.get(&out.tile_nnz, nt1));
+    TSG_TRY(cx.get(&out.tile_csr_Ptr, nt1 * TR));
+    TSG_TRY(cx.get(&out.tile_csr_Col, (size_t)nnz + 1));
+    TSG_TRY(cx.get(&out.tile_csr_Value, (size_t)nnz + 1));
+    TSG_TRY(cx.get(&out.mask, nt1 * TR * (TC / 16)));
+    const int gfill = grid_for(tilem, WAVES, 8192);
+    if (!colmajor) {
+        k_c2t_fill<TR, TC, FILL_A><<<gfill, WG, 0, s>>>(keys, seg, tilem, M.columnindex, M.value, out.tile_ptr,
+                                                       out.tile_columnidx, out.tile_rowidx, out.tile_nnz,
+                                                       out.tile_csr_Ptr, out.tile_csr_Col, out.tile_csr_Value,
+                                                       out.mask, nullptr, nullptr);
+        k_set_i32<<<1, 1, 0, s>>>(out.tile_nnz + numtile, nnz);
+        TSG_HIP(hipGetLastError());
+    } else {
+        int *nnz_rm = nullptr, *fill = nullptr;
+        u64 *tkeys = nullptr;
+        TSG_TRY(cx.get(&nnz_rm, nt1));
+        TSG_TRY(cx.get(&fill, (size_t)tilen + 1));
+        TSG_TRY(cx.get(&tkeys, nt1));
+        TSG_TRY(cx.get(&out.csc_tile_ptr, (size_t)tilen + 1));
+        TSG_TRY(cx.get(&out.csc_tile_rowidx, nt1));
+        TSG_TRY(cx.get(&out.tile_rm2csc, nt1));
+        k_c2t_fill<TR, TC, FILL_B_STRUCT><<<gfill, WG, 0, s>>>(keys, seg, tilem, M.columnindex, M.value,
+                                                              out.tile_ptr, out.tile_columnidx, out.tile_rowidx,
+                                                              nnz_rm, nullptr, nullptr, nullptr, nullptr,
+                                                              nullptr, nullptr);
+        TSG_HIP(hipMemsetAsync(out.csc_tile_ptr, 0, ((size_t)tilen + 1) * sizeof(int), s));
+        TSG_HIP(hipMemsetAsync(fill, 0, ((size_t)tilen + 1) * sizeof(int), s));
+        if (numtile > 0)
+            k_tiles_colcount<<<grid_for(numtile, WG, 8192), WG, 0, s>>>(out.tile_columnidx, numtile,
+                                                                      out.csc_tile_ptr);
+        TSG_TRY(scan_exclusive_i32(cx, out.csc_tile_ptr, (long)tilen + 1, s));
+        if (numtile > 0)
+            k_tiles_scatter<<<grid_for(numtile, WG, 8192), WG, 0, s>>>(out.tile_columnidx, out.tile_rowidx,
+                                                                     numtile, out.csc_tile_ptr, fill, tkeys);
+        TSG_TRY(segmented_sort_u64(cx, tkeys, out.csc_tile_ptr, tilen, numtile, s));
+        if (numtile > 0)
+            k_tiles_finish<<<grid_for(numtile, WG, 8192), WG, 0, s>>>(tkeys, numtile, out.csc_tile_rowidx,
+                                                                    out.tile_rm2csc, nnz_rm, out.tile_nnz);
+        k_set_i32<<<1, 1, 0, s>>>(out.tile_nnz + numtile, 0);
+        TSG_TRY(scan_exclusive_i32(cx, out.tile_nnz, (long)numtile + 1, s));
+        k_c2t_fill<TR, TC, FILL_B_PAYLOAD><<<gfill, WG, 0, s>>>(keys, seg, tilem, M.columnindex, M.value,
+                                                               out.tile_ptr, nullptr, nullptr, nullptr,
+                                                               out.tile_csr_Ptr, out.tile_csr_Col,
+                                                               out.tile_csr_Value, out.mask, out.tile_rm2csc,
+                                                               out.tile_nnz);
+        TSG_HIP(hipGetLastError());
+        cx.put(nnz_rm);
+        cx.put(fill);
+        cx.put(tkeys);
+    }
+    cx.put(seg);
+    cx.put(keys);
+    return TSG_OK;
+}
+
+bool tile_size_supported(int tm, int tn) { return tm == 16 && tn == 16; }
+
+int dev_csr2tile_row_major(Context &cx, const tsg_dev_csr &A, int tm, int tn, tsg_dev_tiles &out,
+                           hipStream_t s) {
+    if (!tile_size_supported(tm, tn)) return TSG_ERR_UNSUPPORTED;
+    return csr2tile_impl<16, 16>(cx, A, false, out, s);
+}
+
+int dev_csr2tile_col_major(Context &cx, const tsg_dev_csr &B, int tm, int tn, tsg_dev_tiles &out,
+                           hipStream_t s) {
+    if (!tile_size_supported(tm, tn)) return TSG_ERR_UNSUPPORTED;
+    // B tiles are tn rows x tm cols
+    return csr2tile_impl<16, 16>(cx, B, true, out, s);
+}
+
+// ---------------------------------------------------------------------------
+// product enumeration: every (A tile a, B tile b) with a in A tile row [a0,a1)
+// and b in B tile row colA[a] whose tile column lies in [clo, chi].  Items are
+// spread over the 256 threads by an LDS exclusive scan of per-A-tile counts.
+// ---------------------------------------------------------------------------
+struct ProdLds {
+    int bs[WG];
+    int off[WG + 1];
+    int red[WAVES];
+};
+
+template <class F>
+__device__ __forceinline__ long for_each_product(int a0, int a1, const int *colA, const int *bptr,
+                                                 const int *bcol, int clo, int chi, bool narrow,
+                                                 ProdLds &L, F &&f) {
+    long items = 0;
+    for (int ab = a0; ab < a1; ab += WG) {
+        const int a = ab + threadIdx.x;
+        int bs = 0, len = 0;
+        if (a < a1) {
+            int k = colA[a];
+            bs = bptr[k];
+            int be = bptr[k + 1];
+            if (narrow) {
+                bs = lower_bound_dev(bcol, bs, be, clo);
+                be = lower_bound_dev(bcol, bs, be, chi + 1);
+            }
+            len = be - bs;
+        }
+        int tot;
+        int off = block_excl_scan(len, &tot, L.red);
+        L.bs[threadIdx.x] = bs;
+        L.off[threadIdx.x] = off;
+        __syncthreads();
+        const int nA = min(WG, a1 - ab);
+        for (int q = threadIdx.x; q < tot; q += WG) {
+            int lo = 0, hi = nA - 1;
+            while (lo < hi) {
+                int mid = (lo + hi + 1) >> 1;
+                if (L.off[mid] <= q) lo = mid; else hi = mid - 1;
+            }
+            f(ab + lo, L.bs[lo] + (q - L.off[lo]));
+        }
+        items += tot;
+        __syncthreads();
+    }
+    return items;
+}
+
+// ---------------------------------------------------------------------------
+// step 1: C tile structure.  Unit = (A tile row i, window w of `win` B tile
+// columns); an LDS bitmask collects the reachable tile columns.
+//   PASS 0: count per unit (+ tile-product total); PASS 1: emit sorted columns.
+// ---------------------------------------------------------------------------
+constexpr int S1_MAXWORDS = 2048;  // 65536 tile columns per window
+
+template <int PASS>
+__global__ __launch_bounds__(WG) void k_step1(const int *Aptr, const int *Acol, const int *Bptr, const int *Bcol,
+                                              int tilemA, int tilenB, int nwin, int win, int *unit_cnt,
+                                              const int *unit_off, int *Ccol, u64 *prod_total) {
+    __shared__ u32 bm[S1_MAXWORDS];
+    __shared__ ProdLds L;
+    __shared__ int red[WAVES];
+    const int nunits = tilemA * nwin;
+    const int words = win >> 5;
+    const int wpt = words / WG;  // words per thread (win is a multiple of 8192)
+    long my_items = 0;
+    for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
+        const int i = u / nwin, w = u - i * nwin;
+        const int a0 = Aptr[i], a1 = Aptr[i + 1];
+        if (a0 == a1) {
+            if (PASS == 0 && threadIdx.x == 0) unit_cnt[u] = 0;
+            continue;
+        }
+        const int clo = w * win, chi = min(clo + win, tilenB) - 1;
+        for (int q = threadIdx.x; q < words; q += WG) bm[q] = 0u;
+        __syncthreads();
+        long it = for_each_product(a0, a1, Acol, Bptr, Bcol, clo, chi, nwin > 1, L, [&](int a, int b) {
+            (void)a;
+            int c = Bcol[b] - clo;
+            atomicOr(&bm[c >> 5], 1u << (c & 31));
+        });
+        if (PASS == 0) my_items += (threadIdx.x == 0) ? it : 0;
+        int cnt = 0;
+        for (int q = 0; q < wpt; ++q) cnt += __popc(bm[threadIdx.x * wpt + q]);
+        if (PASS == 0) {
+            int tot = block_sum(cnt, red);
+            if (threadIdx.x == 0) unit_cnt[u] = tot;
+        } else {
+            int tot;
+            int off = block_excl_scan(cnt, &tot, red) + unit_off[u];
+            for (int q = 0; q < wpt; ++q) {
+                int wi = threadIdx.x * wpt + q;
+                u32 x = bm[wi];
+                while (x) {
+                    int b = __ffs(x) - 1;
+                    Ccol[off++] = clo + wi * 32 + b;
+                    x &= x - 1;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (PASS == 0 && threadIdx.x == 0 && my_items) atomicAdd(prod_total, (u64)my_items);
+}
+
+__global__ void k_rows_from_units(const int *unit_off, int tilem, int nwin, int *Cptr) {
+    for (int i = blockIdx.x * WG + threadIdx.x; i <= tilem; i += gridDim.x * WG) Cptr[i] = unit_off[(long)i * nwin];
+}
+
+// chunks per C tile row: step 2 by tile count, step 3 by weight (nnz + ALPHA per tile)
+constexpr int S2_CH = 1024;
+constexpr int S3_CAPW = 2048, S3_ALPHA = 8;
+constexpr int S3_MAXT = S3_CAPW / S3_ALPHA + 1;
+constexpr int S3_MAXNZ = S3_CAPW + 256 + 8;
+
+__device__ __forceinline__ long s3_wrel(const int *nnzoff, int t0, int t) {
+    return (long)(nnzoff[t] - nnzoff[t0]) + (long)S3_ALPHA * (t - t0);
+}
+
+template <int STEP>
+__global__ void k_units_per_row(const int *Cptr, const int *nnzoff, int tilem, int *nunits) {
+    for (int i = blockIdx.x * WG + threadIdx.x; i < tilem; i += gridDim.x * WG) {
+        int t0 = Cptr[i], t1 = Cptr[i + 1];
+        int n = 0;
+        if (t1 > t0) {
+            if (STEP == 2) n = (t1 - t0 + S2_CH - 1) / S2_CH;
+            else n = (int)(s3_wrel(nnzoff, t0, t1 - 1) / S3_CAPW) + 1;
+        }
+        nunits[i] = n;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) nunits[tilem] = 0;
+}
+
+__global__ void k_unit_rows(const int *uoff, int tilem, int *urow) {
+    for (int i = blockIdx.x * WG + threadIdx.x; i < tilem; i += gridDim.x * WG)
+        for (int u = uoff[i]; u < uoff[i + 1]; ++u) urow[u] = i;
+}
+
+// ---------------------------------------------------------------------------
+// step 2: per C-tile-row chunk of <= S2_CH tiles, C row masks in LDS
+// ---------------------------------------------------------------------------
+template <int TM, int TN>
+__global__ __launch_bounds__(WG) void k_step2(const int *uoff, const int *urow, int tilem, const int *Aptr,
+                                              const int *Acol, const int *Annz, const u16 *ColA,
+                                              const int *Bptr, const int *Bcol, const int *rm2csc,
+                                              const u16 *maskB, const int *Cptr, const int *Ccol,
+                                              u16 *PtrC, u16 *maskC, int *nnzC) {
+    constexpr int MW = TM / 16;            // mask words per C row (= per B row)
+    constexpr int TW = TM * MW;            // u16 mask words per C tile
+    constexpr int TW32 = (TW + 1) / 2;     // u32 LDS words per C tile
+    __shared__ u32 s_mask[S2_CH * TW32];
+    __shared__ int s_cols[S2_CH];
+    __shared__ ProdLds L;
+    const int nunits = uoff[tilem];
+    for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
+        const int i = urow[u];
+        const int q = u - uoff[i];
+        const int t0 = Cptr[i] + q * S2_CH;
+        const int ns = min(S2_CH, Cptr[i + 1] - t0);
+        for (int j = threadIdx.x; j < ns; j += WG) s_cols[j] = Ccol[t0 + j];
+        for (int j = threadIdx.x; j < ns * TW32; j += WG) s_mask[j] = 0u;
+        __syncthreads();
+        const int clo = s_cols[0], chi = s_cols[ns - 1];
+        for_each_product(Aptr[i], Aptr[i + 1], Acol, Bptr, Bcol, clo, chi, true, L, [&](int a, int b) {
+            const int sidx = lower_bound_dev(s_cols, 0, ns, Bcol[b]);
+            const u16 *mb = maskB + (size_t)rm2csc[b] * TN * MW;
+            u16 *ms16 = reinterpret_cast<u16 *>(s_mask) + (size_t)sidx * TW32 * 2;
+            for (int qa = Annz[a]; qa < Annz[a + 1]; ++qa) {
+                const int enc = ColA[qa];
+                const int r = enc / TN, c = enc - (enc / TN) * TN;
+#pragma unroll
+                for (int w = 0; w < MW; ++w) {
+                    u32 mv = mb[c * MW + w];
+                    if (mv) {
+                        int wi = r * MW + w;  // u16 index inside the tile
+                        u32 *word = reinterpret_cast<u32 *>(ms16) + (wi >> 1);
+                        atomicOr(word, mv << ((wi & 1) * 16));
+                    }
+                }
+            }
+        });
+        for (int j = threadIdx.x; j < ns; j += WG) {
+            const u16 *ms16 = reinterpret_cast<const u16 *>(s_mask) + (size_t)j * TW32 * 2;
+            const int t = t0 + j;
+            int nz = 0;
+            for (int k = 0; k < TW; ++k) nz += __popc((u32)ms16[k]);
+            nnzC[t] = nz;
+            if (nz) {
+                int run = 0;
+                for (int r = 0; r < TM; ++r) {
+                    PtrC[(size_t)t * TM + r] = (u16)run;
+                    for (int w = 0; w < MW; ++w) {
+                        u16 v = ms16[r * MW + w];
+                        maskC[(size_t)t * TW + r * MW + w] = v;
+                        run += __popc((u32)v);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// step 3: numeric.  Chunk = C tiles of one C tile row with total weight
+// (nnz + S3_ALPHA per tile) <= S3_CAPW + one tile.  LDS: tile columns, nnz
+// offsets, row masks, u8 row pointers and the fp64 accumulator of the chunk.
+// Accumulator slot of (tile s, row r, col x) = off[s] + ptr[s][r] + popc(bits<x).
+// ---------------------------------------------------------------------------
+template <int TM>
+__device__ __forceinline__ int mask_rank(const u16 *mrow, int x) {
+    constexpr int MW = TM / 16;
+    int rank = 0;
+#pragma unroll
+    for (int w = 0; w < MW; ++w) {
+        u32 v = mrow[w];
+        if (w < (x >> 4)) rank += __popc(v);
+        else if (w == (x >> 4)) rank += __popc(v >> (16 - (x & 15)));
+    }
+    return rank;
+}
+
+template <int TM, int TN>
+__global__ __launch_bounds__(WG) void k_step3(const int *uoff, const int *urow, int tilem, const int *Aptr,
+                                              const int *Acol, const int *Annz, const u16 *ColA,
+                                              const double *ValA, const int *Bptr, const int *Bcol,
+                                              const int *rm2csc, const int *Bnnz, const u16 *PtrB,
+                                              const u16 *ColB, const double *ValB, const int *Cptr,
+                                              const int *Ccol, const int *nnzoff, const u16 *maskC,
+                                              u16 *ColC, double *ValC) {
+    constexpr int MW = TM / 16;
+    constexpr int TW = TM * MW;
+    __shared__ double acc[S3_MAXNZ];
+    __shared__ u16 s_mask[S3_MAXT * TW];
+    __shared__ int s_cols[S3_MAXT];
+    __shared__ int s_off[S3_MAXT];
+    __shared__ unsigned char s_ptr[S3_MAXT * TM];
+    __shared__ ProdLds L;
+    const int nunits = uoff[tilem];
+    for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
+        const int i = urow[u];
+        const int q = u - uoff[i];
+        const int r0 = Cptr[i], r1 = Cptr[i + 1];
+        // chunk q = tiles t in [r0, r1) with floor(wrel(t)/CAPW) == q
+        int lo = r0, hi = r1;
+        while (lo < hi) {
+            int mid = (lo + hi) >> 1;
+            if (s3_wrel(nnzoff, r0, mid) / S3_CAPW < q) lo = mid + 1; else hi = mid;
+        }
+        const int t0 = lo;
+        hi = r1;
+        while (lo < hi) {
+            int mid = (lo + hi) >> 1;
+            if (s3_wrel(nnzoff, r0, mid) / S3_CAPW < q + 1) lo = mid + 1; else hi = mid;
+        }
+        const int t1 = lo;
+        const int ns = t1 - t0;
+        const int nzbase = nnzoff[t0];
+        const int nz = nnzoff[t1] - nzbase;
+        if (ns <= 0 || nz == 0) continue;  // uniform: nothing to compute in this chunk
+        for (int j = threadIdx.x; j < ns; j += WG) {
+            const int t = t0 + j;
+            s_cols[j] = Ccol[t];
+            const int o = nnzoff[t] - nzbase;
+            s_off[j] = o;
+            const bool ne = nnzoff[t + 1] > nnzoff[t];
+            int run = 0;
+            for (int r = 0; r < TM; ++r) {
+                s_ptr[j * TM + r] = (unsigned char)(run > 255 ? 255 : run);
+                for (int w = 0; w < MW; ++w) {
+                    u16 v = ne ? maskC[(size_t)t * TW + r * MW + w] : (u16)0;
+                    s_mask[j * TW + r * MW + w] = v;
+                    run += __popc((u32)v);
+                }
+            }
+        }
+        for (int j = threadIdx.x; j < nz; j += WG) acc[j] = 0.0;
+        __syncthreads();
+        const int clo = s_cols[0], chi = s_cols[ns - 1];
+        for_each_product(Aptr[i], Aptr[i + 1], Acol, Bptr, Bcol, clo, chi, true, L, [&](int a, int b) {
+            const int sidx = lower_bound_dev(s_cols, 0, ns, Bcol[b]);
+            const int onext = (sidx + 1 < ns) ? s_off[sidx + 1] : nz;
+            if (onext == s_off[sidx]) return;  // structurally empty C tile
+            const int bc = rm2csc[b];
+            const int bb = Bnnz[bc], be = Bnnz[bc + 1];
+            const u16 *bp = PtrB + (size_t)bc * TN;
+            for (int qa = Annz[a]; qa < Annz[a + 1]; ++qa) {
+                const int enc = ColA[qa];
+                const int r = enc / TN, c = enc - (enc / TN) * TN;
+                const double va = ValA[qa];
+                const int ks = bb + bp[c];
+                const int ke = (c == TN - 1) ? be : bb + bp[c + 1];
+                if (ks >= ke) continue;
+                const u16 *mrow = &s_mask[sidx * TW + r * MW];
+                const int rowbase = s_off[sidx] + (TM <= 16 ? (int)s_ptr[sidx * TM + r] : 0);
+                int rb = rowbase;
+                if (TM > 16) {  // u8 pointers saturate above 255: recount
+                    rb = s_off[sidx];
+                    for (int rr = 0; rr < r; ++rr)
+                        for (int w = 0; w < MW; ++w) rb += __popc((u32)s_mask[sidx * TW + rr * MW + w]);
+                }
+                for (int kb = ks; kb < ke; ++kb) {
+                    const int x = ColB[kb];
+                    atomicAdd(&acc[rb + mask_rank<TM>(mrow, x)], va * ValB[kb]);
+                }
+            }
+        });
+        // values: contiguous tile-major run of the chunk
+        for (int j = threadIdx.x; j < nz; j += WG) ValC[nzbase + j] = acc[j];
+        // columns: one (tile,row) per thread, bits expanded in ascending order
+        for (int sr = threadIdx.x; sr < ns * TM; sr += WG) {
+            const int j = sr / TM, r = sr - (sr / TM) * TM;
+            int pos = s_off[j];
+            for (int rr = 0; rr < r; ++rr)
+                for (int w = 0; w < MW; ++w) pos += __popc((u32)s_mask[j * TW + rr * MW + w]);
+            for (int w = 0; w < MW; ++w) {
+                u32 v = s_mask[j * TW + r * MW + w];
+                while (v) {
+                    int bit = 31 - __clz(v);  // highest set bit = lowest column (MSB-first)
+                    ColC[nzbase + pos++] = (u16)(w * 16 + (15 - bit));
+                    v &= ~(1u << bit);
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void k_zero_empty_ptr(const int *nnzoff, int numtile, int tm, u16 *Ptr, u16 *mask) {
+    const int mw = tm / 16;
+    for (long x = (long)blockIdx.x * WG + threadIdx.x; x < (long)numtile * tm; x += (long)gridDim.x * WG) {
+        int t = (int)(x / tm);
+        if (nnzoff[t + 1] == nnzoff[t]) {
+            Ptr[x] = 0;
+            for (int w = 0; w < mw; ++w) mask[x * mw + w] = 0;
+        }
+    }
+}
+
+__global__ void k_crow(const int *Cptr, int tilem, int *Crow) {
+    for (int i = blockIdx.x * WG + threadIdx.x; i < tilem; i += gridDim.x * WG)
+        for (int t = Cptr[i]; t < Cptr[i + 1]; ++t) Crow[t] = i;
+}
+
+int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_dev_tiles &C,
+                   tsg_stats *st, hipStream_t s, hipEvent_t *ev) {
+    constexpr int TM = 16, TN = 16;
+    if (A.tile_m != TM || A.tile_n != TN || B.tile_m != TN || B.tile_n != TM) return TSG_ERR_UNSUPPORTED;
+    if (A.n != B.m) return TSG_ERR_INVALID;
+    const int tilemA = A.tilem, tilenB = B.tilen;
+    C = tsg_dev_tiles{};
+    C.m = A.m; C.n = B.n; C.tile_m = TM; C.tile_n = TM;
+    C.tilem = tilemA; C.tilen = tilenB;
+    if (ev) TSG_HIP(hipEventRecord(ev[0], s));
+    // ---- step 1 ----
+    int win = ((tilenB + 8191) / 8192) * 8192;
+    if (win < 8192) win = 8192;
+    if (win > 65536) win = 65536;
+    const int nwin = (tilenB + win - 1) / win;
+    if ((long)tilemA * nwin >= (1L << 31) - 1) return TSG_ERR_UNSUPPORTED;
+    const long nunits1 = (long)tilemA * nwin;
+    int *ucnt = nullptr;
+    u64 *prod = nullptr;
+    TSG_TRY(cx.get(&ucnt, (size_t)nunits1 + 1));
+    TSG_TRY(cx.get(&prod, 1));
+    TSG_TRY(cx.get(&C.tile_ptr, (size_t)tilemA + 1));
+    TSG_HIP(hipMemsetAsync(prod, 0, sizeof(u64), s));
+    TSG_HIP(hipMemsetAsync(ucnt + nunits1, 0, sizeof(int), s));
+    const int g1 = grid_for(nunits1, 1, 16384);
+    if (tilemA > 0)
+        k_step1<0><<<g1, WG, 0, s>>>(A.tile_ptr, A.tile_columnidx, B.tile_ptr, B.tile_columnidx, tilemA, tilenB,
+                                     nwin, win, ucnt, nullptr, nullptr, prod);
+    TSG_HIP(hipGetLastError());
+    TSG_TRY(scan_exclusive_i32(cx, ucnt, nunits1 + 1, s));
+    k_rows_from_units<<<grid_for(tilemA + 1, WG, 4096), WG, 0, s>>>(ucnt, tilemA, nwin, C.tile_ptr);
+    TSG_HIP(hipMemcpyAsync(cx.pinned64, prod, sizeof(u64), hipMemcpyDeviceToHost, s));
+    int numblkC = 0;
+    TSG_TRY(read_i32(cx, C.tile_ptr + tilemA, &numblkC, s));
+    long long tile_products = cx.pinned64[0];
+    C.numtile = numblkC;
+    const size_t nb1 = (size_t)numblkC + 1;
+    TSG_TRY(cx.get(&C.tile_columnidx, nb1));
+    if (tilemA > 0)
+        k_step1<1><<<g1, WG, 0, s>>>(A.tile_ptr, A.tile_columnidx, B.tile_ptr, B.tile_columnidx, tilemA, tilenB,
+                                     nwin, win, nullptr, ucnt, C.tile_columnidx, nullptr);
+    TSG_HIP(hipGetLastError());
+    cx.put(ucnt);
+    cx.put(prod);
+    if (ev) TSG_HIP(hipEventRecord(ev[1], s));
+    // ---- step 2 ----
+    int *nun = nullptr, *urow = nullptr;
+    const long maxu2 = (long)numblkC / S2_CH + tilemA + 1;
+    TSG_TRY(cx.get(&nun, (size_t)tilemA + 1));
+    TSG_TRY(cx.get(&urow, (size_t)maxu2));
+    TSG_TRY(cx.get(&C.tile_nnz, nb1));
+    TSG_TRY(cx.get(&C.tile_csr_Ptr, nb1 * TM));
+    TSG_TRY(cx.get(&C.mask, nb1 * TM * (TM / 16)));
+    k_units_per_row<2><<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(C.tile_ptr, nullptr, tilemA, nun);
+    TSG_TRY(scan_exclusive_i32(cx, nun, (long)tilemA + 1, s));
+    k_unit_rows<<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(nun, tilemA, urow);
+    k_set_i32<<<1, 1, 0, s>>>(C.tile_nnz + numblkC, 0);
+    TSG_HIP(hipGetLastError());
+    if (numblkC > 0)
+        k_step2<TM, TN><<<grid_for(maxu2, 1, 16384), WG, 0, s>>>(
+            nun, urow, tilemA, A.tile_ptr, A.tile_columnidx, A.tile_nnz, A.tile_csr_Col, B.tile_ptr,
+            B.tile_columnidx, B.tile_rm2csc, B.mask, C.tile_ptr, C.tile_columnidx, C.tile_csr_Ptr, C.mask,
+            C.tile_nnz);
+    TSG_HIP(hipGetLastError());
+    TSG_TRY(scan_exclusive_i32(cx, C.tile_nnz, (long)numblkC + 1, s));
+    int nnzC = 0;
+    TSG_TRY(read_i32(cx, C.tile_nnz + numblkC, &nnzC, s));
+    C.nnz = nnzC;
+    if (ev) TSG_HIP(hipEventRecord(ev[2], s));
+    // ---- step 3 ----
+    const long maxu3 = ((long)nnzC + (long)S3_ALPHA * numblkC) / S3_CAPW + tilemA + 1;
+    int *nun3 = nullptr, *urow3 = nullptr;
+    TSG_TRY(cx.get(&nun3, (size_t)tilemA + 1));
+    TSG_TRY(cx.get(&urow3, (size_t)maxu3));
+    TSG_TRY(cx.get(&C.tile_csr_Col, (size_t)nnzC + 1));
+    TSG_TRY(cx.get(&C.tile_csr_Value, (size_t)nnzC + 1));
+    k_units_per_row<3><<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(C.tile_ptr, C.tile_nnz, tilemA, nun3);
+    TSG_TRY(scan_exclusive_i32(cx, nun3, (long)tilemA + 1, s));
+    k_unit_rows<<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(nun3, tilemA, urow3);
+    TSG_HIP(hipGetLastError());
+    if (nnzC > 0)
+        k_step3<TM, TN><<<grid_for(maxu3, 1, 16384), WG, 0, s>>>(
+            nun3, urow3, tilemA, A.tile_ptr, A.tile_columnidx, A.tile_nnz, A.tile_csr_Col, A.tile_csr_Value,
+            B.tile_ptr, B.tile_columnidx, B.tile_rm2csc, B.tile_nnz, B.tile_csr_Ptr, B.tile_csr_Col,
+            B.tile_csr_Value, C.tile_ptr, C.tile_columnidx, C.tile_nnz, C.mask, C.tile_csr_Col,
+            C.tile_csr_Value);
+    TSG_HIP(hipGetLastError());
+    cx.put(nun);
+    cx.put(urow);
+    cx.put(nun3);
+    cx.put(urow3);
+    if (ev) TSG_HIP(hipEventRecord(ev[3], s));
+    if (st) {
+        st->numblkC = numblkC;
+        st->nnzC = nnzC;
+        st->tile_products = tile_products;
+    }
+    return TSG_OK;
+}
+
+// Reference-layout extras for the host drop-in API: zero Ptr of empty C tiles
+// and fill tile_rowidx (the device pipeline needs neither).
+int dev_tiles_finalize_c(Context &cx, tsg_dev_tiles &C, hipStream_t s) {
+    if (C.numtile <= 0) return TSG_OK;
+    k_zero_empty_ptr<<<grid_for((long)C.numtile * C.tile_m, WG, 8192), WG, 0, s>>>(C.tile_nnz, C.numtile,
+                                                                                  C.tile_m, C.tile_csr_Ptr, C.mask);
+    TSG_TRY(cx.get(&C.tile_rowidx, (size_t)C.numtile + 1));
+    k_crow<<<grid_for(C.tilem, WG, 4096), WG, 0, s>>>(C.tile_ptr, C.tilem, C.tile_rowidx);
+    TSG_HIP(hipGetLastError());
+    return TSG_OK;
+}
+
+// rm2csc for a B tiling that arrives from the host (row-major + CSC structure):
+// CSC position p of tile (ti, j) -> its index in the row-major structure.
+__global__ __launch_bounds__(WG) void k_rm2csc(const int *tile_ptr, const int *tcol, const int *csc_ptr,
+                                               const int *csc_rowidx, int tilen, int numtile, int *rm2csc) {
+    for (int p = blockIdx.x * WG + threadIdx.x; p < numtile; p += gridDim.x * WG) {
+        int lo = 0, hi = tilen;  // last j with csc_ptr[j] <= p
+        while (lo < hi) {
+            int mid = (lo + hi + 1) >> 1;
+            if (csc_ptr[mid] <= p) lo = mid; else hi = mid - 1;
+        }
+        const int j = lo, ti = csc_rowidx[p];
+        const int rm = lower_bound_dev(tcol, tile_ptr[ti], tile_ptr[ti + 1], j);
+        rm2csc[rm] = p;
+    }
+}
+
+int dev_rm2csc_from_structs(Context &cx, tsg_dev_tiles &B, hipStream_t s) {
+    TSG_TRY(cx.get(&B.tile_rm2csc, (size_t)B.numtile + 1));
+    if (B.numtile > 0)
+        k_rm2csc<<<grid_for(B.numtile, WG, 8192), WG, 0, s>>>(B.tile_ptr, B.tile_columnidx, B.csc_tile_ptr,
+                                                             B.csc_tile_rowidx, B.tilen, B.numtile, B.tile_rm2csc);
+    TSG_HIP(hipGetLastError());
+    return TSG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// tile2csr (tile2csr.h:72-140).  Wave per C tile row; lane = tile.  Pass 1 sums
+// per-row counts; pass 2 carries 16 running row offsets across 64-tile chunks.
+// ---------------------------------------------------------------------------
+template <int TM>
+__global__ __launch_bounds__(WG) void k_t2c_count(const int *Cptr, int tilem, int m, const int *nnzoff,
+                                                  const u16 *Ptr, int *rowcnt) {
+    const int lane = lane_id();
+    const int gw = (blockIdx.x * WG + threadIdx.x) >> 6, nw = gridDim.x * WAVES;
+    for (int i = gw; i < tilem; i += nw) {
+        int cnt[TM];
+#pragma unroll
+        for (int r = 0; r < TM; ++r) cnt[r] = 0;
+        for (int base = Cptr[i]; base < Cptr[i + 1]; base += 64) {
+            const int t = base + lane;
+            if (t < Cptr[i + 1]) {
+                const int o0 = nnzoff[t], tnz = nnzoff[t + 1] - o0;
+                if (tnz) {
+                    const u16 *p = Ptr + (size_t)t * TM;
+#pragma unroll
+                    for (int r = 0; r < TM; ++r) {
+                        int nx = (r == TM - 1) ? tnz : (int)p[r + 1];
+                        cnt[r] += nx - (int)p[r];
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < TM; ++r) {
+            int v = wave_sum(cnt[r]);
+            if (lane == r && i * TM + r < m) rowcnt[i * TM + r] = v;
+        }
+    }
+}
+
+template <int TM>
+__global__ __launch_bounds__(WG) void k_t2c_fill(const int *Cptr, const int *Ccol, int tilem, int m,
+                                                 const int *nnzoff, const u16 *Ptr, const u16 *ColC,
+                                                 const double *ValC, const int *rowptr, int *col, double *val) {
+    const int lane = lane_id();
+    const int gw = (blockIdx.x * WG + threadIdx.x) >> 6, nw = gridDim.x * WAVES;
+    for (int i = gw; i < tilem; i += nw) {
+        const int rowlen = min(TM, m - i * TM);
+        int carry[TM];
+#pragma unroll
+        for (int r = 0; r < TM; ++r) carry[r] = 0;
+        for (int base = Cptr[i]; base < Cptr[i + 1]; base += 64) {
+            const int t = base + lane;
+            const bool in = t < Cptr[i + 1];
+            int o0 = 0, tnz = 0;
+            if (in) { o0 = nnzoff[t]; tnz = nnzoff[t + 1] - o0; }
+            if (__ballot(tnz > 0) == 0ull) continue;
+            const u16 *p = Ptr + (size_t)(in ? t : 0) * TM;
+            const int tc = in ? Ccol[t] : 0;
+#pragma unroll
+            for (int r = 0; r < TM; ++r) {
+                int st = tnz ? (int)p[r] : 0;
+                int nx = tnz ? ((r == TM - 1) ? tnz : (int)p[r + 1]) : 0;
+                int c = nx - st;
+                int inc = wave_incl_scan(c);
+                int dst0 = carry[r] + inc - c;
+                carry[r] += __shfl(inc, 63, 64);
+                if (r < rowlen && c > 0) {
+                    const int R = i * TM + r;
+                    int d = rowptr[R] + dst0;
+                    for (int k = 0; k < c; ++k) {
+                        col[d + k] = tc * TM + (int)ColC[o0 + st + k];
+                        val[d + k] = ValC[o0 + st + k];
+                    }
+                }
+            }
+        }
+    }
+}
+
+int dev_tile2csr(Context &cx, const tsg_dev_tiles &C, tsg_dev_csr &out, hipStream_t s) {
+    if (C.tile_m != 16) return TSG_ERR_UNSUPPORTED;
+    out.m = C.m;
+    out.n = C.n;
+    out.nnz = C.nnz;
+    TSG_TRY(cx.get(&out.rowpointer, (size_t)C.m + 1));
+    TSG_TRY(cx.get(&out.columnindex, (size_t)C.nnz + 1));
+    TSG_TRY(cx.get(&out.value, (size_t)C.nnz + 1));
+    TSG_HIP(hipMemsetAsync(out.rowpointer, 0, ((size_t)C.m + 1) * sizeof(int), s));
+    const int g = grid_for(C.tilem, WAVES, 8192);
+    if (C.tilem > 0)
+        k_t2c_count<16><<<g, WG, 0, s>>>(C.tile_ptr, C.tilem, C.m, C.tile_nnz, C.tile_csr_Ptr, out.rowpointer);
+    TSG_HIP(hipGetLastError());
+    TSG_TRY(scan_exclusive_i32(cx, out.rowpointer, (long)C.m + 1, s));
+    if (C.tilem > 0 && C.nnz > 0)
+        k_t2c_fill<16><<<g, WG, 0, s>>>(C.tile_ptr, C.tile_columnidx, C.tilem, C.m, C.tile_nnz, C.tile_csr_Ptr,
+                                        C.tile_csr_Col, C.tile_csr_Value, out.rowpointer, out.columnindex,
+                                        out.value);
+    TSG_HIP(hipGetLastError());
+    return TSG_OK;
+}
+
+}  // namespace tsg

@@ -1,0 +1,97 @@
+// tsg_internal.h -- host-side internals shared by the device code (tsg_device.hip)
+// and the C-ABI layer (tsg_api.cpp).  gfx950 / wave64 only.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <map>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/tsg.h"
+
+namespace tsg {
+
+#define TSG_HIP(call)                                                    \
+    do {                                                                 \
+        hipError_t _e = (call);                                          \
+        if (_e != hipSuccess) {                                          \
+            ::tsg::report_hip_error(_e, #call, __FILE__, __LINE__);      \
+            return (_e == hipErrorOutOfMemory) ? TSG_ERR_OOM : TSG_ERR_HIP; \
+        }                                                                \
+    } while (0)
+
+#define TSG_TRY(call)                   \
+    do {                                \
+        int _rc = (call);               \
+        if (_rc != TSG_OK) return _rc;  \
+    } while (0)
+
+void report_hip_error(hipError_t e, const char *what, const char *file, int line);
+
+// Caching device allocator: power-of-two size classes, blocks return to a free
+// list and are reused by later allocations on the (single) call stream, so the
+// steady-state pipeline performs no hipMalloc.
+class DevicePool {
+  public:
+    ~DevicePool();
+    int alloc(void **p, size_t bytes);
+    void release(void *p);
+    void release_all_live();  // returns every live block to the cache
+    void trim();              // hipFree of the cached blocks
+    size_t bytes_reserved() const { return reserved_; }
+
+  private:
+    std::multimap<size_t, void *> free_;
+    std::unordered_map<void *, size_t> live_;
+    size_t reserved_ = 0;
+};
+
+struct Context {
+    int device = 0;
+    DevicePool pool;
+    int *pinned = nullptr;        // host pinned scratch for size read-backs
+    long long *pinned64 = nullptr;
+    hipEvent_t ev[16];
+    bool ev_ready = false;
+    std::vector<void *> owned;    // outputs handed to the caller (released on reset)
+    int init(int dev);
+    void destroy();
+    template <class T> int get(T **p, size_t count) {
+        void *v = nullptr;
+        int rc = pool.alloc(&v, count * sizeof(T) + 16);
+        *p = static_cast<T *>(v);
+        return rc;
+    }
+    void put(void *p) { if (p) pool.release(p); }
+};
+
+// ---- launchers implemented in tsg_device.hip (all stream-ordered, no sync) ----
+// Exclusive scan in place over n elements (a[n-1] ends up = sum of a[0..n-2]
+// when the caller stored 0 there, i.e. the reference's "n+1 scan" idiom).
+int scan_exclusive_i32(Context &cx, int *a, long n, hipStream_t s);
+int scan_exclusive_i64(Context &cx, long long *a, long n, hipStream_t s);
+// Sort u64 keys ascending inside each segment [seg[i], seg[i+1]) in place.
+int segmented_sort_u64(Context &cx, unsigned long long *keys, const int *seg, int nseg,
+                       long total, hipStream_t s);
+
+int launch_nnzcub(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B,
+                  unsigned long long *d_out, hipStream_t s);
+int dev_transpose(Context &cx, const tsg_dev_csr &A, tsg_dev_csr &out, hipStream_t s);
+int dev_csr2tile_row_major(Context &cx, const tsg_dev_csr &A, int tm, int tn, tsg_dev_tiles &out,
+                           hipStream_t s);
+int dev_csr2tile_col_major(Context &cx, const tsg_dev_csr &B, int tm, int tn, tsg_dev_tiles &out,
+                           hipStream_t s);
+int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_dev_tiles &C,
+                   tsg_stats *st, hipStream_t s, hipEvent_t *ev_marks);
+int dev_tile2csr(Context &cx, const tsg_dev_tiles &C, tsg_dev_csr &out, hipStream_t s);
+
+// read a device int / long long synchronously through pinned memory
+int read_i32(Context &cx, const int *d, int *h, hipStream_t s);
+int read_i64(Context &cx, const long long *d, long long *h, hipStream_t s);
+
+bool tile_size_supported(int tm, int tn);
+
+}  // namespace tsg

@@ -1,0 +1,94 @@
+"""Multi-GPU TileSpGEMM: one process per GPU.
+
+C's tile row i depends only on A's tile row i and all of B, so A is split into
+contiguous blocks of tile rows of equal WORK (prefix sum of the per-tile-row
+intermediate products, the quantity nsparse's set_intprod_num bins on,
+src/spgemm_nsparse_kernel.h:135-151), B is replicated, every rank runs the full
+device pipeline on its block, and the single exchange step is a gather of the
+C row blocks to rank 0 (point-to-point sends over RCCL/xGMI; each peer uses its
+own link into the root, RCCL has no gatherv).  Backend-agnostic: the same code
+runs on gloo (CPU tensors, tests) and nccl (= RCCL on ROCm, GPU tensors).
+"""
+import numpy as np
+
+
+def tile_row_work(rowptr_a, col_a, rowptr_b, m, tile_m):
+    """Element-level intermediate products per A tile row (sum of B row lengths)."""
+    blen = np.diff(rowptr_b.astype(np.int64))
+    per_entry = blen[col_a]
+    per_row = np.add.reduceat(per_entry, rowptr_a[:-1]) if len(per_entry) else np.zeros(m, np.int64)
+    per_row = np.where(np.diff(rowptr_a) > 0, per_row, 0)
+    tilem = (m + tile_m - 1) // tile_m
+    pad = np.zeros(tilem * tile_m, dtype=np.int64)
+    pad[:m] = per_row
+    return pad.reshape(tilem, tile_m).sum(axis=1)
+
+
+def partition_tile_rows(work, world):
+    """Contiguous [begin, end) tile-row ranges of ~equal work (+1 per row so
+    empty rows still spread)."""
+    w = np.asarray(work, dtype=np.float64) + 1.0
+    cum = np.concatenate([[0.0], np.cumsum(w)])
+    bounds = [0]
+    for r in range(1, world):
+        bounds.append(int(np.searchsorted(cum, cum[-1] * r / world, side="left")))
+    bounds.append(len(w))
+    bounds = np.maximum.accumulate(np.array(bounds))
+    return [(int(bounds[r]), int(bounds[r + 1])) for r in range(world)]
+
+
+def slice_rows(m, rowptr, col, val, r0, r1):
+    """Rows [r0, r1) of a CSR as a standalone CSR (row pointers rebased)."""
+    r0, r1 = max(0, min(r0, m)), max(0, min(r1, m))
+    s, e = int(rowptr[r0]), int(rowptr[r1])
+    rp = (rowptr[r0:r1 + 1] - s).astype(np.int32)
+    return r1 - r0, rp, col[s:e], val[s:e]
+
+
+def gather_csr_blocks(rowptr, col, val, rank, world, device=None):
+    """Gather CSR row blocks (torch tensors on `device`) to rank 0.
+
+    Returns (rowptr, col, val) of the concatenated matrix on rank 0, None elsewhere.
+    One all_gather of the per-rank (rows, nnz) counts, then point-to-point
+    sends of each block's arrays into the root's slices."""
+    import torch
+    import torch.distributed as dist
+
+    dev = device if device is not None else rowptr.device
+    counts = torch.tensor([rowptr.numel() - 1, col.numel()], dtype=torch.int64, device=dev)
+    allc = [torch.zeros(2, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(allc, counts)
+    rows = [int(c[0]) for c in allc]
+    nnzs = [int(c[1]) for c in allc]
+    if rank != 0:
+        ops = [dist.P2POp(dist.isend, rowptr.contiguous(), 0)]
+        if nnzs[rank]:
+            ops += [dist.P2POp(dist.isend, col.contiguous(), 0), dist.P2POp(dist.isend, val.contiguous(), 0)]
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+        return None
+    M, NNZ = sum(rows), sum(nnzs)
+    out_rp = torch.zeros(M + 1, dtype=torch.int32, device=dev)
+    out_ci = torch.empty(NNZ, dtype=col.dtype, device=dev)
+    out_v = torch.empty(NNZ, dtype=val.dtype, device=dev)
+    recv_rp = [None] * world
+    ops = []
+    for r in range(1, world):
+        recv_rp[r] = torch.empty(rows[r] + 1, dtype=torch.int32, device=dev)
+        ops.append(dist.P2POp(dist.irecv, recv_rp[r], r))
+        if nnzs[r]:
+            o = sum(nnzs[:r])
+            ops.append(dist.P2POp(dist.irecv, out_ci[o:o + nnzs[r]], r))
+            ops.append(dist.P2POp(dist.irecv, out_v[o:o + nnzs[r]], r))
+    reqs = dist.batch_isend_irecv(ops) if ops else []
+    out_ci[:nnzs[0]] = col
+    out_v[:nnzs[0]] = val
+    recv_rp[0] = rowptr
+    for w in reqs:
+        w.wait()
+    ro, no = 0, 0
+    for r in range(world):
+        out_rp[ro:ro + rows[r] + 1] = recv_rp[r].to(torch.int32) + no
+        ro += rows[r]
+        no += nnzs[r]
+    return out_rp, out_ci, out_v

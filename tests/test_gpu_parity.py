@@ -1,0 +1,192 @@
+"""GPU parity: every stage of the HIP path against the oracle, through the C ABI.
+
+Bar (north_star): C's nnz, row pointers, column pattern and the tiled layouts
+bit-exact; fp64 values within rtol 1e-10 (here exact in practice: with the
+reference's value[k] = k % 10 every product and sum is a small integer).
+The structural oracle is pinned to the reference's own host code by
+tests/test_oracle.py; goldens in tests/golden/ref come from that code.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import _oracle as O
+from conftest import FIXTURES, golden_cases
+from spgemm_amd import synth
+from spgemm_amd import tilespgemm as T
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-10
+TILE_KEYS = ("tile_ptr", "tile_columnidx", "tile_nnz", "tile_csr_Ptr", "tile_csr_Col", "tile_csr_Value", "mask")
+SUPPORTED = {(16, 16)}
+
+
+def g(npz, key):
+    return npz[key.replace(".", "__")]
+
+
+def both(path, aat):
+    """(product A, product B, oracle A, oracle B) for a fixture."""
+    A = T.mmio_allinone(path)
+    T.values_pos_mod10(A)
+    B = T.transpose(A) if aat else T.Matrix.alias(A)
+    oA = O.OMat.load(path)
+    oB = O.transpose(oA) if aat else O.OMat.alias(oA)
+    return A, B, oA, oB
+
+
+def assert_csr_equal(got, ref, values=True):
+    gm, gn, grp, gci, gvv = got
+    rm, rn, rrp, rci, rvv = ref
+    assert (gm, gn) == (rm, rn)
+    np.testing.assert_array_equal(grp, rrp)
+    np.testing.assert_array_equal(gci, rci)
+    if values:
+        np.testing.assert_allclose(gvv, rvv, rtol=RTOL, atol=0)
+
+
+CASES = [c for c in golden_cases() if (c.values[3], c.values[4]) in SUPPORTED]
+
+
+@pytest.mark.parametrize("path,name,aat,tm,tn", CASES)
+def test_pipeline_stages_vs_reference_goldens(path, name, aat, tm, tn):
+    ref = np.load(path)
+    A, B, oA, oB = both(os.path.join(FIXTURES, name + ".mtx"), aat)
+    # GPU transpose (-aat 1) vs the reference's matrix_transposition
+    _, _, brp, bci, bvv = B.csr()
+    np.testing.assert_array_equal(brp, g(ref, "B.rowpointer"))
+    np.testing.assert_array_equal(bci, g(ref, "B.columnindex"))
+    np.testing.assert_array_equal(bvv, g(ref, "B.value"))
+    assert T.nnzcub(A, B) == int(g(ref, "nnzCub"))
+    # GPU csr2tile vs the reference's csr2tile (bit-exact, every field)
+    T.csr2tile_row_major(A, tm, tn)
+    T.csr2tile_col_major(B, tm, tn)
+    at, bt = A.tiles(tm, tn // 16), B.tiles(tn, tm // 16, csc=True)
+    for k in ("tilem", "tilen", "numtile"):
+        assert at[k] == int(g(ref, "At." + k)), k
+        assert bt[k] == int(g(ref, "Bt." + k)), k
+    for k in TILE_KEYS:
+        np.testing.assert_array_equal(at[k], g(ref, "At." + k), err_msg="A " + k)
+        np.testing.assert_array_equal(bt[k], g(ref, "Bt." + k), err_msg="B " + k)
+    np.testing.assert_array_equal(bt["csc_tile_ptr"], g(ref, "Bt.csc_tile_ptr"))
+    np.testing.assert_array_equal(bt["csc_tile_rowidx"], g(ref, "Bt.csc_tile_rowidx"))
+    # GPU steps 1-3 vs oracle tiled C (every field) and the reference step-1 structure
+    Cm, info = T.tilespgemm(A, B, tm, tn, nnzCub=int(g(ref, "nnzCub")))
+    O.csr2tile_row_major(oA, tm, tn)
+    O.csr2tile_col_major(oB, tm, tn)
+    oC = O.tilespgemm(oA, oB, tm, tn)
+    ct, oct_ = Cm.tiles(tm, tm // 16), O.c_tiles(oC, tm)
+    np.testing.assert_array_equal(ct["tile_ptr"], g(ref, "Ct.tile_ptr"))
+    np.testing.assert_array_equal(ct["tile_columnidx"], g(ref, "Ct.tile_columnidx"))
+    assert ct["numtile"] == oct_["numtile"]
+    for k in TILE_KEYS:
+        np.testing.assert_array_equal(ct[k], oct_[k], err_msg="C " + k)
+    assert info["nnzC"] == oC.s.nnz
+    # GPU tile2csr vs the reference SPA pattern + oracle values
+    T.tile2csr(Cm, tm, tm)
+    O.tile2csr(oC, tm, tm)
+    got = Cm.csr()
+    np.testing.assert_array_equal(got[2], g(ref, "C.rowpointer"))
+    np.testing.assert_array_equal(got[3], g(ref, "C.columnindex"))
+    assert_csr_equal(got, oC.csr())
+
+
+@pytest.mark.parametrize("path,name,aat,tm,tn", CASES)
+def test_one_shot_spgemm_vs_oracle(path, name, aat, tm, tn):
+    A, B, oA, oB = both(os.path.join(FIXTURES, name + ".mtx"), aat)
+    Cm, st = T.spgemm(A, B, tm, tn)
+    ref = O.gustavson(oA, oB)
+    assert_csr_equal(Cm.csr(), ref.csr())
+    assert st["nnzC"] == ref.s.nnz
+
+
+def _synthetic_cases():
+    out = []
+    for (m, n, d, uns, dup) in [(1, 1, 1.0, False, False), (17, 17, 0.2, False, False),
+                                (300, 300, 0.02, False, False), (1000, 1000, 0.004, True, False),
+                                (999, 999, 0.01, False, True), (2048, 2048, 0.002, True, True),
+                                (513, 513, 0.3, False, False)]:
+        out.append(pytest.param(m, n, d, uns, dup, id=f"rand{m}x{n}_d{d}_u{int(uns)}_dup{int(dup)}"))
+    return out
+
+
+@pytest.mark.parametrize("m,n,density,unsorted,dups", _synthetic_cases())
+def test_random_matrices_tiled_and_csr(m, n, density, unsorted, dups):
+    mm, nn, rp, ci, vv = synth.random_csr(m, n, density=density, seed=7 + m, unsorted=unsorted, dups=dups)
+    A = T.Matrix.from_csr(mm, nn, rp, ci, vv)
+    B = T.Matrix.alias(A)
+    oA = O.OMat.from_csr(mm, nn, rp, ci, vv)
+    oB = O.OMat.alias(oA)
+    T.csr2tile_row_major(A, 16, 16)
+    T.csr2tile_col_major(B, 16, 16)
+    O.csr2tile_row_major(oA, 16, 16)
+    O.csr2tile_col_major(oB, 16, 16)
+    at, oat = A.tiles(16, 1), oA.tiles(16, 1)
+    bt, obt = B.tiles(16, 1, csc=True), oB.tiles(16, 1, csc=True)
+    for k in TILE_KEYS:
+        np.testing.assert_array_equal(at[k], oat[k], err_msg="A " + k)
+        np.testing.assert_array_equal(bt[k], obt[k], err_msg="B " + k)
+    Cm, _ = T.tilespgemm(A, B, 16, 16)
+    oC = O.tilespgemm(oA, oB, 16, 16)
+    ct, oct_ = Cm.tiles(16, 1), O.c_tiles(oC, 16)
+    for k in TILE_KEYS:
+        np.testing.assert_array_equal(ct[k], oct_[k], err_msg="C " + k)
+    T.tile2csr(Cm, 16, 16)
+    ref = O.gustavson(oA, oB)
+    assert_csr_equal(Cm.csr(), ref.csr())
+
+
+def test_aat_rectangular_and_empty():
+    # A*A^T of a wide matrix with empty rows, and an all-empty matrix
+    mm, nn, rp, ci, vv = synth.random_csr(130, 777, density=0.01, seed=3)
+    A = T.Matrix.from_csr(mm, nn, rp, ci, vv)
+    B = T.transpose(A)
+    oA = O.OMat.from_csr(mm, nn, rp, ci, vv)
+    oB = O.transpose(oA)
+    assert_csr_equal(B.csr(), oB.csr())
+    Cm, _ = T.spgemm(A, B)
+    assert_csr_equal(Cm.csr(), O.gustavson(oA, oB).csr())
+    E = T.Matrix.from_csr(40, 40, np.zeros(41, np.int32), np.zeros(0, np.int32), np.zeros(0))
+    Ce, st = T.spgemm(E, T.Matrix.alias(E))
+    m, n, rp, ci, vv = Ce.csr()
+    assert (m, n) == (40, 40) and rp.sum() == 0 and len(ci) == 0 and st["nnzC"] == 0
+
+
+@pytest.mark.parametrize("name", ["cant", "mc2depi", "webbase"])
+def test_full_size_synthetic_vs_oracle(name):
+    """BASELINE configs at full size (synthetic stand-ins): pattern bit-exact,
+    values exact, against the numeric Gustavson oracle."""
+    m, n, rp, ci, vv = synth.GENERATORS[name]()
+    A = T.Matrix.from_csr(m, n, rp, ci, vv)
+    if name == "mc2depi":  # config 3 is C = A*A^T
+        B = T.transpose(A)
+        oA = O.OMat.from_csr(m, n, rp, ci, vv)
+        oB = O.transpose(oA)
+    else:
+        B = T.Matrix.alias(A)
+        oA = O.OMat.from_csr(m, n, rp, ci, vv)
+        oB = O.OMat.alias(oA)
+    Cm, st = T.spgemm(A, B)
+    ref = O.gustavson(oA, oB)
+    assert_csr_equal(Cm.csr(), ref.csr())
+    assert st["nnzC"] == ref.s.nnz
+
+
+def test_device_api_matches_host_api():
+    import torch
+    from spgemm_amd.device import Context, DeviceCSR
+    m, n, rp, ci, vv = synth.random_csr(3000, 3000, density=0.003, seed=11)
+    ctx = Context(0)
+    dA = DeviceCSR.from_host(m, n, rp, ci, vv)
+    c, st = ctx.spgemm(dA, dA)
+    got = ctx.to_host(c)
+    torch.cuda.synchronize()
+    oA = O.OMat.from_csr(m, n, rp, ci, vv)
+    assert_csr_equal(got, O.gustavson(oA, O.OMat.alias(oA)).csr())
+    # repeated calls reuse the cached pool and stay exact
+    for _ in range(3):
+        ctx.reset()
+        c2, _ = ctx.spgemm(dA, dA)
+        assert_csr_equal(ctx.to_host(c2), got)
+    ctx.close()

@@ -1,0 +1,90 @@
+"""CPU-side checks of the product library (no compute call needs a GPU here):
+the C ABI library builds for gfx950, loads, exports every symbol include/tsg.h
+declares, refuses to run without a device (no CPU fallback), and its host-only
+Matrix-Market reader reproduces mmio_allinone's CSR order (pinned through the
+oracle on the reference fixtures)."""
+import ctypes as C
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from conftest import FIXTURES
+import _oracle as O
+from spgemm_amd import _lib
+from spgemm_amd import tilespgemm as T
+
+
+@pytest.fixture(scope="module")
+def L():
+    if not os.path.exists(_lib.LIB_PATH):
+        _lib.build()
+    return _lib.lib()
+
+
+def test_exports_every_header_symbol(L):
+    syms = _lib.header_symbols()
+    assert len(syms) >= 25
+    for s in syms:
+        assert hasattr(L, s), f"libtsg.so does not export {s}"
+
+
+def test_code_object_is_gfx950():
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+    assert b"gfx90a" not in data and b"gfx942" not in data
+
+
+def test_status_strings(L):
+    assert L.tsg_status_string(0) == b"ok"
+    assert b"device" in L.tsg_status_string(-5)
+    assert L.tsg_version().startswith(b"tsg-mi355x")
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="GPU present")
+def test_fails_loudly_without_device(L):
+    A = T.Matrix.from_csr(2, 2, [0, 1, 2], [0, 1], [1.0, 2.0])
+    with pytest.raises(_lib.TsgError) as ei:
+        T.csr2tile_row_major(A, 16, 16)
+    assert ei.value.rc == -5
+    with pytest.raises(_lib.TsgError):
+        T.spgemm(A, T.Matrix.alias(A))
+
+
+def test_invalid_tile_size_rejected(L):
+    A = T.Matrix.from_csr(2, 2, [0, 1, 2], [0, 1], [1.0, 2.0])
+    for tm, tn in [(8, 16), (16, 24), (0, 16), (128, 16)]:
+        with pytest.raises(_lib.TsgError) as ei:
+            T.csr2tile_row_major(A, tm, tn)
+        assert ei.value.rc == -1
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(FIXTURES, "*.mtx"))),
+                         ids=lambda p: os.path.basename(p))
+def test_mmio_reader_matches_oracle(L, path):
+    A = T.mmio_allinone(path)
+    T.values_pos_mod10(A)
+    ref = O.OMat.load(path)
+    m, n, rp, ci, vv = A.csr()
+    om, on, orp, oci, ovv = ref.csr()
+    assert (m, n) == (om, on)
+    assert A.s.isSymmetric == ref.s.isSymmetric
+    np.testing.assert_array_equal(rp, orp)
+    np.testing.assert_array_equal(ci, oci)
+    np.testing.assert_array_equal(vv, ovv)
+
+
+def test_mmio_reader_errors(L, tmp_path):
+    bad = tmp_path / "bad.mtx"
+    bad.write_text("%%MatrixMarket matrix array real general\n2 2\n1\n2\n3\n4\n")
+    with pytest.raises(_lib.TsgError) as ei:
+        T.mmio_allinone(str(bad))
+    assert ei.value.rc == -6
+    with pytest.raises(_lib.TsgError) as ei:
+        T.mmio_allinone(str(tmp_path / "missing.mtx"))
+    assert ei.value.rc == -7
+    oob = tmp_path / "oob.mtx"
+    oob.write_text("%%MatrixMarket matrix coordinate real general\n2 2 1\n3 1 1.0\n")
+    with pytest.raises(_lib.TsgError):
+        T.mmio_allinone(str(oob))
