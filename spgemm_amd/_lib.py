@@ -127,6 +127,14 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"libtsg.so not built ({LIB_PATH}); run spgemm_amd._lib.build() "
                               "or `make -C spgemm_amd/csrc`")
+        # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64.so.7.
+        # Loading torch first makes libtsg.so's NEEDED libamdhip64.so.7 resolve to
+        # that already-loaded copy; the other order would put two runtimes (and
+        # two device views) in the process and torch then sees no GPU.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         for name, (args, res) in _SIGS.items():
             fn = getattr(L, name)
