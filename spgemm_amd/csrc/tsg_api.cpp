@@ -205,7 +205,7 @@ static int download_tiles(const tsg_dev_tiles &t, tsg_smatrix *M, bool csc, hipS
     TSG_TRY(download(&M->tile_csr_Ptr, t.tile_csr_Ptr, nt * t.tile_m, s));
     TSG_TRY(download(&M->tile_csr_Col, t.tile_csr_Col, (size_t)t.nnz, s));
     TSG_TRY(download(&M->tile_csr_Value, t.tile_csr_Value, (size_t)t.nnz, s));
-    TSG_TRY(download(&M->mask, t.mask, nt * t.tile_m * (t.tile_n / 16), s));
+    if (t.mask) TSG_TRY(download(&M->mask, t.mask, nt * t.tile_m * (t.tile_n / 16), s));
     if (csc) {
         TSG_TRY(download(&M->csc_tile_ptr, t.csc_tile_ptr, (size_t)t.tilen + 1, s));
         TSG_TRY(download(&M->csc_tile_rowidx, t.csc_tile_rowidx, nt, s));
@@ -227,7 +227,7 @@ static int upload_tiles(Context &cx, const tsg_smatrix *M, int tile_m, int tile_
     TSG_TRY(upload(cx, &t.tile_csr_Ptr, M->tile_csr_Ptr, nt * tile_m, s));
     TSG_TRY(upload(cx, &t.tile_csr_Col, M->tile_csr_Col, (size_t)M->nnz, s));
     TSG_TRY(upload(cx, &t.tile_csr_Value, M->tile_csr_Value, (size_t)M->nnz, s));
-    TSG_TRY(upload(cx, &t.mask, M->mask, nt * tile_m * (tile_n / 16), s));
+    if (M->mask) TSG_TRY(upload(cx, &t.mask, M->mask, nt * tile_m * (tile_n / 16), s));
     if (csc) {
         if (!M->csc_tile_ptr || !M->csc_tile_rowidx) return TSG_ERR_INVALID;
         TSG_TRY(upload(cx, &t.csc_tile_ptr, M->csc_tile_ptr, (size_t)M->tilen + 1, s));
@@ -452,7 +452,7 @@ int tsg_tilespgemm(tsg_smatrix *A, tsg_smatrix *B, tsg_smatrix *C, unsigned int 
     (void)bmA; (void)bmB; (void)bmlen; (void)densityA; (void)densityB; (void)filename;
     if (!A || !B || !C || !valid_tiles(tm, tn)) return TSG_ERR_INVALID;
     if (!tile_size_supported(tm, tn)) return TSG_ERR_UNSUPPORTED;
-    if (A->n != B->m || !A->tile_ptr || !B->tile_ptr) return TSG_ERR_INVALID;
+    if (A->n != B->m || !A->tile_ptr || !B->tile_ptr || !B->mask || !B->csc_tile_ptr) return TSG_ERR_INVALID;
     tsg_context *c;
     TSG_TRY(default_ctx(&c));
     Context &cx = c->cx;
@@ -463,7 +463,7 @@ int tsg_tilespgemm(tsg_smatrix *A, tsg_smatrix *B, tsg_smatrix *C, unsigned int 
     TSG_HIP(hipStreamSynchronize(s));
     tsg_stats st{};
     auto h0 = std::chrono::steady_clock::now();
-    int rc = dev_tilespgemm(cx, dA, dB, dC, &st, s, cx.ev);
+    int rc = dev_tilespgemm(cx, dA, dB, dC, &st, s, cx.ev, nullptr);
     if (rc == TSG_OK) TSG_HIP(hipStreamSynchronize(s));
     auto h1 = std::chrono::steady_clock::now();
     if (rc == TSG_OK) rc = dev_tiles_finalize_c(cx, dC, s);
@@ -595,7 +595,7 @@ int tsg_dev_tilespgemm(tsg_context *ctx, const tsg_dev_tiles *A, const tsg_dev_t
                        tsg_dev_tiles *C, tsg_stats *stats) {
     if (!ctx || !A || !B || !C) return TSG_ERR_INVALID;
     if (!B->tile_rm2csc) return TSG_ERR_INVALID;
-    return dev_tilespgemm(ctx->cx, *A, *B, *C, stats, (hipStream_t)stream, nullptr);
+    return dev_tilespgemm(ctx->cx, *A, *B, *C, stats, (hipStream_t)stream, nullptr, nullptr);
 }
 
 int tsg_dev_tile2csr(tsg_context *ctx, const tsg_dev_tiles *C, void *stream, tsg_dev_csr *out) {
@@ -629,8 +629,8 @@ int tsg_dev_spgemm(tsg_context *ctx, const tsg_dev_csr *A, const tsg_dev_csr *B,
     TSG_TRY(dev_csr2tile_row_major(cx, *A, tm, tn, tA, s));
     TSG_TRY(dev_csr2tile_col_major(cx, *B, tm, tn, tB, s));
     TSG_HIP(hipEventRecord(cx.ev[9], s));
-    TSG_TRY(dev_tilespgemm(cx, tA, tB, tC, &st, s, cx.ev));
-    TSG_TRY(dev_tile2csr(cx, tC, *C, s));
+    // tile2csr is fused into step 3's epilogue on this path (C tiles stay materialised)
+    TSG_TRY(dev_tilespgemm(cx, tA, tB, tC, &st, s, cx.ev, C));
     TSG_HIP(hipEventRecord(cx.ev[10], s));
     TSG_HIP(hipEventSynchronize(cx.ev[10]));
     auto h1 = std::chrono::steady_clock::now();

@@ -20,6 +20,7 @@
 #include "tsg_internal.h"
 
 #include <cstdio>
+#include <type_traits>
 
 namespace tsg {
 
@@ -201,12 +202,26 @@ int scan_exclusive_i64(Context &cx, long long *a, long n, hipStream_t s) {
 constexpr int SORT_T1 = 16, SORT_T2 = 512, SORT_T3 = 4096;
 
 __global__ __launch_bounds__(WG) void k_sort_classify(const int *seg, int nseg, int *lists, int *counts) {
-    for (int i = blockIdx.x * WG + threadIdx.x; i < nseg; i += gridDim.x * WG) {
-        int len = seg[i + 1] - seg[i];
-        if (len <= 1) continue;
-        int tier = len <= SORT_T1 ? 0 : len <= SORT_T2 ? 1 : len <= SORT_T3 ? 2 : 3;
-        int pos = atomicAdd(&counts[tier], 1);
-        lists[(long)tier * nseg + pos] = i;
+    const int lane = lane_id();
+    const u64 below = (1ull << lane) - 1ull;
+    for (long base = (long)blockIdx.x * WG; base < nseg; base += (long)gridDim.x * WG) {
+        const long i = base + threadIdx.x;
+        int tier = -1;
+        if (i < nseg) {
+            int len = seg[i + 1] - seg[i];
+            if (len > 1) tier = len <= SORT_T1 ? 0 : len <= SORT_T2 ? 1 : len <= SORT_T3 ? 2 : 3;
+        }
+        // one atomic per (wave, tier) instead of one per segment on 4 hot words
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const u64 msk = __ballot(tier == t);
+            if (!msk) continue;
+            const int leader = __ffsll((long long)msk) - 1;
+            int pos0 = 0;
+            if (lane == leader) pos0 = atomicAdd(&counts[t], __popcll(msk));
+            pos0 = __shfl(pos0, leader, 64);
+            if (tier == t) lists[(long)t * nseg + pos0 + __popcll(msk & below)] = (int)i;
+        }
     }
 }
 
@@ -284,38 +299,67 @@ __global__ __launch_bounds__(WG) void k_sort_t3(u64 *keys, const int *seg, const
     }
 }
 
-__global__ __launch_bounds__(WG) void k_sort_t4(u64 *keys, u64 *tmp, const int *seg, const int *list,
-                                                const int *count) {
+// tier 4 work items are (segment, 4096-chunk) pairs spread over the whole grid;
+// each workgroup walks the (short) list of big segments to find its pair.
+__device__ __forceinline__ bool t4_pair(const int *seg, const int *list, int n, long idx, int *st, int *len,
+                                        int *c) {
+    for (int j = 0; j < n; ++j) {
+        const int sg = list[j];
+        const int l = seg[sg + 1] - seg[sg];
+        const long nch = (l + SORT_T3 - 1) / SORT_T3;
+        if (idx < nch) {
+            *st = seg[sg];
+            *len = l;
+            *c = (int)idx;
+            return true;
+        }
+        idx -= nch;
+    }
+    return false;
+}
+
+__global__ __launch_bounds__(WG) void k_sort_t4_chunks(u64 *keys, const int *seg, const int *list, const int *count) {
     __shared__ u64 s[SORT_T3];
     const int n = *count;
-    for (int j = blockIdx.x; j < n; j += gridDim.x) {
-        int i = list[j];
-        int st = seg[i], len = seg[i + 1] - st;
-        int nch = (len + SORT_T3 - 1) / SORT_T3;
-        for (int c = 0; c < nch; ++c) {
-            int cs = st + c * SORT_T3, cl = min(SORT_T3, len - c * SORT_T3);
-            for (int q = threadIdx.x; q < SORT_T3; q += WG) s[q] = q < cl ? keys[cs + q] : ~0ull;
-            __syncthreads();
-            block_bitonic_sort(s, SORT_T3);
-            for (int q = threadIdx.x; q < cl; q += WG) keys[cs + q] = s[q];
-            __syncthreads();
-        }
-        __threadfence_block();
+    int st, len, c;
+    for (long idx = blockIdx.x; t4_pair(seg, list, n, idx, &st, &len, &c); idx += gridDim.x) {
+        const int cs = st + c * SORT_T3, cl = min(SORT_T3, len - c * SORT_T3);
+        for (int q = threadIdx.x; q < SORT_T3; q += WG) s[q] = q < cl ? keys[cs + q] : ~0ull;
         __syncthreads();
-        for (int q = threadIdx.x; q < len; q += WG) {
-            u64 k = keys[st + q];
-            int own = q / SORT_T3;
-            long rank = q - own * SORT_T3;
-            for (int c = 0; c < nch; ++c) {
-                if (c == own) continue;
-                int cs = st + c * SORT_T3, cl = min(SORT_T3, len - c * SORT_T3);
-                rank += lower_bound_dev(keys + cs, 0, cl, k);
+        block_bitonic_sort(s, SORT_T3);
+        for (int q = threadIdx.x; q < cl; q += WG) keys[cs + q] = s[q];
+        __syncthreads();
+    }
+}
+
+// place every key of a chunk at its rank in the merged segment (keys unique)
+__global__ __launch_bounds__(WG) void k_sort_t4_place(const u64 *keys, u64 *tmp, const int *seg, const int *list,
+                                                      const int *count) {
+    const int n = *count;
+    int st, len, c;
+    for (long idx = blockIdx.x; t4_pair(seg, list, n, idx, &st, &len, &c); idx += gridDim.x) {
+        const int nch = (len + SORT_T3 - 1) / SORT_T3;
+        const int cs = st + c * SORT_T3, cl = min(SORT_T3, len - c * SORT_T3);
+        for (int q = threadIdx.x; q < cl; q += WG) {
+            const u64 k = keys[cs + q];
+            long rank = q;
+            for (int o = 0; o < nch; ++o) {
+                if (o == c) continue;
+                const int os = st + o * SORT_T3, ol = min(SORT_T3, len - o * SORT_T3);
+                rank += lower_bound_dev(keys + os, 0, ol, k);
             }
             tmp[st + rank] = k;
         }
-        __syncthreads();
-        for (int q = threadIdx.x; q < len; q += WG) keys[st + q] = tmp[st + q];
-        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(WG) void k_sort_t4_copy(u64 *keys, const u64 *tmp, const int *seg, const int *list,
+                                                     const int *count) {
+    const int n = *count;
+    int st, len, c;
+    for (long idx = blockIdx.x; t4_pair(seg, list, n, idx, &st, &len, &c); idx += gridDim.x) {
+        const int cs = st + c * SORT_T3, cl = min(SORT_T3, len - c * SORT_T3);
+        for (int q = threadIdx.x; q < cl; q += WG) keys[cs + q] = tmp[cs + q];
     }
 }
 
@@ -331,7 +375,10 @@ int segmented_sort_u64(Context &cx, u64 *keys, const int *seg, int nseg, long to
     k_sort_t1<<<grid_for(nseg, WG, 2048), WG, 0, s>>>(keys, seg, lists, counts);
     k_sort_t2<<<grid_for(nseg, WAVES, 2048), WG, 0, s>>>(keys, seg, lists + nseg, counts + 1);
     k_sort_t3<<<grid_for(nseg, 1, 1024), WG, 0, s>>>(keys, seg, lists + 2L * nseg, counts + 2);
-    k_sort_t4<<<grid_for(nseg, 1, 512), WG, 0, s>>>(keys, tmp, seg, lists + 3L * nseg, counts + 3);
+    const int g4 = grid_for(total / SORT_T3 + 1, 1, 1024);
+    k_sort_t4_chunks<<<g4, WG, 0, s>>>(keys, seg, lists + 3L * nseg, counts + 3);
+    k_sort_t4_place<<<g4, WG, 0, s>>>(keys, tmp, seg, lists + 3L * nseg, counts + 3);
+    k_sort_t4_copy<<<g4, WG, 0, s>>>(keys, tmp, seg, lists + 3L * nseg, counts + 3);
     TSG_HIP(hipGetLastError());
     cx.put(lists);
     cx.put(counts);
@@ -810,27 +857,30 @@ __global__ void k_rows_from_units(const int *unit_off, int tilem, int nwin, int 
     for (int i = blockIdx.x * WG + threadIdx.x; i <= tilem; i += gridDim.x * WG) Cptr[i] = unit_off[(long)i * nwin];
 }
 
-// chunks per C tile row: step 2 by tile count, step 3 by weight (nnz + ALPHA per tile)
-constexpr int S2_CH = 1024;
-constexpr int S3_CAPW = 2048, S3_ALPHA = 8;
-constexpr int S3_MAXT = S3_CAPW / S3_ALPHA + 1;
-constexpr int S3_MAXNZ = S3_CAPW + 256 + 8;
+// ---------------------------------------------------------------------------
+// Steps 2 and 3 share one chunking: unit = (C tile row i, <= CH consecutive C
+// tiles of that row).  Both enumerate the unit's (A tile, B tile) products and
+// OR the B tile row masks into LDS C row masks (the reference's step-2 bitmask
+// symbolic, tilespgemm-cuda.h:567-577); step 3 recomputes the masks in LDS
+// instead of round-tripping them through HBM.
+// ---------------------------------------------------------------------------
+constexpr int CH = 512;          // C tiles per unit
+constexpr int S3_NZCAP = 2048;   // fp64 accumulator slots per numeric pass
 
-__device__ __forceinline__ long s3_wrel(const int *nnzoff, int t0, int t) {
-    return (long)(nnzoff[t] - nnzoff[t0]) + (long)S3_ALPHA * (t - t0);
+template <int TM> struct CM {
+    static constexpr int MW = TM / 16;           // u16 mask words per C row
+    static constexpr int TW = TM * MW;           // u16 mask words per C tile
+    static constexpr int TW32 = (TW + 1) / 2;    // u32 LDS words per C tile
+};
+
+template <int TM> __device__ __forceinline__ u32 lds_row_word(const u32 *tile, int r, int w) {
+    const int k = r * CM<TM>::MW + w;
+    return (tile[k >> 1] >> ((k & 1) * 16)) & 0xffffu;
 }
 
-template <int STEP>
-__global__ void k_units_per_row(const int *Cptr, const int *nnzoff, int tilem, int *nunits) {
-    for (int i = blockIdx.x * WG + threadIdx.x; i < tilem; i += gridDim.x * WG) {
-        int t0 = Cptr[i], t1 = Cptr[i + 1];
-        int n = 0;
-        if (t1 > t0) {
-            if (STEP == 2) n = (t1 - t0 + S2_CH - 1) / S2_CH;
-            else n = (int)(s3_wrel(nnzoff, t0, t1 - 1) / S3_CAPW) + 1;
-        }
-        nunits[i] = n;
-    }
+__global__ void k_units_per_row(const int *Cptr, int tilem, int *nunits) {
+    for (int i = blockIdx.x * WG + threadIdx.x; i < tilem; i += gridDim.x * WG)
+        nunits[i] = (Cptr[i + 1] - Cptr[i] + CH - 1) / CH;
     if (blockIdx.x == 0 && threadIdx.x == 0) nunits[tilem] = 0;
 }
 
@@ -839,214 +889,272 @@ __global__ void k_unit_rows(const int *uoff, int tilem, int *urow) {
         for (int u = uoff[i]; u < uoff[i + 1]; ++u) urow[u] = i;
 }
 
+struct ABView {
+    const int *Aptr, *Acol, *Annz;
+    const u16 *ColA;
+    const double *ValA;
+    const int *Bptr, *Bcol, *rm2csc, *Bnnz;
+    const u16 *PtrB, *ColB, *maskB;
+    const double *ValB;
+};
+
+// OR every product's B row masks into the unit's LDS C masks.
+template <int TM, int TN>
+__device__ __forceinline__ void unit_or_masks(int i, const int *s_cols, int ns, u32 *s_mask, const ABView &V,
+                                              ProdLds &L) {
+    constexpr int MW = CM<TM>::MW, TW32 = CM<TM>::TW32;
+    const int clo = s_cols[0], chi = s_cols[ns - 1];
+    for_each_product(V.Aptr[i], V.Aptr[i + 1], V.Acol, V.Bptr, V.Bcol, clo, chi, true, L, [&](int a, int b) {
+        const int sidx = lower_bound_dev(s_cols, 0, ns, V.Bcol[b]);
+        const u16 *mb = V.maskB + (size_t)V.rm2csc[b] * TN * MW;
+        u32 *tile = s_mask + sidx * TW32;
+        const int q1 = V.Annz[a + 1];
+        for (int qa = V.Annz[a]; qa < q1; ++qa) {
+            const int enc = V.ColA[qa];
+            const int r = enc / TN, c = enc - (enc / TN) * TN;
+#pragma unroll
+            for (int w = 0; w < MW; ++w) {
+                const u32 mv = mb[c * MW + w];
+                if (mv) {
+                    const int k = r * MW + w;
+                    atomicOr(&tile[k >> 1], mv << ((k & 1) * 16));
+                }
+            }
+        }
+    });
+}
+
+template <int TM>
+__device__ __forceinline__ void unit_load_cols_zero(const int *Ccol, int t0, int ns, int *s_cols, u32 *s_mask) {
+    constexpr int TW32 = CM<TM>::TW32;
+    for (int j = threadIdx.x; j < ns; j += WG) s_cols[j] = Ccol[t0 + j];
+    uint4 *m4 = reinterpret_cast<uint4 *>(s_mask);
+    const int n4 = (ns * TW32 + 3) / 4;
+    for (int j = threadIdx.x; j < n4; j += WG) m4[j] = make_uint4(0u, 0u, 0u, 0u);
+}
+
 // ---------------------------------------------------------------------------
-// step 2: per C-tile-row chunk of <= S2_CH tiles, C row masks in LDS
+// step 2: per-tile nnz (+ per-unit per-row counts for the CSR row pointers)
 // ---------------------------------------------------------------------------
 template <int TM, int TN>
-__global__ __launch_bounds__(WG) void k_step2(const int *uoff, const int *urow, int tilem, const int *Aptr,
-                                              const int *Acol, const int *Annz, const u16 *ColA,
-                                              const int *Bptr, const int *Bcol, const int *rm2csc,
-                                              const u16 *maskB, const int *Cptr, const int *Ccol,
-                                              u16 *PtrC, u16 *maskC, int *nnzC) {
-    constexpr int MW = TM / 16;            // mask words per C row (= per B row)
-    constexpr int TW = TM * MW;            // u16 mask words per C tile
-    constexpr int TW32 = (TW + 1) / 2;     // u32 LDS words per C tile
-    __shared__ u32 s_mask[S2_CH * TW32];
-    __shared__ int s_cols[S2_CH];
+__global__ __launch_bounds__(WG) void k_step2(const int *uoff, const int *urow, int tilem, ABView V,
+                                              const int *Cptr, const int *Ccol, int *nnzC, int *unit_rc) {
+    constexpr int MW = CM<TM>::MW, TW32 = CM<TM>::TW32;
+    __shared__ __align__(16) u32 s_mask[CH * TW32];
+    __shared__ int s_cols[CH];
+    __shared__ int s_rc[TM];
     __shared__ ProdLds L;
     const int nunits = uoff[tilem];
     for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
         const int i = urow[u];
-        const int q = u - uoff[i];
-        const int t0 = Cptr[i] + q * S2_CH;
-        const int ns = min(S2_CH, Cptr[i + 1] - t0);
-        for (int j = threadIdx.x; j < ns; j += WG) s_cols[j] = Ccol[t0 + j];
-        for (int j = threadIdx.x; j < ns * TW32; j += WG) s_mask[j] = 0u;
+        const int t0 = Cptr[i] + (u - uoff[i]) * CH;
+        const int ns = min(CH, Cptr[i + 1] - t0);
+        unit_load_cols_zero<TM>(Ccol, t0, ns, s_cols, s_mask);
+        if (threadIdx.x < TM) s_rc[threadIdx.x] = 0;
         __syncthreads();
-        const int clo = s_cols[0], chi = s_cols[ns - 1];
-        for_each_product(Aptr[i], Aptr[i + 1], Acol, Bptr, Bcol, clo, chi, true, L, [&](int a, int b) {
-            const int sidx = lower_bound_dev(s_cols, 0, ns, Bcol[b]);
-            const u16 *mb = maskB + (size_t)rm2csc[b] * TN * MW;
-            u16 *ms16 = reinterpret_cast<u16 *>(s_mask) + (size_t)sidx * TW32 * 2;
-            for (int qa = Annz[a]; qa < Annz[a + 1]; ++qa) {
-                const int enc = ColA[qa];
-                const int r = enc / TN, c = enc - (enc / TN) * TN;
+        unit_or_masks<TM, TN>(i, s_cols, ns, s_mask, V, L);
+        int rc[TM];
 #pragma unroll
-                for (int w = 0; w < MW; ++w) {
-                    u32 mv = mb[c * MW + w];
-                    if (mv) {
-                        int wi = r * MW + w;  // u16 index inside the tile
-                        u32 *word = reinterpret_cast<u32 *>(ms16) + (wi >> 1);
-                        atomicOr(word, mv << ((wi & 1) * 16));
-                    }
-                }
-            }
-        });
+        for (int r = 0; r < TM; ++r) rc[r] = 0;
         for (int j = threadIdx.x; j < ns; j += WG) {
-            const u16 *ms16 = reinterpret_cast<const u16 *>(s_mask) + (size_t)j * TW32 * 2;
-            const int t = t0 + j;
+            const u32 *tile = s_mask + j * TW32;
             int nz = 0;
-            for (int k = 0; k < TW; ++k) nz += __popc((u32)ms16[k]);
-            nnzC[t] = nz;
-            if (nz) {
-                int run = 0;
-                for (int r = 0; r < TM; ++r) {
-                    PtrC[(size_t)t * TM + r] = (u16)run;
-                    for (int w = 0; w < MW; ++w) {
-                        u16 v = ms16[r * MW + w];
-                        maskC[(size_t)t * TW + r * MW + w] = v;
-                        run += __popc((u32)v);
-                    }
-                }
+#pragma unroll
+            for (int r = 0; r < TM; ++r) {
+                int c = 0;
+#pragma unroll
+                for (int w = 0; w < MW; ++w) c += __popc(lds_row_word<TM>(tile, r, w));
+                rc[r] += c;
+                nz += c;
             }
+            nnzC[t0 + j] = nz;
         }
+#pragma unroll
+        for (int r = 0; r < TM; ++r) {
+            int v = wave_sum(rc[r]);
+            if (lane_id() == 0 && v) atomicAdd(&s_rc[r], v);
+        }
+        __syncthreads();
+        if (threadIdx.x < TM) unit_rc[(long)u * TM + threadIdx.x] = s_rc[threadIdx.x];
         __syncthreads();
     }
 }
 
+// per (tile row, r): exclusive prefix of unit row counts along the row's units
+// (unit_rb) and the CSR row count (rowcnt)
+template <int TM>
+__global__ void k_unit_rowbase(const int *uoff, int tilem, int m, const int *unit_rc, int *unit_rb, int *rowcnt) {
+    for (long x = (long)blockIdx.x * WG + threadIdx.x; x < (long)tilem * TM; x += (long)gridDim.x * WG) {
+        const int i = (int)(x / TM), r = (int)(x - (long)i * TM);
+        int run = 0;
+        for (int u = uoff[i]; u < uoff[i + 1]; ++u) {
+            int v = unit_rc[(long)u * TM + r];
+            unit_rb[(long)u * TM + r] = run;
+            run += v;
+        }
+        if ((long)i * TM + r < m) rowcnt[(long)i * TM + r] = run;
+    }
+}
+
 // ---------------------------------------------------------------------------
-// step 3: numeric.  Chunk = C tiles of one C tile row with total weight
-// (nnz + S3_ALPHA per tile) <= S3_CAPW + one tile.  LDS: tile columns, nnz
-// offsets, row masks, u8 row pointers and the fp64 accumulator of the chunk.
-// Accumulator slot of (tile s, row r, col x) = off[s] + ptr[s][r] + popc(bits<x).
+// step 3: numeric.  Masks rebuilt in LDS; per tile: Ptr (u16 x TM, vector
+// stores) and local cols; values in passes over tile sub-ranges holding at
+// most S3_NZCAP nonzeros: LDS fp64 accumulator (ds_add_f64) addressed by
+//   off[s] + ptr[s][r] + popcount(row mask bits of columns < x),
+// then a contiguous write of the tile-layout values and (CSR=true) the CSR
+// scatter of the same values (tile2csr fused into the epilogue).
 // ---------------------------------------------------------------------------
 template <int TM>
-__device__ __forceinline__ int mask_rank(const u16 *mrow, int x) {
-    constexpr int MW = TM / 16;
+__device__ __forceinline__ int lds_rank(const u32 *tile, int r, int x) {
+    constexpr int MW = CM<TM>::MW;
     int rank = 0;
 #pragma unroll
     for (int w = 0; w < MW; ++w) {
-        u32 v = mrow[w];
+        const u32 v = lds_row_word<TM>(tile, r, w);
         if (w < (x >> 4)) rank += __popc(v);
         else if (w == (x >> 4)) rank += __popc(v >> (16 - (x & 15)));
     }
     return rank;
 }
 
-template <int TM, int TN>
-__global__ __launch_bounds__(WG) void k_step3(const int *uoff, const int *urow, int tilem, const int *Aptr,
-                                              const int *Acol, const int *Annz, const u16 *ColA,
-                                              const double *ValA, const int *Bptr, const int *Bcol,
-                                              const int *rm2csc, const int *Bnnz, const u16 *PtrB,
-                                              const u16 *ColB, const double *ValB, const int *Cptr,
-                                              const int *Ccol, const int *nnzoff, const u16 *maskC,
-                                              u16 *ColC, double *ValC) {
-    constexpr int MW = TM / 16;
-    constexpr int TW = TM * MW;
-    __shared__ double acc[S3_MAXNZ];
-    __shared__ u16 s_mask[S3_MAXT * TW];
-    __shared__ int s_cols[S3_MAXT];
-    __shared__ int s_off[S3_MAXT];
-    __shared__ unsigned char s_ptr[S3_MAXT * TM];
+template <int TM, int TN, bool CSR>
+__global__ __launch_bounds__(WG) void k_step3(const int *uoff, const int *urow, int tilem, int m, ABView V,
+                                              const int *Cptr, const int *Ccol, const int *nnzoff, u16 *PtrC,
+                                              u16 *ColC, double *ValC, const int *unit_rb, const int *rowptr,
+                                              int *csr_col, double *csr_val) {
+    constexpr int MW = CM<TM>::MW, TW32 = CM<TM>::TW32;
+    typedef typename std::conditional<(TM <= 16), unsigned char, u16>::type ptr_t;
+    constexpr int LANES = WG / TM;  // CSR epilogue: TM rows x LANES tile blocks
+    __shared__ __align__(16) u32 s_mask[CH * TW32];
+    __shared__ __align__(16) double acc[S3_NZCAP];
+    __shared__ int s_cols[CH];
+    __shared__ int s_off[CH + 1];
+    __shared__ ptr_t s_ptr[CH * TM];
+    __shared__ int s_carry[TM];
     __shared__ ProdLds L;
     const int nunits = uoff[tilem];
     for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
         const int i = urow[u];
-        const int q = u - uoff[i];
-        const int r0 = Cptr[i], r1 = Cptr[i + 1];
-        // chunk q = tiles t in [r0, r1) with floor(wrel(t)/CAPW) == q
-        int lo = r0, hi = r1;
-        while (lo < hi) {
-            int mid = (lo + hi) >> 1;
-            if (s3_wrel(nnzoff, r0, mid) / S3_CAPW < q) lo = mid + 1; else hi = mid;
-        }
-        const int t0 = lo;
-        hi = r1;
-        while (lo < hi) {
-            int mid = (lo + hi) >> 1;
-            if (s3_wrel(nnzoff, r0, mid) / S3_CAPW < q + 1) lo = mid + 1; else hi = mid;
-        }
-        const int t1 = lo;
-        const int ns = t1 - t0;
+        const int t0 = Cptr[i] + (u - uoff[i]) * CH;
+        const int ns = min(CH, Cptr[i + 1] - t0);
         const int nzbase = nnzoff[t0];
-        const int nz = nnzoff[t1] - nzbase;
-        if (ns <= 0 || nz == 0) continue;  // uniform: nothing to compute in this chunk
+        if (nnzoff[t0 + ns] == nzbase) continue;  // uniform: the unit's tiles are all empty
+        unit_load_cols_zero<TM>(Ccol, t0, ns, s_cols, s_mask);
+        for (int j = threadIdx.x; j <= ns; j += WG) s_off[j] = nnzoff[t0 + j] - nzbase;
+        if (threadIdx.x < TM) s_carry[threadIdx.x] = 0;
+        __syncthreads();
+        unit_or_masks<TM, TN>(i, s_cols, ns, s_mask, V, L);
+        // per tile: Ptr, LDS row pointers, tile-layout local columns
         for (int j = threadIdx.x; j < ns; j += WG) {
-            const int t = t0 + j;
-            s_cols[j] = Ccol[t];
-            const int o = nnzoff[t] - nzbase;
-            s_off[j] = o;
-            const bool ne = nnzoff[t + 1] > nnzoff[t];
+            if (s_off[j + 1] == s_off[j]) continue;
+            const u32 *tile = s_mask + j * TW32;
+            u16 p[TM];
             int run = 0;
+            int pos = nzbase + s_off[j];
+#pragma unroll
             for (int r = 0; r < TM; ++r) {
-                s_ptr[j * TM + r] = (unsigned char)(run > 255 ? 255 : run);
+                p[r] = (u16)run;
+                s_ptr[j * TM + r] = (ptr_t)run;
+#pragma unroll
                 for (int w = 0; w < MW; ++w) {
-                    u16 v = ne ? maskC[(size_t)t * TW + r * MW + w] : (u16)0;
-                    s_mask[j * TW + r * MW + w] = v;
-                    run += __popc((u32)v);
+                    u32 v = lds_row_word<TM>(tile, r, w);
+                    run += __popc(v);
+                    while (v) {
+                        const int hb = 31 - __clz(v);  // highest set bit = lowest column (MSB-first)
+                        ColC[pos++] = (u16)(w * 16 + (15 - hb));
+                        v &= ~(1u << hb);
+                    }
                 }
             }
-        }
-        for (int j = threadIdx.x; j < nz; j += WG) acc[j] = 0.0;
-        __syncthreads();
-        const int clo = s_cols[0], chi = s_cols[ns - 1];
-        for_each_product(Aptr[i], Aptr[i + 1], Acol, Bptr, Bcol, clo, chi, true, L, [&](int a, int b) {
-            const int sidx = lower_bound_dev(s_cols, 0, ns, Bcol[b]);
-            const int onext = (sidx + 1 < ns) ? s_off[sidx + 1] : nz;
-            if (onext == s_off[sidx]) return;  // structurally empty C tile
-            const int bc = rm2csc[b];
-            const int bb = Bnnz[bc], be = Bnnz[bc + 1];
-            const u16 *bp = PtrB + (size_t)bc * TN;
-            for (int qa = Annz[a]; qa < Annz[a + 1]; ++qa) {
-                const int enc = ColA[qa];
-                const int r = enc / TN, c = enc - (enc / TN) * TN;
-                const double va = ValA[qa];
-                const int ks = bb + bp[c];
-                const int ke = (c == TN - 1) ? be : bb + bp[c + 1];
-                if (ks >= ke) continue;
-                const u16 *mrow = &s_mask[sidx * TW + r * MW];
-                const int rowbase = s_off[sidx] + (TM <= 16 ? (int)s_ptr[sidx * TM + r] : 0);
-                int rb = rowbase;
-                if (TM > 16) {  // u8 pointers saturate above 255: recount
-                    rb = s_off[sidx];
-                    for (int rr = 0; rr < r; ++rr)
-                        for (int w = 0; w < MW; ++w) rb += __popc((u32)s_mask[sidx * TW + rr * MW + w]);
-                }
-                for (int kb = ks; kb < ke; ++kb) {
-                    const int x = ColB[kb];
-                    atomicAdd(&acc[rb + mask_rank<TM>(mrow, x)], va * ValB[kb]);
-                }
-            }
-        });
-        // values: contiguous tile-major run of the chunk
-        for (int j = threadIdx.x; j < nz; j += WG) ValC[nzbase + j] = acc[j];
-        // columns: one (tile,row) per thread, bits expanded in ascending order
-        for (int sr = threadIdx.x; sr < ns * TM; sr += WG) {
-            const int j = sr / TM, r = sr - (sr / TM) * TM;
-            int pos = s_off[j];
-            for (int rr = 0; rr < r; ++rr)
-                for (int w = 0; w < MW; ++w) pos += __popc((u32)s_mask[j * TW + rr * MW + w]);
-            for (int w = 0; w < MW; ++w) {
-                u32 v = s_mask[j * TW + r * MW + w];
-                while (v) {
-                    int bit = 31 - __clz(v);  // highest set bit = lowest column (MSB-first)
-                    ColC[nzbase + pos++] = (u16)(w * 16 + (15 - bit));
-                    v &= ~(1u << bit);
-                }
-            }
+            uint4 *dst = reinterpret_cast<uint4 *>(PtrC + (size_t)(t0 + j) * TM);
+#pragma unroll
+            for (int k = 0; k < TM / 8; ++k)
+                dst[k] = make_uint4(p[8 * k] | ((u32)p[8 * k + 1] << 16), p[8 * k + 2] | ((u32)p[8 * k + 3] << 16),
+                                    p[8 * k + 4] | ((u32)p[8 * k + 5] << 16), p[8 * k + 6] | ((u32)p[8 * k + 7] << 16));
         }
         __syncthreads();
-    }
-}
-
-__global__ void k_zero_empty_ptr(const int *nnzoff, int numtile, int tm, u16 *Ptr, u16 *mask) {
-    const int mw = tm / 16;
-    for (long x = (long)blockIdx.x * WG + threadIdx.x; x < (long)numtile * tm; x += (long)gridDim.x * WG) {
-        int t = (int)(x / tm);
-        if (nnzoff[t + 1] == nnzoff[t]) {
-            Ptr[x] = 0;
-            for (int w = 0; w < mw; ++w) mask[x * mw + w] = 0;
+        for (int s_lo = 0; s_lo < ns;) {
+            // largest s_hi with s_off[s_hi] - s_off[s_lo] <= S3_NZCAP (one tile always fits)
+            int lo = s_lo + 1, hi = ns;
+            while (lo < hi) {
+                int mid = (lo + hi + 1) >> 1;
+                if (s_off[mid] - s_off[s_lo] <= S3_NZCAP) lo = mid; else hi = mid - 1;
+            }
+            const int s_hi = lo;
+            const int base = s_off[s_lo];
+            const int nsub = s_off[s_hi] - base;
+            if (nsub == 0) { s_lo = s_hi; continue; }  // uniform
+            for (int j = threadIdx.x; j < nsub; j += WG) acc[j] = 0.0;
+            __syncthreads();
+            for_each_product(V.Aptr[i], V.Aptr[i + 1], V.Acol, V.Bptr, V.Bcol, s_cols[s_lo], s_cols[s_hi - 1], true, L,
+                             [&](int a, int b) {
+                const int sidx = lower_bound_dev(s_cols, s_lo, s_hi, V.Bcol[b]);
+                const int orel = s_off[sidx] - base;
+                if (s_off[sidx + 1] == s_off[sidx]) return;  // structurally empty C tile
+                const int bc = V.rm2csc[b];
+                const int bb = V.Bnnz[bc], be = V.Bnnz[bc + 1];
+                const u16 *bp = V.PtrB + (size_t)bc * TN;
+                const u32 *tile = s_mask + sidx * TW32;
+                const int q1 = V.Annz[a + 1];
+                for (int qa = V.Annz[a]; qa < q1; ++qa) {
+                    const int enc = V.ColA[qa];
+                    const int r = enc / TN, c = enc - (enc / TN) * TN;
+                    const int ks = bb + bp[c];
+                    const int ke = (c == TN - 1) ? be : bb + bp[c + 1];
+                    if (ks >= ke) continue;
+                    const double va = V.ValA[qa];
+                    const int rb = orel + (int)s_ptr[sidx * TM + r];
+                    for (int kb = ks; kb < ke; ++kb)
+                        atomicAdd(&acc[rb + lds_rank<TM>(tile, r, V.ColB[kb])], va * V.ValB[kb]);
+                }
+            });
+            for (int j = threadIdx.x; j < nsub; j += WG) ValC[nzbase + base + j] = acc[j];
+            if (CSR) {
+                const int r = threadIdx.x / LANES, l = threadIdx.x - (threadIdx.x / LANES) * LANES;
+                const int nt = s_hi - s_lo, blk = (nt + LANES - 1) / LANES;
+                const int sb = s_lo + l * blk, se = min(s_hi, sb + blk);
+                int tot = 0;
+                for (int sx = sb; sx < se; ++sx)
+#pragma unroll
+                    for (int w = 0; w < MW; ++w) tot += __popc(lds_row_word<TM>(s_mask + sx * TW32, r, w));
+                int inc = tot;
+#pragma unroll
+                for (int d = 1; d < LANES; d <<= 1) {
+                    int y = __shfl_up(inc, d, LANES);
+                    if (l >= d) inc += y;
+                }
+                const long R = (long)i * TM + r;
+                if (R < m) {
+                    int dst = rowptr[R] + unit_rb[(long)u * TM + r] + s_carry[r] + inc - tot;
+                    for (int sx = sb; sx < se; ++sx) {
+                        const u32 *tile = s_mask + sx * TW32;
+                        int k = s_off[sx] - base + (int)s_ptr[sx * TM + r];
+                        const int cbase = s_cols[sx] * TM;
+#pragma unroll
+                        for (int w = 0; w < MW; ++w) {
+                            u32 v = lds_row_word<TM>(tile, r, w);
+                            while (v) {
+                                const int hb = 31 - __clz(v);
+                                csr_col[dst] = cbase + w * 16 + (15 - hb);
+                                csr_val[dst] = acc[k];
+                                ++dst;
+                                ++k;
+                                v &= ~(1u << hb);
+                            }
+                        }
+                    }
+                }
+                __syncthreads();
+                if (l == LANES - 1) s_carry[r] += inc;
+            }
+            __syncthreads();
+            s_lo = s_hi;
         }
     }
-}
-
-__global__ void k_crow(const int *Cptr, int tilem, int *Crow) {
-    for (int i = blockIdx.x * WG + threadIdx.x; i < tilem; i += gridDim.x * WG)
-        for (int t = Cptr[i]; t < Cptr[i + 1]; ++t) Crow[t] = i;
 }
 
 int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_dev_tiles &C,
-                   tsg_stats *st, hipStream_t s, hipEvent_t *ev) {
+                   tsg_stats *st, hipStream_t s, hipEvent_t *ev, tsg_dev_csr *csr_out) {
     constexpr int TM = 16, TN = 16;
     if (A.tile_m != TM || A.tile_n != TN || B.tile_m != TN || B.tile_n != TM) return TSG_ERR_UNSUPPORTED;
     if (A.n != B.m) return TSG_ERR_INVALID;
@@ -1091,51 +1199,65 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     cx.put(prod);
     if (ev) TSG_HIP(hipEventRecord(ev[1], s));
     // ---- step 2 ----
-    int *nun = nullptr, *urow = nullptr;
-    const long maxu2 = (long)numblkC / S2_CH + tilemA + 1;
-    TSG_TRY(cx.get(&nun, (size_t)tilemA + 1));
-    TSG_TRY(cx.get(&urow, (size_t)maxu2));
+    const ABView V{A.tile_ptr, A.tile_columnidx, A.tile_nnz, A.tile_csr_Col, A.tile_csr_Value,
+                   B.tile_ptr, B.tile_columnidx, B.tile_rm2csc, B.tile_nnz, B.tile_csr_Ptr,
+                   B.tile_csr_Col, B.mask, B.tile_csr_Value};
+    int *uoff = nullptr, *urow = nullptr, *unit_rc = nullptr;
+    const long maxu = (long)numblkC / CH + tilemA + 1;
+    TSG_TRY(cx.get(&uoff, (size_t)tilemA + 1));
+    TSG_TRY(cx.get(&urow, (size_t)maxu));
+    TSG_TRY(cx.get(&unit_rc, (size_t)maxu * TM));
     TSG_TRY(cx.get(&C.tile_nnz, nb1));
-    TSG_TRY(cx.get(&C.tile_csr_Ptr, nb1 * TM));
-    TSG_TRY(cx.get(&C.mask, nb1 * TM * (TM / 16)));
-    k_units_per_row<2><<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(C.tile_ptr, nullptr, tilemA, nun);
-    TSG_TRY(scan_exclusive_i32(cx, nun, (long)tilemA + 1, s));
-    k_unit_rows<<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(nun, tilemA, urow);
+    k_units_per_row<<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(C.tile_ptr, tilemA, uoff);
+    TSG_TRY(scan_exclusive_i32(cx, uoff, (long)tilemA + 1, s));
+    k_unit_rows<<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(uoff, tilemA, urow);
     k_set_i32<<<1, 1, 0, s>>>(C.tile_nnz + numblkC, 0);
     TSG_HIP(hipGetLastError());
+    const int gu = grid_for(maxu, 1, 16384);
     if (numblkC > 0)
-        k_step2<TM, TN><<<grid_for(maxu2, 1, 16384), WG, 0, s>>>(
-            nun, urow, tilemA, A.tile_ptr, A.tile_columnidx, A.tile_nnz, A.tile_csr_Col, B.tile_ptr,
-            B.tile_columnidx, B.tile_rm2csc, B.mask, C.tile_ptr, C.tile_columnidx, C.tile_csr_Ptr, C.mask,
-            C.tile_nnz);
+        k_step2<TM, TN><<<gu, WG, 0, s>>>(uoff, urow, tilemA, V, C.tile_ptr, C.tile_columnidx, C.tile_nnz, unit_rc);
     TSG_HIP(hipGetLastError());
     TSG_TRY(scan_exclusive_i32(cx, C.tile_nnz, (long)numblkC + 1, s));
     int nnzC = 0;
     TSG_TRY(read_i32(cx, C.tile_nnz + numblkC, &nnzC, s));
     C.nnz = nnzC;
+    int *unit_rb = nullptr;
+    if (csr_out) {
+        csr_out->m = A.m;
+        csr_out->n = B.n;
+        csr_out->nnz = nnzC;
+        TSG_TRY(cx.get(&csr_out->rowpointer, (size_t)A.m + 1));
+        TSG_TRY(cx.get(&csr_out->columnindex, (size_t)nnzC + 1));
+        TSG_TRY(cx.get(&csr_out->value, (size_t)nnzC + 1));
+        TSG_TRY(cx.get(&unit_rb, (size_t)maxu * TM));
+        k_set_i32<<<1, 1, 0, s>>>(csr_out->rowpointer + A.m, 0);
+        if (tilemA > 0)
+            k_unit_rowbase<TM><<<grid_for((long)tilemA * TM, WG, 8192), WG, 0, s>>>(uoff, tilemA, A.m, unit_rc, unit_rb,
+                                                                                  csr_out->rowpointer);
+        TSG_HIP(hipGetLastError());
+        TSG_TRY(scan_exclusive_i32(cx, csr_out->rowpointer, (long)A.m + 1, s));
+    }
     if (ev) TSG_HIP(hipEventRecord(ev[2], s));
     // ---- step 3 ----
-    const long maxu3 = ((long)nnzC + (long)S3_ALPHA * numblkC) / S3_CAPW + tilemA + 1;
-    int *nun3 = nullptr, *urow3 = nullptr;
-    TSG_TRY(cx.get(&nun3, (size_t)tilemA + 1));
-    TSG_TRY(cx.get(&urow3, (size_t)maxu3));
+    TSG_TRY(cx.get(&C.tile_csr_Ptr, nb1 * TM));
     TSG_TRY(cx.get(&C.tile_csr_Col, (size_t)nnzC + 1));
     TSG_TRY(cx.get(&C.tile_csr_Value, (size_t)nnzC + 1));
-    k_units_per_row<3><<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(C.tile_ptr, C.tile_nnz, tilemA, nun3);
-    TSG_TRY(scan_exclusive_i32(cx, nun3, (long)tilemA + 1, s));
-    k_unit_rows<<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(nun3, tilemA, urow3);
+    if (nnzC > 0) {
+        if (csr_out)
+            k_step3<TM, TN, true><<<gu, WG, 0, s>>>(uoff, urow, tilemA, A.m, V, C.tile_ptr, C.tile_columnidx,
+                                                     C.tile_nnz, C.tile_csr_Ptr, C.tile_csr_Col, C.tile_csr_Value,
+                                                     unit_rb, csr_out->rowpointer, csr_out->columnindex,
+                                                     csr_out->value);
+        else
+            k_step3<TM, TN, false><<<gu, WG, 0, s>>>(uoff, urow, tilemA, A.m, V, C.tile_ptr, C.tile_columnidx,
+                                                      C.tile_nnz, C.tile_csr_Ptr, C.tile_csr_Col, C.tile_csr_Value,
+                                                      nullptr, nullptr, nullptr, nullptr);
+    }
     TSG_HIP(hipGetLastError());
-    if (nnzC > 0)
-        k_step3<TM, TN><<<grid_for(maxu3, 1, 16384), WG, 0, s>>>(
-            nun3, urow3, tilemA, A.tile_ptr, A.tile_columnidx, A.tile_nnz, A.tile_csr_Col, A.tile_csr_Value,
-            B.tile_ptr, B.tile_columnidx, B.tile_rm2csc, B.tile_nnz, B.tile_csr_Ptr, B.tile_csr_Col,
-            B.tile_csr_Value, C.tile_ptr, C.tile_columnidx, C.tile_nnz, C.mask, C.tile_csr_Col,
-            C.tile_csr_Value);
-    TSG_HIP(hipGetLastError());
-    cx.put(nun);
+    cx.put(uoff);
     cx.put(urow);
-    cx.put(nun3);
-    cx.put(urow3);
+    cx.put(unit_rc);
+    cx.put(unit_rb);
     if (ev) TSG_HIP(hipEventRecord(ev[3], s));
     if (st) {
         st->numblkC = numblkC;
@@ -1143,6 +1265,23 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
         st->tile_products = tile_products;
     }
     return TSG_OK;
+}
+
+__global__ void k_zero_empty_ptr(const int *nnzoff, int numtile, int tm, u16 *Ptr, u16 *mask) {
+    const int mw = tm / 16;
+    for (long x = (long)blockIdx.x * WG + threadIdx.x; x < (long)numtile * tm; x += (long)gridDim.x * WG) {
+        int t = (int)(x / tm);
+        if (nnzoff[t + 1] == nnzoff[t]) {
+            Ptr[x] = 0;
+            if (mask)
+                for (int w = 0; w < mw; ++w) mask[x * mw + w] = 0;
+        }
+    }
+}
+
+__global__ void k_crow(const int *Cptr, int tilem, int *Crow) {
+    for (int i = blockIdx.x * WG + threadIdx.x; i < tilem; i += gridDim.x * WG)
+        for (int t = Cptr[i]; t < Cptr[i + 1]; ++t) Crow[t] = i;
 }
 
 // Reference-layout extras for the host drop-in API: zero Ptr of empty C tiles
