@@ -168,6 +168,9 @@ typedef struct tsg_dev_tiles {
     int *csc_tile_ptr;
     int *csc_tile_rowidx;
     int *tile_rm2csc;          /* row-major tile index -> CSC tile index      */
+    uint16_t *rm_mask;         /* B only: tile masks in row-major tile order   */
+    int *rm_rowstart;          /* B only: per row-major tile, tile_n+1 absolute
+                                  row starts into the CSC-ordered payload      */
 } tsg_dev_tiles;
 
 /* A context owns a device, a caching device allocator and the outputs of the

@@ -63,7 +63,8 @@ class DevTiles(C.Structure):
                 ("tilem", C.c_int), ("tilen", C.c_int), ("numtile", C.c_int)] + [
         (n, C.c_void_p) for n in ("tile_ptr", "tile_columnidx", "tile_rowidx", "tile_nnz",
                                   "tile_csr_Ptr", "tile_csr_Col", "tile_csr_Value", "mask",
-                                  "csc_tile_ptr", "csc_tile_rowidx", "tile_rm2csc")]
+                                  "csc_tile_ptr", "csc_tile_rowidx", "tile_rm2csc",
+                                  "rm_mask", "rm_rowstart")]
 
 
 _lib = None

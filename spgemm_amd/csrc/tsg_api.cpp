@@ -594,7 +594,7 @@ int tsg_dev_csr2tile_col_major(tsg_context *ctx, const tsg_dev_csr *B, int tm, i
 int tsg_dev_tilespgemm(tsg_context *ctx, const tsg_dev_tiles *A, const tsg_dev_tiles *B, void *stream,
                        tsg_dev_tiles *C, tsg_stats *stats) {
     if (!ctx || !A || !B || !C) return TSG_ERR_INVALID;
-    if (!B->tile_rm2csc) return TSG_ERR_INVALID;
+    if (!B->tile_rm2csc || !B->rm_mask || !B->rm_rowstart) return TSG_ERR_INVALID;
     return dev_tilespgemm(ctx->cx, *A, *B, *C, stats, (hipStream_t)stream, nullptr, nullptr);
 }
 
@@ -611,7 +611,7 @@ int tsg_dev_transpose(tsg_context *ctx, const tsg_dev_csr *A, void *stream, tsg_
 static void release_tiles(Context &cx, tsg_dev_tiles &t) {
     void *ps[] = {t.tile_ptr, t.tile_columnidx, t.tile_rowidx, t.tile_nnz, t.tile_csr_Ptr,
                   t.tile_csr_Col, t.tile_csr_Value, t.mask, t.csc_tile_ptr, t.csc_tile_rowidx,
-                  t.tile_rm2csc};
+                  t.tile_rm2csc, t.rm_mask, t.rm_rowstart};
     for (void *p : ps) cx.put(p);
     t = tsg_dev_tiles{};
 }

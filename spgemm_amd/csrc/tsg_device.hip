@@ -20,6 +20,7 @@
 #include "tsg_internal.h"
 
 #include <cstdio>
+#include <cstdlib>
 #include <type_traits>
 
 namespace tsg {
@@ -547,7 +548,8 @@ template <int TR, int TC, int MODE>
 __global__ __launch_bounds__(WG) void k_c2t_fill(const u64 *keys, const int *seg, int nseg, const int *col,
                                                  const double *val, const int *tile_ptr, int *tcol,
                                                  int *trow, int *tnnz, u16 *Ptr, u16 *Col, double *Val,
-                                                 u16 *mask, const int *rm2csc, const int *csc_nnz) {
+                                                 u16 *mask, const int *rm2csc, const int *csc_nnz,
+                                                 u16 *rm_mask, int *rm_rowstart) {
     constexpr int MW = TC / 16;
     const int lane = lane_id();
     const int gw = (blockIdx.x * WG + threadIdx.x) >> 6, nw = gridDim.x * WAVES;
@@ -591,11 +593,21 @@ __global__ __launch_bounds__(WG) void k_c2t_fill(const u64 *keys, const int *seg
             }
             u16 *Pt = Ptr + (size_t)t * TR;
             u16 *Mt = mask + (size_t)t * TR * MW;
+            // B: row-major views for the SpGEMM steps (no rm->csc indirection there)
+            u16 *Mr = (MODE == FILL_B_PAYLOAD) ? rm_mask + (size_t)trm * TR * MW : nullptr;
+            int *Rs = (MODE == FILL_B_PAYLOAD) ? rm_rowstart + (size_t)trm * (TR + 1) : nullptr;
+            const int rsbase = (MODE == FILL_B_PAYLOAD) ? csc_nnz[t] : 0;
             if (gs) {
                 const int rprev = nt ? -1 : key_lr(kp);
-                for (int rr = rprev + 1; rr <= lr; ++rr) Pt[rr] = (u16)(p - f);
+                for (int rr = rprev + 1; rr <= lr; ++rr) {
+                    Pt[rr] = (u16)(p - f);
+                    if (MODE == FILL_B_PAYLOAD) Rs[rr] = rsbase + (p - f);
+                }
                 for (int rr = rprev + 1; rr < lr; ++rr)
-                    for (int w = 0; w < MW; ++w) Mt[rr * MW + w] = 0;
+                    for (int w = 0; w < MW; ++w) {
+                        Mt[rr * MW + w] = 0;
+                        if (MODE == FILL_B_PAYLOAD) Mr[rr * MW + w] = 0;
+                    }
                 u16 mw[MW];
                 for (int w = 0; w < MW; ++w) mw[w] = 0;
                 for (int q = p; q < e; ++q) {
@@ -604,13 +616,21 @@ __global__ __launch_bounds__(WG) void k_c2t_fill(const u64 *keys, const int *seg
                     int lcq = col[s + key_lpos(kq)] % TC;
                     mw[lcq >> 4] |= (u16)(1u << (15 - (lcq & 15)));
                 }
-                for (int w = 0; w < MW; ++w) Mt[lr * MW + w] = mw[w];
+                for (int w = 0; w < MW; ++w) {
+                    Mt[lr * MW + w] = mw[w];
+                    if (MODE == FILL_B_PAYLOAD) Mr[lr * MW + w] = mw[w];
+                }
             }
             if (te) {
                 for (int rr = lr + 1; rr < TR; ++rr) {
                     Pt[rr] = (u16)(p - f + 1);
-                    for (int w = 0; w < MW; ++w) Mt[rr * MW + w] = 0;
+                    if (MODE == FILL_B_PAYLOAD) Rs[rr] = rsbase + (p - f + 1);
+                    for (int w = 0; w < MW; ++w) {
+                        Mt[rr * MW + w] = 0;
+                        if (MODE == FILL_B_PAYLOAD) Mr[rr * MW + w] = 0;
+                    }
                 }
+                if (MODE == FILL_B_PAYLOAD) Rs[TR] = rsbase + (p - f + 1);
             }
         }
     }
@@ -686,7 +706,7 @@ static int csr2tile_impl(Context &cx, const tsg_dev_csr &M, bool colmajor, tsg_d
         k_c2t_fill<TR, TC, FILL_A><<<gfill, WG, 0, s>>>(keys, seg, tilem, M.columnindex, M.value, out.tile_ptr,
                                                        out.tile_columnidx, out.tile_rowidx, out.tile_nnz,
                                                        out.tile_csr_Ptr, out.tile_csr_Col, out.tile_csr_Value,
-                                                       out.mask, nullptr, nullptr);
+                                                       out.mask, nullptr, nullptr, nullptr, nullptr);
         k_set_i32<<<1, 1, 0, s>>>(out.tile_nnz + numtile, nnz);
         TSG_HIP(hipGetLastError());
     } else {
@@ -698,10 +718,12 @@ static int csr2tile_impl(Context &cx, const tsg_dev_csr &M, bool colmajor, tsg_d
         TSG_TRY(cx.get(&out.csc_tile_ptr, (size_t)tilen + 1));
         TSG_TRY(cx.get(&out.csc_tile_rowidx, nt1));
         TSG_TRY(cx.get(&out.tile_rm2csc, nt1));
+        TSG_TRY(cx.get(&out.rm_mask, nt1 * TR * (TC / 16)));
+        TSG_TRY(cx.get(&out.rm_rowstart, nt1 * (TR + 1)));
         k_c2t_fill<TR, TC, FILL_B_STRUCT><<<gfill, WG, 0, s>>>(keys, seg, tilem, M.columnindex, M.value,
                                                               out.tile_ptr, out.tile_columnidx, out.tile_rowidx,
                                                               nnz_rm, nullptr, nullptr, nullptr, nullptr,
-                                                              nullptr, nullptr);
+                                                              nullptr, nullptr, nullptr, nullptr);
         TSG_HIP(hipMemsetAsync(out.csc_tile_ptr, 0, ((size_t)tilen + 1) * sizeof(int), s));
         TSG_HIP(hipMemsetAsync(fill, 0, ((size_t)tilen + 1) * sizeof(int), s));
         if (numtile > 0)
@@ -721,7 +743,7 @@ static int csr2tile_impl(Context &cx, const tsg_dev_csr &M, bool colmajor, tsg_d
                                                                out.tile_ptr, nullptr, nullptr, nullptr,
                                                                out.tile_csr_Ptr, out.tile_csr_Col,
                                                                out.tile_csr_Value, out.mask, out.tile_rm2csc,
-                                                               out.tile_nnz);
+                                                               out.tile_nnz, out.rm_mask, out.rm_rowstart);
         TSG_HIP(hipGetLastError());
         cx.put(nnz_rm);
         cx.put(fill);
@@ -859,13 +881,17 @@ __global__ void k_rows_from_units(const int *unit_off, int tilem, int nwin, int 
 
 // ---------------------------------------------------------------------------
 // Steps 2 and 3 share one chunking: unit = (C tile row i, <= CH consecutive C
-// tiles of that row).  Both enumerate the unit's (A tile, B tile) products and
-// OR the B tile row masks into LDS C row masks (the reference's step-2 bitmask
-// symbolic, tilespgemm-cuda.h:567-577); step 3 recomputes the masks in LDS
-// instead of round-tripping them through HBM.
+// tiles of that row), units are independent workgroup tasks.  A unit's (A
+// tile, B tile) products are the B tiles of each A tile's B row whose column
+// lies in the unit's column range; they are spread item-by-item over the 256
+// threads (consecutive items -> consecutive lanes, coalesced B reads).  Both
+// steps OR the B tile row masks into LDS C row masks (the reference's step-2
+// bitmask symbolic, tilespgemm-cuda.h:567-577); step 3 rebuilds them in LDS
+// instead of round-tripping 32 B per C tile through HBM.  B is read through
+// the row-major views (rm_mask, rm_rowstart) that csr2tile builds.
 // ---------------------------------------------------------------------------
-constexpr int CH = 512;          // C tiles per unit
-constexpr int S3_NZCAP = 2048;   // fp64 accumulator slots per numeric pass
+constexpr int CH = 256;          // C tiles per unit
+constexpr int S3_NZCAP = 1024;   // fp64 accumulator slots per numeric pass
 
 template <int TM> struct CM {
     static constexpr int MW = TM / 16;           // u16 mask words per C row
@@ -878,6 +904,19 @@ template <int TM> __device__ __forceinline__ u32 lds_row_word(const u32 *tile, i
     return (tile[k >> 1] >> ((k & 1) * 16)) & 0xffffu;
 }
 
+struct ABView {
+    const int *Aptr, *Acol, *Annz;
+    const u16 *ColA;
+    const double *ValA;
+    const int *Bptr, *Bcol;
+    const u16 *maskBrm;   // B tile masks, row-major tile order
+    const int *rowsBrm;   // B tile absolute row starts (TN+1 per tile), row-major tile order
+    const u16 *ColB;
+    const double *ValB;
+    const int *split;     // per (unit, A tile): first B tile of the unit's column range
+    const long long *sbase;  // per C tile row: offset of its units' split entries
+};
+
 __global__ void k_units_per_row(const int *Cptr, int tilem, int *nunits) {
     for (int i = blockIdx.x * WG + threadIdx.x; i < tilem; i += gridDim.x * WG)
         nunits[i] = (Cptr[i + 1] - Cptr[i] + CH - 1) / CH;
@@ -889,39 +928,124 @@ __global__ void k_unit_rows(const int *uoff, int tilem, int *urow) {
         for (int u = uoff[i]; u < uoff[i + 1]; ++u) urow[u] = i;
 }
 
-struct ABView {
-    const int *Aptr, *Acol, *Annz;
-    const u16 *ColA;
-    const double *ValA;
-    const int *Bptr, *Bcol, *rm2csc, *Bnnz;
-    const u16 *PtrB, *ColB, *maskB;
-    const double *ValB;
-};
+// per (tile row, r): exclusive prefix of the unit row counts along the row's
+// units (unit_rb) and the CSR row count (rowcnt)
+template <int TM>
+__global__ void k_unit_rowbase(const int *uoff, int tilem, int m, const int *unit_rc, int *unit_rb, int *rowcnt) {
+    for (long x = (long)blockIdx.x * WG + threadIdx.x; x < (long)tilem * TM; x += (long)gridDim.x * WG) {
+        const int i = (int)(x / TM), r = (int)(x - (long)i * TM);
+        int run = 0;
+        for (int u = uoff[i]; u < uoff[i + 1]; ++u) {
+            const int v = unit_rc[(long)u * TM + r];
+            unit_rb[(long)u * TM + r] = run;
+            run += v;
+        }
+        if ((long)i * TM + r < m) rowcnt[(long)i * TM + r] = run;
+    }
+}
 
-// OR every product's B row masks into the unit's LDS C masks.
+__global__ void k_crow(const int *Cptr, int tilem, int *Crow) {
+    for (int i = blockIdx.x * WG + threadIdx.x; i < tilem; i += gridDim.x * WG)
+        for (int t = Cptr[i]; t < Cptr[i + 1]; ++t) Crow[t] = i;
+}
+
+// split entries per C tile row: (#units) x (#A tiles)
+__global__ void k_split_counts(const int *uoff, const int *Aptr, int tilem, long long *sbase) {
+    for (int i = blockIdx.x * WG + threadIdx.x; i < tilem; i += gridDim.x * WG)
+        sbase[i] = (long long)(uoff[i + 1] - uoff[i]) * (Aptr[i + 1] - Aptr[i]);
+    if (blockIdx.x == 0 && threadIdx.x == 0) sbase[tilem] = 0;
+}
+
+// first index in [lo, hi) with Bcol[idx] >= key (exponential search from lo)
+__device__ __forceinline__ int gallop_ge(const int *Bcol, int lo, int hi, int key) {
+    if (lo >= hi || Bcol[lo] >= key) return lo;
+    int p = lo, step = 1;  // Bcol[p] < key
+    while (p + step < hi && Bcol[p + step] < key) {
+        p += step;
+        step <<= 1;
+    }
+    int l = p + 1, h = min(p + step, hi);
+    while (l < h) {
+        const int mid = (l + h) >> 1;
+        if (Bcol[mid] < key) l = mid + 1; else h = mid;
+    }
+    return l;
+}
+
+// thread per A tile: walk its B tile row once across the units of its C tile
+// row, recording where each unit's column range starts
+__global__ __launch_bounds__(WG) void k_unit_splits(int numtileA, const int *trowA, const int *Aptr, const int *Acol,
+                                                    const int *Bptr, const int *Bcol, const int *uoff, const int *Cptr,
+                                                    const int *Ccol, const long long *sbase, int *split) {
+    for (int a = blockIdx.x * WG + threadIdx.x; a < numtileA; a += gridDim.x * WG) {
+        const int i = trowA[a];
+        const int lena = Aptr[i + 1] - Aptr[i], j = a - Aptr[i];
+        const int nu = uoff[i + 1] - uoff[i];
+        const int k = Acol[a];
+        int p = Bptr[k];
+        const int b1 = Bptr[k + 1];
+        int *out = split + sbase[i] + j;
+        for (int q = 0; q < nu; ++q) {
+            if (q) p = gallop_ge(Bcol, p, b1, Ccol[Cptr[i] + q * CH]);
+            out[(long)q * lena] = p;
+        }
+    }
+}
+
+// Products of A tiles [ab, ab+na) (row i, unit q of nu, A tiles from a0) that
+// fall in the unit's column range, from the precomputed split points:
+// bs[], off[] (exclusive scan of the counts, off[na] = total).
+__device__ __forceinline__ int unit_setup(const ABView &V, int i, int q, int nu, int a0, int ab, int na, ProdLds &L) {
+    const int a = ab + threadIdx.x;
+    int bs = 0, len = 0;
+    if (threadIdx.x < na) {
+        const int lena = V.Aptr[i + 1] - a0;
+        const int *sp = V.split + V.sbase[i] + (a - a0);
+        bs = sp[(long)q * lena];
+        const int be = (q + 1 < nu) ? sp[(long)(q + 1) * lena] : V.Bptr[V.Acol[a] + 1];
+        len = be - bs;
+    }
+    int tot;
+    const int off = block_excl_scan(len, &tot, L.red);
+    L.bs[threadIdx.x] = bs;
+    L.off[threadIdx.x] = off;
+    if (threadIdx.x == 0) L.off[WG] = tot;
+    __syncthreads();
+    return tot;
+}
+
+// f(a, b, slot) for every item of the current setup
+template <class F>
+__device__ __forceinline__ void unit_items(const ABView &V, int ab, int na, int tot, const int *s_cols, int ns,
+                                           ProdLds &L, F &&f) {
+    for (int q = threadIdx.x; q < tot; q += WG) {
+        int lo = 0, hi = na - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (L.off[mid] <= q) lo = mid; else hi = mid - 1;
+        }
+        const int b = L.bs[lo] + (q - L.off[lo]);
+        f(ab + lo, b, lower_bound_dev(s_cols, 0, ns, V.Bcol[b]));
+    }
+}
+
 template <int TM, int TN>
-__device__ __forceinline__ void unit_or_masks(int i, const int *s_cols, int ns, u32 *s_mask, const ABView &V,
-                                              ProdLds &L) {
-    constexpr int MW = CM<TM>::MW, TW32 = CM<TM>::TW32;
-    const int clo = s_cols[0], chi = s_cols[ns - 1];
-    for_each_product(V.Aptr[i], V.Aptr[i + 1], V.Acol, V.Bptr, V.Bcol, clo, chi, true, L, [&](int a, int b) {
-        const int sidx = lower_bound_dev(s_cols, 0, ns, V.Bcol[b]);
-        const u16 *mb = V.maskB + (size_t)V.rm2csc[b] * TN * MW;
-        u32 *tile = s_mask + sidx * TW32;
-        const int q1 = V.Annz[a + 1];
-        for (int qa = V.Annz[a]; qa < q1; ++qa) {
-            const int enc = V.ColA[qa];
-            const int r = enc / TN, c = enc - (enc / TN) * TN;
+__device__ __forceinline__ void or_product_masks(const ABView &V, int a, int b, u32 *tile) {
+    constexpr int MW = CM<TM>::MW;
+    const u16 *mb = V.maskBrm + (size_t)b * TN * MW;
+    const int q1 = V.Annz[a + 1];
+    for (int qa = V.Annz[a]; qa < q1; ++qa) {
+        const int enc = V.ColA[qa];
+        const int r = enc / TN, c = enc - (enc / TN) * TN;
 #pragma unroll
-            for (int w = 0; w < MW; ++w) {
-                const u32 mv = mb[c * MW + w];
-                if (mv) {
-                    const int k = r * MW + w;
-                    atomicOr(&tile[k >> 1], mv << ((k & 1) * 16));
-                }
+        for (int w = 0; w < MW; ++w) {
+            const u32 mv = mb[c * MW + w];
+            if (mv) {
+                const int k = r * MW + w;
+                atomicOr(&tile[k >> 1], mv << ((k & 1) * 16));
             }
         }
-    });
+    }
 }
 
 template <int TM>
@@ -933,12 +1057,30 @@ __device__ __forceinline__ void unit_load_cols_zero(const int *Ccol, int t0, int
     for (int j = threadIdx.x; j < n4; j += WG) m4[j] = make_uint4(0u, 0u, 0u, 0u);
 }
 
+// OR the masks of every product of the unit.  Returns true when the whole
+// row fitted one A batch, i.e. L still holds the setup for a second pass.
+template <int TM, int TN>
+__device__ __forceinline__ bool unit_masks(const ABView &V, int i, int q, int nu, int a0, int a1, const int *s_cols,
+                                           int ns, u32 *s_mask, ProdLds &L, int *tot_out) {
+    constexpr int TW32 = CM<TM>::TW32;
+    int tot = 0;
+    for (int ab = a0; ab < a1; ab += WG) {
+        const int na = min(WG, a1 - ab);
+        tot = unit_setup(V, i, q, nu, a0, ab, na, L);
+        unit_items(V, ab, na, tot, s_cols, ns, L,
+                   [&](int a, int b, int sl) { or_product_masks<TM, TN>(V, a, b, s_mask + sl * TW32); });
+        __syncthreads();
+    }
+    *tot_out = tot;
+    return a1 - a0 <= WG;
+}
+
 // ---------------------------------------------------------------------------
-// step 2: per-tile nnz (+ per-unit per-row counts for the CSR row pointers)
+// step 2: per-tile nnz and per-unit per-row counts (-> CSR row pointers)
 // ---------------------------------------------------------------------------
 template <int TM, int TN>
-__global__ __launch_bounds__(WG) void k_step2(const int *uoff, const int *urow, int tilem, ABView V,
-                                              const int *Cptr, const int *Ccol, int *nnzC, int *unit_rc) {
+__global__ __launch_bounds__(WG) void k_step2(const int *uoff, const int *urow, int tilem, ABView V, const int *Cptr,
+                                              const int *Ccol, int *nnzC, int *unit_rc) {
     constexpr int MW = CM<TM>::MW, TW32 = CM<TM>::TW32;
     __shared__ __align__(16) u32 s_mask[CH * TW32];
     __shared__ int s_cols[CH];
@@ -952,11 +1094,14 @@ __global__ __launch_bounds__(WG) void k_step2(const int *uoff, const int *urow, 
         unit_load_cols_zero<TM>(Ccol, t0, ns, s_cols, s_mask);
         if (threadIdx.x < TM) s_rc[threadIdx.x] = 0;
         __syncthreads();
-        unit_or_masks<TM, TN>(i, s_cols, ns, s_mask, V, L);
+        int tot;
+        unit_masks<TM, TN>(V, i, u - uoff[i], uoff[i + 1] - uoff[i], V.Aptr[i], V.Aptr[i + 1], s_cols, ns, s_mask, L,
+                           &tot);
         int rc[TM];
 #pragma unroll
         for (int r = 0; r < TM; ++r) rc[r] = 0;
-        for (int j = threadIdx.x; j < ns; j += WG) {
+        if (threadIdx.x < ns) {  // ns <= CH == WG
+            const int j = threadIdx.x;
             const u32 *tile = s_mask + j * TW32;
             int nz = 0;
 #pragma unroll
@@ -964,14 +1109,14 @@ __global__ __launch_bounds__(WG) void k_step2(const int *uoff, const int *urow, 
                 int c = 0;
 #pragma unroll
                 for (int w = 0; w < MW; ++w) c += __popc(lds_row_word<TM>(tile, r, w));
-                rc[r] += c;
+                rc[r] = c;
                 nz += c;
             }
             nnzC[t0 + j] = nz;
         }
 #pragma unroll
         for (int r = 0; r < TM; ++r) {
-            int v = wave_sum(rc[r]);
+            const int v = wave_sum(rc[r]);
             if (lane_id() == 0 && v) atomicAdd(&s_rc[r], v);
         }
         __syncthreads();
@@ -980,29 +1125,13 @@ __global__ __launch_bounds__(WG) void k_step2(const int *uoff, const int *urow, 
     }
 }
 
-// per (tile row, r): exclusive prefix of unit row counts along the row's units
-// (unit_rb) and the CSR row count (rowcnt)
-template <int TM>
-__global__ void k_unit_rowbase(const int *uoff, int tilem, int m, const int *unit_rc, int *unit_rb, int *rowcnt) {
-    for (long x = (long)blockIdx.x * WG + threadIdx.x; x < (long)tilem * TM; x += (long)gridDim.x * WG) {
-        const int i = (int)(x / TM), r = (int)(x - (long)i * TM);
-        int run = 0;
-        for (int u = uoff[i]; u < uoff[i + 1]; ++u) {
-            int v = unit_rc[(long)u * TM + r];
-            unit_rb[(long)u * TM + r] = run;
-            run += v;
-        }
-        if ((long)i * TM + r < m) rowcnt[(long)i * TM + r] = run;
-    }
-}
-
 // ---------------------------------------------------------------------------
-// step 3: numeric.  Masks rebuilt in LDS; per tile: Ptr (u16 x TM, vector
-// stores) and local cols; values in passes over tile sub-ranges holding at
-// most S3_NZCAP nonzeros: LDS fp64 accumulator (ds_add_f64) addressed by
-//   off[s] + ptr[s][r] + popcount(row mask bits of columns < x),
-// then a contiguous write of the tile-layout values and (CSR=true) the CSR
-// scatter of the same values (tile2csr fused into the epilogue).
+// step 3: numeric.  Per unit: masks rebuilt in LDS, then passes over tile
+// sub-ranges holding <= S3_NZCAP nonzeros.  The LDS fp64 accumulator of a pass
+// is in CSR order (row r, then tiles, then columns):
+//   slot(s, r, x) = rowoff[r] + pre[s][r] + popc(row-r bits of columns < x)
+// so the CSR epilogue (tile2csr fused) writes runs coalesced; the tile-layout
+// output (Ptr/Col/Val, host API) is written per tile from the same slots.
 // ---------------------------------------------------------------------------
 template <int TM>
 __device__ __forceinline__ int lds_rank(const u32 *tile, int r, int x) {
@@ -1017,19 +1146,21 @@ __device__ __forceinline__ int lds_rank(const u32 *tile, int r, int x) {
     return rank;
 }
 
-template <int TM, int TN, bool CSR>
-__global__ __launch_bounds__(WG) void k_step3(const int *uoff, const int *urow, int tilem, int m, ABView V,
-                                              const int *Cptr, const int *Ccol, const int *nnzoff, u16 *PtrC,
-                                              u16 *ColC, double *ValC, const int *unit_rb, const int *rowptr,
-                                              int *csr_col, double *csr_val) {
+template <int TM, int TN, bool WCSR, bool WTILE>
+__global__ __launch_bounds__(WG) void k_step3(const int *uoff, const int *urow, int tilem, ABView V, const int *Cptr,
+                                              const int *Ccol, const int *nnzoff, const int *unit_rb,
+                                              const int *rowptr, int *csr_col, double *csr_val, u16 *PtrC, u16 *ColC,
+                                              double *ValC, int ablate) {
     constexpr int MW = CM<TM>::MW, TW32 = CM<TM>::TW32;
-    typedef typename std::conditional<(TM <= 16), unsigned char, u16>::type ptr_t;
-    constexpr int LANES = WG / TM;  // CSR epilogue: TM rows x LANES tile blocks
+    constexpr int LANES = WG / TM;  // P phase: TM rows x LANES contiguous tile blocks
     __shared__ __align__(16) u32 s_mask[CH * TW32];
     __shared__ __align__(16) double acc[S3_NZCAP];
+    __shared__ int s_ccol[S3_NZCAP];
     __shared__ int s_cols[CH];
     __shared__ int s_off[CH + 1];
-    __shared__ ptr_t s_ptr[CH * TM];
+    __shared__ u16 s_pre[CH * TM];
+    __shared__ int s_cnt[TM];
+    __shared__ int s_rowoff[TM + 1];
     __shared__ int s_carry[TM];
     __shared__ ProdLds L;
     const int nunits = uoff[tilem];
@@ -1039,80 +1170,53 @@ __global__ __launch_bounds__(WG) void k_step3(const int *uoff, const int *urow, 
         const int ns = min(CH, Cptr[i + 1] - t0);
         const int nzbase = nnzoff[t0];
         if (nnzoff[t0 + ns] == nzbase) continue;  // uniform: the unit's tiles are all empty
+        const int a0 = V.Aptr[i], a1 = V.Aptr[i + 1];
         unit_load_cols_zero<TM>(Ccol, t0, ns, s_cols, s_mask);
         for (int j = threadIdx.x; j <= ns; j += WG) s_off[j] = nnzoff[t0 + j] - nzbase;
-        if (threadIdx.x < TM) s_carry[threadIdx.x] = 0;
+        if (threadIdx.x < TM) s_carry[threadIdx.x] = WCSR ? unit_rb[(long)u * TM + threadIdx.x] : 0;
         __syncthreads();
-        unit_or_masks<TM, TN>(i, s_cols, ns, s_mask, V, L);
-        // per tile: Ptr, LDS row pointers, tile-layout local columns
-        for (int j = threadIdx.x; j < ns; j += WG) {
-            if (s_off[j + 1] == s_off[j]) continue;
-            const u32 *tile = s_mask + j * TW32;
-            u16 p[TM];
-            int run = 0;
-            int pos = nzbase + s_off[j];
+        int tot1 = 0;
+        bool single = true;
+        const int q = u - uoff[i], nu = uoff[i + 1] - uoff[i];
+        if (!(ablate & 1)) single = unit_masks<TM, TN>(V, i, q, nu, a0, a1, s_cols, ns, s_mask, L, &tot1);
+        else tot1 = unit_setup(V, i, q, nu, a0, a0, min(WG, a1 - a0), L);
+        if (WTILE) {  // Ptr of every non-empty tile (u16 x TM, vector stores)
+            for (int j = threadIdx.x; j < ns; j += WG) {
+                if (s_off[j + 1] == s_off[j]) continue;
+                const u32 *tile = s_mask + j * TW32;
+                u16 p[TM];
+                int run = 0;
 #pragma unroll
-            for (int r = 0; r < TM; ++r) {
-                p[r] = (u16)run;
-                s_ptr[j * TM + r] = (ptr_t)run;
+                for (int r = 0; r < TM; ++r) {
+                    p[r] = (u16)run;
 #pragma unroll
-                for (int w = 0; w < MW; ++w) {
-                    u32 v = lds_row_word<TM>(tile, r, w);
-                    run += __popc(v);
-                    while (v) {
-                        const int hb = 31 - __clz(v);  // highest set bit = lowest column (MSB-first)
-                        ColC[pos++] = (u16)(w * 16 + (15 - hb));
-                        v &= ~(1u << hb);
-                    }
+                    for (int w = 0; w < MW; ++w) run += __popc(lds_row_word<TM>(tile, r, w));
                 }
-            }
-            uint4 *dst = reinterpret_cast<uint4 *>(PtrC + (size_t)(t0 + j) * TM);
+                uint4 *dst = reinterpret_cast<uint4 *>(PtrC + (size_t)(t0 + j) * TM);
 #pragma unroll
-            for (int k = 0; k < TM / 8; ++k)
-                dst[k] = make_uint4(p[8 * k] | ((u32)p[8 * k + 1] << 16), p[8 * k + 2] | ((u32)p[8 * k + 3] << 16),
-                                    p[8 * k + 4] | ((u32)p[8 * k + 5] << 16), p[8 * k + 6] | ((u32)p[8 * k + 7] << 16));
+                for (int k = 0; k < TM / 8; ++k)
+                    dst[k] = make_uint4(p[8 * k] | ((u32)p[8 * k + 1] << 16), p[8 * k + 2] | ((u32)p[8 * k + 3] << 16),
+                                        p[8 * k + 4] | ((u32)p[8 * k + 5] << 16),
+                                        p[8 * k + 6] | ((u32)p[8 * k + 7] << 16));
+            }
         }
-        __syncthreads();
         for (int s_lo = 0; s_lo < ns;) {
-            // largest s_hi with s_off[s_hi] - s_off[s_lo] <= S3_NZCAP (one tile always fits)
-            int lo = s_lo + 1, hi = ns;
+            int lo = s_lo + 1, hi = ns;  // largest s_hi with nnz(s_lo..s_hi) <= NZCAP
             while (lo < hi) {
-                int mid = (lo + hi + 1) >> 1;
+                const int mid = (lo + hi + 1) >> 1;
                 if (s_off[mid] - s_off[s_lo] <= S3_NZCAP) lo = mid; else hi = mid - 1;
             }
             const int s_hi = lo;
-            const int base = s_off[s_lo];
-            const int nsub = s_off[s_hi] - base;
-            if (nsub == 0) { s_lo = s_hi; continue; }  // uniform
-            for (int j = threadIdx.x; j < nsub; j += WG) acc[j] = 0.0;
-            __syncthreads();
-            for_each_product(V.Aptr[i], V.Aptr[i + 1], V.Acol, V.Bptr, V.Bcol, s_cols[s_lo], s_cols[s_hi - 1], true, L,
-                             [&](int a, int b) {
-                const int sidx = lower_bound_dev(s_cols, s_lo, s_hi, V.Bcol[b]);
-                const int orel = s_off[sidx] - base;
-                if (s_off[sidx + 1] == s_off[sidx]) return;  // structurally empty C tile
-                const int bc = V.rm2csc[b];
-                const int bb = V.Bnnz[bc], be = V.Bnnz[bc + 1];
-                const u16 *bp = V.PtrB + (size_t)bc * TN;
-                const u32 *tile = s_mask + sidx * TW32;
-                const int q1 = V.Annz[a + 1];
-                for (int qa = V.Annz[a]; qa < q1; ++qa) {
-                    const int enc = V.ColA[qa];
-                    const int r = enc / TN, c = enc - (enc / TN) * TN;
-                    const int ks = bb + bp[c];
-                    const int ke = (c == TN - 1) ? be : bb + bp[c + 1];
-                    if (ks >= ke) continue;
-                    const double va = V.ValA[qa];
-                    const int rb = orel + (int)s_ptr[sidx * TM + r];
-                    for (int kb = ks; kb < ke; ++kb)
-                        atomicAdd(&acc[rb + lds_rank<TM>(tile, r, V.ColB[kb])], va * V.ValB[kb]);
-                }
-            });
-            for (int j = threadIdx.x; j < nsub; j += WG) ValC[nzbase + base + j] = acc[j];
-            if (CSR) {
+            const int nz = s_off[s_hi] - s_off[s_lo];
+            if (nz == 0) {  // uniform
+                s_lo = s_hi;
+                continue;
+            }
+            // P: per-row counts, row offsets, per-(tile,row) prefixes, CSR columns
+            {
                 const int r = threadIdx.x / LANES, l = threadIdx.x - (threadIdx.x / LANES) * LANES;
                 const int nt = s_hi - s_lo, blk = (nt + LANES - 1) / LANES;
-                const int sb = s_lo + l * blk, se = min(s_hi, sb + blk);
+                const int sb = s_lo + min(nt, l * blk), se = s_lo + min(nt, l * blk + blk);
                 int tot = 0;
                 for (int sx = sb; sx < se; ++sx)
 #pragma unroll
@@ -1120,44 +1224,113 @@ __global__ __launch_bounds__(WG) void k_step3(const int *uoff, const int *urow, 
                 int inc = tot;
 #pragma unroll
                 for (int d = 1; d < LANES; d <<= 1) {
-                    int y = __shfl_up(inc, d, LANES);
+                    const int y = __shfl_up(inc, d, LANES);
                     if (l >= d) inc += y;
                 }
-                const long R = (long)i * TM + r;
-                if (R < m) {
-                    int dst = rowptr[R] + unit_rb[(long)u * TM + r] + s_carry[r] + inc - tot;
-                    for (int sx = sb; sx < se; ++sx) {
-                        const u32 *tile = s_mask + sx * TW32;
-                        int k = s_off[sx] - base + (int)s_ptr[sx * TM + r];
-                        const int cbase = s_cols[sx] * TM;
+                if (l == LANES - 1) s_cnt[r] = inc;
+                __syncthreads();
+                if (threadIdx.x == 0) {
+                    int run = 0;
+                    for (int rr = 0; rr < TM; ++rr) {
+                        s_rowoff[rr] = run;
+                        run += s_cnt[rr];
+                    }
+                    s_rowoff[TM] = run;
+                }
+                __syncthreads();
+                int pre = inc - tot;
+                int pos = s_rowoff[r] + pre;
+                for (int sx = sb; sx < se; ++sx) {
+                    s_pre[sx * TM + r] = (u16)pre;
+                    const int cb = s_cols[sx] * TM;
+#pragma unroll
+                    for (int w = 0; w < MW; ++w) {
+                        u32 v = lds_row_word<TM>(s_mask + sx * TW32, r, w);
+                        pre += __popc(v);
+                        while (v) {
+                            const int hb = 31 - __clz(v);  // highest set bit = lowest column (MSB-first)
+                            s_ccol[pos++] = cb + w * 16 + (15 - hb);
+                            v &= ~(1u << hb);
+                        }
+                    }
+                }
+                for (int e = threadIdx.x; e < nz; e += WG) acc[e] = 0.0;
+                __syncthreads();
+            }
+            // V: values
+            if (!(ablate & 4)) {
+                for (int ab = a0; ab < a1; ab += WG) {
+                    const int na = min(WG, a1 - ab);
+                    const int tot = single ? tot1 : unit_setup(V, i, q, nu, a0, ab, na, L);
+                    unit_items(V, ab, na, tot, s_cols, ns, L, [&](int a, int b, int sl) {
+                        if (sl < s_lo || sl >= s_hi || s_off[sl + 1] == s_off[sl]) return;
+                        const int *br = V.rowsBrm + (size_t)b * (TN + 1);
+                        const u32 *tile = s_mask + sl * TW32;
+                        const int q1 = V.Annz[a + 1];
+                        for (int qa = V.Annz[a]; qa < q1; ++qa) {
+                            const int enc = V.ColA[qa];
+                            const int r = enc / TN, c = enc - (enc / TN) * TN;
+                            const int ks = br[c], ke = br[c + 1];
+                            if (ks >= ke) continue;
+                            const double va = V.ValA[qa];
+                            const int rb = s_rowoff[r] + (int)s_pre[sl * TM + r];
+                            for (int kb = ks; kb < ke; ++kb)
+                                atomicAdd(&acc[rb + lds_rank<TM>(tile, r, V.ColB[kb])], va * V.ValB[kb]);
+                        }
+                    });
+                    __syncthreads();
+                }
+            }
+            // W: outputs of the pass
+            if (WCSR && !(ablate & 8)) {
+                for (int e = threadIdx.x; e < nz; e += WG) {
+                    int r = 0;
+#pragma unroll
+                    for (int rr = 1; rr < TM; ++rr) r += (s_rowoff[rr] <= e) ? 1 : 0;
+                    const int dst = rowptr[(long)i * TM + r] + s_carry[r] + (e - s_rowoff[r]);
+                    csr_col[dst] = s_ccol[e];
+                    csr_val[dst] = acc[e];
+                }
+            }
+            if (WTILE) {
+                for (int j = s_lo + threadIdx.x; j < s_hi; j += WG) {
+                    if (s_off[j + 1] == s_off[j]) continue;
+                    const u32 *tile = s_mask + j * TW32;
+                    int out = nzbase + s_off[j];
+#pragma unroll
+                    for (int r = 0; r < TM; ++r) {
+                        int k = s_rowoff[r] + (int)s_pre[j * TM + r];
 #pragma unroll
                         for (int w = 0; w < MW; ++w) {
                             u32 v = lds_row_word<TM>(tile, r, w);
                             while (v) {
                                 const int hb = 31 - __clz(v);
-                                csr_col[dst] = cbase + w * 16 + (15 - hb);
-                                csr_val[dst] = acc[k];
-                                ++dst;
-                                ++k;
+                                ColC[out] = (u16)(w * 16 + (15 - hb));
+                                ValC[out++] = acc[k++];
                                 v &= ~(1u << hb);
                             }
                         }
                     }
                 }
-                __syncthreads();
-                if (l == LANES - 1) s_carry[r] += inc;
             }
+            __syncthreads();
+            if (threadIdx.x < TM) s_carry[threadIdx.x] += s_cnt[threadIdx.x];
             __syncthreads();
             s_lo = s_hi;
         }
     }
 }
 
+// TSG_ABLATE (diagnostics only: results are wrong when set) skips parts of
+// step 3 so that their cost can be measured: 1 masks, 4 values, 8 CSR writes.
+static int g_ablate = -1;
+
 int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_dev_tiles &C,
                    tsg_stats *st, hipStream_t s, hipEvent_t *ev, tsg_dev_csr *csr_out) {
+    if (g_ablate < 0) g_ablate = getenv("TSG_ABLATE") ? atoi(getenv("TSG_ABLATE")) : 0;
     constexpr int TM = 16, TN = 16;
     if (A.tile_m != TM || A.tile_n != TN || B.tile_m != TN || B.tile_n != TM) return TSG_ERR_UNSUPPORTED;
-    if (A.n != B.m) return TSG_ERR_INVALID;
+    if (A.n != B.m || !B.rm_mask || !B.rm_rowstart) return TSG_ERR_INVALID;
     const int tilemA = A.tilem, tilenB = B.tilen;
     C = tsg_dev_tiles{};
     C.m = A.m; C.n = B.n; C.tile_m = TM; C.tile_n = TM;
@@ -1199,10 +1372,7 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     cx.put(prod);
     if (ev) TSG_HIP(hipEventRecord(ev[1], s));
     // ---- step 2 ----
-    const ABView V{A.tile_ptr, A.tile_columnidx, A.tile_nnz, A.tile_csr_Col, A.tile_csr_Value,
-                   B.tile_ptr, B.tile_columnidx, B.tile_rm2csc, B.tile_nnz, B.tile_csr_Ptr,
-                   B.tile_csr_Col, B.mask, B.tile_csr_Value};
-    int *uoff = nullptr, *urow = nullptr, *unit_rc = nullptr;
+    int *uoff = nullptr, *urow = nullptr, *unit_rc = nullptr, *unit_rb = nullptr;
     const long maxu = (long)numblkC / CH + tilemA + 1;
     TSG_TRY(cx.get(&uoff, (size_t)tilemA + 1));
     TSG_TRY(cx.get(&urow, (size_t)maxu));
@@ -1213,22 +1383,38 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     k_unit_rows<<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(uoff, tilemA, urow);
     k_set_i32<<<1, 1, 0, s>>>(C.tile_nnz + numblkC, 0);
     TSG_HIP(hipGetLastError());
+    // split points of every A tile's B row at its C tile row's unit boundaries
+    long long *sbase = nullptr;
+    int *split = nullptr;
+    TSG_TRY(cx.get(&sbase, (size_t)tilemA + 1));
+    k_split_counts<<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(uoff, A.tile_ptr, tilemA, sbase);
+    TSG_TRY(scan_exclusive_i64(cx, sbase, (long)tilemA + 1, s));
+    long long nsplit = 0;
+    TSG_TRY(read_i64(cx, sbase + tilemA, &nsplit, s));
+    TSG_TRY(cx.get(&split, (size_t)nsplit + 1));
+    int *trowA = A.tile_rowidx;
+    if (!trowA) {
+        TSG_TRY(cx.get(&trowA, (size_t)A.numtile + 1));
+        k_crow<<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(A.tile_ptr, tilemA, trowA);
+    }
+    if (A.numtile > 0)
+        k_unit_splits<<<grid_for(A.numtile, WG, 8192), WG, 0, s>>>(A.numtile, trowA, A.tile_ptr, A.tile_columnidx,
+                                                                  B.tile_ptr, B.tile_columnidx, uoff, C.tile_ptr,
+                                                                  C.tile_columnidx, sbase, split);
+    TSG_HIP(hipGetLastError());
+    if (trowA != A.tile_rowidx) cx.put(trowA);
+    const ABView V{A.tile_ptr, A.tile_columnidx, A.tile_nnz, A.tile_csr_Col, A.tile_csr_Value,
+                   B.tile_ptr, B.tile_columnidx, B.rm_mask, B.rm_rowstart, B.tile_csr_Col, B.tile_csr_Value,
+                   split, sbase};
     const int gu = grid_for(maxu, 1, 16384);
     if (numblkC > 0)
         k_step2<TM, TN><<<gu, WG, 0, s>>>(uoff, urow, tilemA, V, C.tile_ptr, C.tile_columnidx, C.tile_nnz, unit_rc);
     TSG_HIP(hipGetLastError());
     TSG_TRY(scan_exclusive_i32(cx, C.tile_nnz, (long)numblkC + 1, s));
-    int nnzC = 0;
-    TSG_TRY(read_i32(cx, C.tile_nnz + numblkC, &nnzC, s));
-    C.nnz = nnzC;
-    int *unit_rb = nullptr;
     if (csr_out) {
         csr_out->m = A.m;
         csr_out->n = B.n;
-        csr_out->nnz = nnzC;
         TSG_TRY(cx.get(&csr_out->rowpointer, (size_t)A.m + 1));
-        TSG_TRY(cx.get(&csr_out->columnindex, (size_t)nnzC + 1));
-        TSG_TRY(cx.get(&csr_out->value, (size_t)nnzC + 1));
         TSG_TRY(cx.get(&unit_rb, (size_t)maxu * TM));
         k_set_i32<<<1, 1, 0, s>>>(csr_out->rowpointer + A.m, 0);
         if (tilemA > 0)
@@ -1237,27 +1423,37 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
         TSG_HIP(hipGetLastError());
         TSG_TRY(scan_exclusive_i32(cx, csr_out->rowpointer, (long)A.m + 1, s));
     }
+    int nnzC = 0;
+    TSG_TRY(read_i32(cx, C.tile_nnz + numblkC, &nnzC, s));
+    C.nnz = nnzC;
     if (ev) TSG_HIP(hipEventRecord(ev[2], s));
     // ---- step 3 ----
-    TSG_TRY(cx.get(&C.tile_csr_Ptr, nb1 * TM));
-    TSG_TRY(cx.get(&C.tile_csr_Col, (size_t)nnzC + 1));
-    TSG_TRY(cx.get(&C.tile_csr_Value, (size_t)nnzC + 1));
-    if (nnzC > 0) {
-        if (csr_out)
-            k_step3<TM, TN, true><<<gu, WG, 0, s>>>(uoff, urow, tilemA, A.m, V, C.tile_ptr, C.tile_columnidx,
-                                                     C.tile_nnz, C.tile_csr_Ptr, C.tile_csr_Col, C.tile_csr_Value,
-                                                     unit_rb, csr_out->rowpointer, csr_out->columnindex,
-                                                     csr_out->value);
-        else
-            k_step3<TM, TN, false><<<gu, WG, 0, s>>>(uoff, urow, tilemA, A.m, V, C.tile_ptr, C.tile_columnidx,
-                                                      C.tile_nnz, C.tile_csr_Ptr, C.tile_csr_Col, C.tile_csr_Value,
-                                                      nullptr, nullptr, nullptr, nullptr);
+    if (csr_out) {
+        csr_out->nnz = nnzC;
+        TSG_TRY(cx.get(&csr_out->columnindex, (size_t)nnzC + 1));
+        TSG_TRY(cx.get(&csr_out->value, (size_t)nnzC + 1));
+        if (nnzC > 0)
+            k_step3<TM, TN, true, false><<<gu, WG, 0, s>>>(uoff, urow, tilemA, V, C.tile_ptr, C.tile_columnidx,
+                                                           C.tile_nnz, unit_rb, csr_out->rowpointer,
+                                                           csr_out->columnindex, csr_out->value, nullptr, nullptr,
+                                                           nullptr, g_ablate);
+    } else {
+        TSG_TRY(cx.get(&C.tile_csr_Ptr, nb1 * TM));
+        TSG_TRY(cx.get(&C.tile_csr_Col, (size_t)nnzC + 1));
+        TSG_TRY(cx.get(&C.tile_csr_Value, (size_t)nnzC + 1));
+        if (nnzC > 0)
+            k_step3<TM, TN, false, true><<<gu, WG, 0, s>>>(uoff, urow, tilemA, V, C.tile_ptr, C.tile_columnidx,
+                                                           C.tile_nnz, nullptr, nullptr, nullptr, nullptr,
+                                                           C.tile_csr_Ptr, C.tile_csr_Col, C.tile_csr_Value,
+                                                           g_ablate);
     }
     TSG_HIP(hipGetLastError());
     cx.put(uoff);
     cx.put(urow);
     cx.put(unit_rc);
     cx.put(unit_rb);
+    cx.put(split);
+    cx.put(sbase);
     if (ev) TSG_HIP(hipEventRecord(ev[3], s));
     if (st) {
         st->numblkC = numblkC;
@@ -1277,11 +1473,6 @@ __global__ void k_zero_empty_ptr(const int *nnzoff, int numtile, int tm, u16 *Pt
                 for (int w = 0; w < mw; ++w) mask[x * mw + w] = 0;
         }
     }
-}
-
-__global__ void k_crow(const int *Cptr, int tilem, int *Crow) {
-    for (int i = blockIdx.x * WG + threadIdx.x; i < tilem; i += gridDim.x * WG)
-        for (int t = Cptr[i]; t < Cptr[i + 1]; ++t) Crow[t] = i;
 }
 
 // Reference-layout extras for the host drop-in API: zero Ptr of empty C tiles
@@ -1312,11 +1503,27 @@ __global__ __launch_bounds__(WG) void k_rm2csc(const int *tile_ptr, const int *t
     }
 }
 
+__global__ __launch_bounds__(WG) void k_build_b_aux(int numtile, int tn, int mw, const int *rm2csc, const int *Bnnz,
+                                                     const u16 *PtrB, const u16 *maskB, u16 *rm_mask, int *rm_rowstart) {
+    for (int t = blockIdx.x * WG + threadIdx.x; t < numtile; t += gridDim.x * WG) {
+        const int bc = rm2csc[t];
+        for (int c = 0; c < tn; ++c) rm_rowstart[(size_t)t * (tn + 1) + c] = Bnnz[bc] + PtrB[(size_t)bc * tn + c];
+        rm_rowstart[(size_t)t * (tn + 1) + tn] = Bnnz[bc + 1];
+        for (int k = 0; k < tn * mw; ++k) rm_mask[(size_t)t * tn * mw + k] = maskB[(size_t)bc * tn * mw + k];
+    }
+}
+
 int dev_rm2csc_from_structs(Context &cx, tsg_dev_tiles &B, hipStream_t s) {
     TSG_TRY(cx.get(&B.tile_rm2csc, (size_t)B.numtile + 1));
     if (B.numtile > 0)
         k_rm2csc<<<grid_for(B.numtile, WG, 8192), WG, 0, s>>>(B.tile_ptr, B.tile_columnidx, B.csc_tile_ptr,
                                                              B.csc_tile_rowidx, B.tilen, B.numtile, B.tile_rm2csc);
+    TSG_TRY(cx.get(&B.rm_mask, ((size_t)B.numtile + 1) * B.tile_m * (B.tile_n / 16)));
+    TSG_TRY(cx.get(&B.rm_rowstart, ((size_t)B.numtile + 1) * (B.tile_m + 1)));
+    if (B.numtile > 0)
+        k_build_b_aux<<<grid_for(B.numtile, WG, 8192), WG, 0, s>>>(B.numtile, B.tile_m, B.tile_n / 16, B.tile_rm2csc,
+                                                                  B.tile_nnz, B.tile_csr_Ptr, B.mask, B.rm_mask,
+                                                                  B.rm_rowstart);
     TSG_HIP(hipGetLastError());
     return TSG_OK;
 }
