@@ -630,7 +630,7 @@ int tsg_dev_spgemm(tsg_context *ctx, const tsg_dev_csr *A, const tsg_dev_csr *B,
     TSG_TRY(dev_csr2tile_col_major(cx, *B, tm, tn, tB, s));
     TSG_HIP(hipEventRecord(cx.ev[9], s));
     // tile2csr is fused into step 3's epilogue on this path (C tiles stay materialised)
-    TSG_TRY(dev_tilespgemm(cx, tA, tB, tC, &st, s, cx.ev, C));
+    TSG_TRY(dev_tilespgemm(cx, tA, tB, tC, &st, s, cx.ev, C, A, B));
     TSG_HIP(hipEventRecord(cx.ev[10], s));
     TSG_HIP(hipEventSynchronize(cx.ev[10]));
     auto h1 = std::chrono::steady_clock::now();

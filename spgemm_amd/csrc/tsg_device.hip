@@ -992,6 +992,61 @@ __global__ __launch_bounds__(WG) void k_unit_splits(int numtileA, const int *tro
     }
 }
 
+// Element-streaming numeric: per (unit, A CSR entry of the C tile row) the
+// first position in B's CSR row whose column reaches the unit's column range.
+struct ECsr {
+    int m;
+    const int *rpA, *ciA;
+    const double *vA;
+    const int *rpB, *ciB;
+    const double *vB;
+    const int *esplit;
+    const long long *ebase;
+};
+
+template <int TM>
+__global__ void k_esplit_counts(const int *uoff, const int *rpA, int m, int tilem, long long *ebase) {
+    for (int i = blockIdx.x * WG + threadIdx.x; i < tilem; i += gridDim.x * WG) {
+        const int e0 = rpA[i * TM], e1 = rpA[min((long)(i + 1) * TM, (long)m)];
+        ebase[i] = (long long)(uoff[i + 1] - uoff[i]) * (e1 - e0);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) ebase[tilem] = 0;
+}
+
+template <int TM>
+__global__ __launch_bounds__(WG) void k_esplit(int m, const int *rpA, const int *ciA, const int *rpB, const int *ciB,
+                                               const int *uoff, const int *Cptr, const int *Ccol,
+                                               const long long *ebase, int *esplit) {
+    const int nnzA = rpA[m];
+    for (int p = blockIdx.x * WG + threadIdx.x; p < nnzA; p += gridDim.x * WG) {
+        int lo = 0, hi = m - 1;  // row of entry p (last R with rpA[R] <= p)
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (rpA[mid] <= p) lo = mid; else hi = mid - 1;
+        }
+        const int i = lo / TM;
+        const int e0 = rpA[i * TM], ei = rpA[min((i + 1) * TM, m)] - e0;
+        const int nu = uoff[i + 1] - uoff[i];
+        const int k = ciA[p];
+        int pos = rpB[k];
+        const int be = rpB[k + 1];
+        int *out = esplit + ebase[i] + (p - e0);
+        for (int q = 0; q < nu; ++q) {
+            if (q) pos = gallop_ge(ciB, pos, be, Ccol[Cptr[i] + q * CH] * TM);
+            out[(long)q * ei] = pos;
+        }
+    }
+}
+
+__global__ __launch_bounds__(WG) void k_rows_unsorted(const int *rp, const int *ci, int m, int *flag) {
+    for (int R = blockIdx.x * WG + threadIdx.x; R < m; R += gridDim.x * WG)
+        for (int p = rp[R] + 1; p < rp[R + 1]; ++p)
+            if (ci[p] < ci[p - 1]) {
+                *flag = 1;
+                break;
+            }
+}
+
 // Products of A tiles [ab, ab+na) (row i, unit q of nu, A tiles from a0) that
 // fall in the unit's column range, from the precomputed split points:
 // bs[], off[] (exclusive scan of the counts, off[na] = total).
@@ -1080,7 +1135,7 @@ __device__ __forceinline__ bool unit_masks(const ABView &V, int i, int q, int nu
 // ---------------------------------------------------------------------------
 template <int TM, int TN>
 __global__ __launch_bounds__(WG) void k_step2(const int *uoff, const int *urow, int tilem, ABView V, const int *Cptr,
-                                              const int *Ccol, int *nnzC, int *unit_rc) {
+                                              const int *Ccol, int *nnzC, int *unit_rc, u16 *maskC) {
     constexpr int MW = CM<TM>::MW, TW32 = CM<TM>::TW32;
     __shared__ __align__(16) u32 s_mask[CH * TW32];
     __shared__ int s_cols[CH];
@@ -1113,6 +1168,13 @@ __global__ __launch_bounds__(WG) void k_step2(const int *uoff, const int *urow, 
                 nz += c;
             }
             nnzC[t0 + j] = nz;
+            if (nz) {  // C row masks of non-empty tiles (device-internal, as in the reference)
+                static_assert((CM<TM>::TW32 % 4) == 0, "mask tile must be whole uint4");
+                const uint4 *src = reinterpret_cast<const uint4 *>(tile);
+                uint4 *dst = reinterpret_cast<uint4 *>(maskC + (size_t)(t0 + j) * CM<TM>::TW);
+#pragma unroll
+                for (int k = 0; k < TW32 / 4; ++k) dst[k] = src[k];
+            }
         }
 #pragma unroll
         for (int r = 0; r < TM; ++r) {
@@ -1146,19 +1208,21 @@ __device__ __forceinline__ int lds_rank(const u32 *tile, int r, int x) {
     return rank;
 }
 
-template <int TM, int TN, bool WCSR, bool WTILE>
-__global__ __launch_bounds__(WG) void k_step3(const int *uoff, const int *urow, int tilem, ABView V, const int *Cptr,
-                                              const int *Ccol, const int *nnzoff, const int *unit_rb,
-                                              const int *rowptr, int *csr_col, double *csr_val, u16 *PtrC, u16 *ColC,
-                                              double *ValC, int ablate) {
+template <int TM, int TN, bool WCSR, bool WTILE, bool ELEM>
+__global__ __launch_bounds__(WG) void k_step3(const int *uoff, const int *urow, int tilem, ABView V, ECsr E,
+                                              const int *Cptr, const int *Ccol, const int *nnzoff, const u16 *maskC,
+                                              const int *unit_rb, const int *rowptr, int *csr_col, double *csr_val,
+                                              u16 *PtrC, u16 *ColC, double *ValC, int ablate) {
     constexpr int MW = CM<TM>::MW, TW32 = CM<TM>::TW32;
     constexpr int LANES = WG / TM;  // P phase: TM rows x LANES contiguous tile blocks
     __shared__ __align__(16) u32 s_mask[CH * TW32];
     __shared__ __align__(16) double acc[S3_NZCAP];
+    __shared__ __align__(16) double s_va[WG];
     __shared__ int s_ccol[S3_NZCAP];
     __shared__ int s_cols[CH];
     __shared__ int s_off[CH + 1];
     __shared__ u16 s_pre[CH * TM];
+    __shared__ unsigned char s_r[WG];
     __shared__ int s_cnt[TM];
     __shared__ int s_rowoff[TM + 1];
     __shared__ int s_carry[TM];
@@ -1170,16 +1234,19 @@ __global__ __launch_bounds__(WG) void k_step3(const int *uoff, const int *urow, 
         const int ns = min(CH, Cptr[i + 1] - t0);
         const int nzbase = nnzoff[t0];
         if (nnzoff[t0 + ns] == nzbase) continue;  // uniform: the unit's tiles are all empty
-        const int a0 = V.Aptr[i], a1 = V.Aptr[i + 1];
-        unit_load_cols_zero<TM>(Ccol, t0, ns, s_cols, s_mask);
+        const int q = u - uoff[i], nu = uoff[i + 1] - uoff[i];
+        for (int j = threadIdx.x; j < ns; j += WG) s_cols[j] = Ccol[t0 + j];
         for (int j = threadIdx.x; j <= ns; j += WG) s_off[j] = nnzoff[t0 + j] - nzbase;
         if (threadIdx.x < TM) s_carry[threadIdx.x] = WCSR ? unit_rb[(long)u * TM + threadIdx.x] : 0;
         __syncthreads();
-        int tot1 = 0;
-        bool single = true;
-        const int q = u - uoff[i], nu = uoff[i + 1] - uoff[i];
-        if (!(ablate & 1)) single = unit_masks<TM, TN>(V, i, q, nu, a0, a1, s_cols, ns, s_mask, L, &tot1);
-        else tot1 = unit_setup(V, i, q, nu, a0, a0, min(WG, a1 - a0), L);
+        // C row masks written by step 2 (non-empty tiles only; empty tiles -> 0)
+        for (int x = threadIdx.x; x < ns * (TW32 / 4); x += WG) {
+            const int j = x / (TW32 / 4), k = x - j * (TW32 / 4);
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if (s_off[j + 1] > s_off[j]) v = reinterpret_cast<const uint4 *>(maskC + (size_t)(t0 + j) * CM<TM>::TW)[k];
+            reinterpret_cast<uint4 *>(s_mask)[x] = v;
+        }
+        __syncthreads();
         if (WTILE) {  // Ptr of every non-empty tile (u16 x TM, vector stores)
             for (int j = threadIdx.x; j < ns; j += WG) {
                 if (s_off[j + 1] == s_off[j]) continue;
@@ -1259,26 +1326,71 @@ __global__ __launch_bounds__(WG) void k_step3(const int *uoff, const int *urow, 
             }
             // V: values
             if (!(ablate & 4)) {
-                for (int ab = a0; ab < a1; ab += WG) {
-                    const int na = min(WG, a1 - ab);
-                    const int tot = single ? tot1 : unit_setup(V, i, q, nu, a0, ab, na, L);
-                    unit_items(V, ab, na, tot, s_cols, ns, L, [&](int a, int b, int sl) {
-                        if (sl < s_lo || sl >= s_hi || s_off[sl + 1] == s_off[sl]) return;
-                        const int *br = V.rowsBrm + (size_t)b * (TN + 1);
-                        const u32 *tile = s_mask + sl * TW32;
-                        const int q1 = V.Annz[a + 1];
-                        for (int qa = V.Annz[a]; qa < q1; ++qa) {
-                            const int enc = V.ColA[qa];
-                            const int r = enc / TN, c = enc - (enc / TN) * TN;
-                            const int ks = br[c], ke = br[c + 1];
-                            if (ks >= ke) continue;
-                            const double va = V.ValA[qa];
-                            const int rb = s_rowoff[r] + (int)s_pre[sl * TM + r];
-                            for (int kb = ks; kb < ke; ++kb)
-                                atomicAdd(&acc[rb + lds_rank<TM>(tile, r, V.ColB[kb])], va * V.ValB[kb]);
+                if (ELEM) {
+                    // stream each A entry's B CSR row segment inside the unit's columns
+                    const int e0 = E.rpA[i * TM];
+                    const int ei = E.rpA[min((long)(i + 1) * TM, (long)E.m)] - e0;
+                    for (int eb = 0; eb < ei; eb += WG) {
+                        const int na = min(WG, ei - eb);
+                        int bs = 0, len = 0;
+                        if (threadIdx.x < na) {
+                            const int p = e0 + eb + threadIdx.x;
+                            int lo2 = i * TM, hi2 = min((i + 1) * TM, E.m) - 1;  // row of entry p
+                            while (lo2 < hi2) {
+                                const int mid = (lo2 + hi2 + 1) >> 1;
+                                if (E.rpA[mid] <= p) lo2 = mid; else hi2 = mid - 1;
+                            }
+                            s_r[threadIdx.x] = (unsigned char)(lo2 - i * TM);
+                            s_va[threadIdx.x] = E.vA[p];
+                            const int *sp = E.esplit + E.ebase[i] + (eb + threadIdx.x);
+                            bs = sp[(long)q * ei];
+                            const int be = (q + 1 < nu) ? sp[(long)(q + 1) * ei] : E.rpB[E.ciA[p] + 1];
+                            len = be - bs;
                         }
-                    });
-                    __syncthreads();
+                        int tot;
+                        const int off = block_excl_scan(len, &tot, L.red);
+                        L.bs[threadIdx.x] = bs;
+                        L.off[threadIdx.x] = off;
+                        __syncthreads();
+                        for (int it = threadIdx.x; it < tot; it += WG) {
+                            int lo3 = 0, hi3 = na - 1;
+                            while (lo3 < hi3) {
+                                const int mid = (lo3 + hi3 + 1) >> 1;
+                                if (L.off[mid] <= it) lo3 = mid; else hi3 = mid - 1;
+                            }
+                            const int pb = L.bs[lo3] + (it - L.off[lo3]);
+                            const int x = E.ciB[pb];
+                            const int sl = lower_bound_dev(s_cols, s_lo, s_hi, x / TM);
+                            if (sl >= s_hi || s_cols[sl] != x / TM) continue;  // other pass of this unit
+                            const int r = s_r[lo3];
+                            const int rb = s_rowoff[r] + (int)s_pre[sl * TM + r];
+                            atomicAdd(&acc[rb + lds_rank<TM>(s_mask + sl * TW32, r, x % TM)], s_va[lo3] * E.vB[pb]);
+                        }
+                        __syncthreads();
+                    }
+                } else {
+                    const int a0 = V.Aptr[i], a1 = V.Aptr[i + 1];
+                    for (int ab = a0; ab < a1; ab += WG) {
+                        const int na = min(WG, a1 - ab);
+                        const int tot = unit_setup(V, i, q, nu, a0, ab, na, L);
+                        unit_items(V, ab, na, tot, s_cols, ns, L, [&](int a, int b, int sl) {
+                            if (sl < s_lo || sl >= s_hi || s_off[sl + 1] == s_off[sl]) return;
+                            const int *br = V.rowsBrm + (size_t)b * (TN + 1);
+                            const u32 *tile = s_mask + sl * TW32;
+                            const int q1 = V.Annz[a + 1];
+                            for (int qa = V.Annz[a]; qa < q1; ++qa) {
+                                const int enc = V.ColA[qa];
+                                const int r = enc / TN, c = enc - (enc / TN) * TN;
+                                const int ks = br[c], ke = br[c + 1];
+                                if (ks >= ke) continue;
+                                const double va = V.ValA[qa];
+                                const int rb = s_rowoff[r] + (int)s_pre[sl * TM + r];
+                                for (int kb = ks; kb < ke; ++kb)
+                                    atomicAdd(&acc[rb + lds_rank<TM>(tile, r, V.ColB[kb])], va * V.ValB[kb]);
+                            }
+                        });
+                        __syncthreads();
+                    }
                 }
             }
             // W: outputs of the pass
@@ -1326,7 +1438,8 @@ __global__ __launch_bounds__(WG) void k_step3(const int *uoff, const int *urow, 
 static int g_ablate = -1;
 
 int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_dev_tiles &C,
-                   tsg_stats *st, hipStream_t s, hipEvent_t *ev, tsg_dev_csr *csr_out) {
+                   tsg_stats *st, hipStream_t s, hipEvent_t *ev, tsg_dev_csr *csr_out, const tsg_dev_csr *Acsr,
+                   const tsg_dev_csr *Bcsr) {
     if (g_ablate < 0) g_ablate = getenv("TSG_ABLATE") ? atoi(getenv("TSG_ABLATE")) : 0;
     constexpr int TM = 16, TN = 16;
     if (A.tile_m != TM || A.tile_n != TN || B.tile_m != TN || B.tile_n != TM) return TSG_ERR_UNSUPPORTED;
@@ -1378,6 +1491,7 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     TSG_TRY(cx.get(&urow, (size_t)maxu));
     TSG_TRY(cx.get(&unit_rc, (size_t)maxu * TM));
     TSG_TRY(cx.get(&C.tile_nnz, nb1));
+    TSG_TRY(cx.get(&C.mask, nb1 * CM<TM>::TW));
     k_units_per_row<<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(C.tile_ptr, tilemA, uoff);
     TSG_TRY(scan_exclusive_i32(cx, uoff, (long)tilemA + 1, s));
     k_unit_rows<<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(uoff, tilemA, urow);
@@ -1408,7 +1522,8 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
                    split, sbase};
     const int gu = grid_for(maxu, 1, 16384);
     if (numblkC > 0)
-        k_step2<TM, TN><<<gu, WG, 0, s>>>(uoff, urow, tilemA, V, C.tile_ptr, C.tile_columnidx, C.tile_nnz, unit_rc);
+        k_step2<TM, TN><<<gu, WG, 0, s>>>(uoff, urow, tilemA, V, C.tile_ptr, C.tile_columnidx, C.tile_nnz, unit_rc,
+                                          C.mask);
     TSG_HIP(hipGetLastError());
     TSG_TRY(scan_exclusive_i32(cx, C.tile_nnz, (long)numblkC + 1, s));
     if (csr_out) {
@@ -1428,25 +1543,63 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     C.nnz = nnzC;
     if (ev) TSG_HIP(hipEventRecord(ev[2], s));
     // ---- step 3 ----
+    // Element-streaming values when the CSR operands are at hand and B's rows
+    // are column-sorted (split points need sorted rows); else the tile path.
+    ECsr E{};
+    int *esplit = nullptr;
+    long long *ebase = nullptr;
+    bool elem = csr_out && Acsr && Bcsr && Acsr->m == A.m && Bcsr->m == B.m && Acsr->nnz > 0 && !(g_ablate & 16);
+    if (elem) {
+        int *flag = nullptr;
+        TSG_TRY(cx.get(&flag, 1));
+        TSG_HIP(hipMemsetAsync(flag, 0, sizeof(int), s));
+        if (Bcsr->m > 0)
+            k_rows_unsorted<<<grid_for(Bcsr->m, WG, 8192), WG, 0, s>>>(Bcsr->rowpointer, Bcsr->columnindex, Bcsr->m,
+                                                                       flag);
+        int unsorted = 0;
+        TSG_TRY(read_i32(cx, flag, &unsorted, s));
+        cx.put(flag);
+        elem = !unsorted;
+    }
+    if (elem) {
+        TSG_TRY(cx.get(&ebase, (size_t)tilemA + 1));
+        k_esplit_counts<TM><<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(uoff, Acsr->rowpointer, A.m, tilemA, ebase);
+        TSG_TRY(scan_exclusive_i64(cx, ebase, (long)tilemA + 1, s));
+        long long ne = 0;
+        TSG_TRY(read_i64(cx, ebase + tilemA, &ne, s));
+        TSG_TRY(cx.get(&esplit, (size_t)ne + 1));
+        k_esplit<TM><<<grid_for(Acsr->nnz, WG, 16384), WG, 0, s>>>(A.m, Acsr->rowpointer, Acsr->columnindex,
+                                                                   Bcsr->rowpointer, Bcsr->columnindex, uoff,
+                                                                   C.tile_ptr, C.tile_columnidx, ebase, esplit);
+        TSG_HIP(hipGetLastError());
+        E = ECsr{A.m, Acsr->rowpointer, Acsr->columnindex, Acsr->value, Bcsr->rowpointer, Bcsr->columnindex,
+                 Bcsr->value, esplit, ebase};
+    }
     if (csr_out) {
         csr_out->nnz = nnzC;
         TSG_TRY(cx.get(&csr_out->columnindex, (size_t)nnzC + 1));
         TSG_TRY(cx.get(&csr_out->value, (size_t)nnzC + 1));
-        if (nnzC > 0)
-            k_step3<TM, TN, true, false><<<gu, WG, 0, s>>>(uoff, urow, tilemA, V, C.tile_ptr, C.tile_columnidx,
-                                                           C.tile_nnz, unit_rb, csr_out->rowpointer,
-                                                           csr_out->columnindex, csr_out->value, nullptr, nullptr,
-                                                           nullptr, g_ablate);
+        if (nnzC > 0) {
+            if (elem)
+                k_step3<TM, TN, true, false, true><<<gu, WG, 0, s>>>(
+                    uoff, urow, tilemA, V, E, C.tile_ptr, C.tile_columnidx, C.tile_nnz, C.mask, unit_rb,
+                    csr_out->rowpointer, csr_out->columnindex, csr_out->value, nullptr, nullptr, nullptr, g_ablate);
+            else
+                k_step3<TM, TN, true, false, false><<<gu, WG, 0, s>>>(
+                    uoff, urow, tilemA, V, E, C.tile_ptr, C.tile_columnidx, C.tile_nnz, C.mask, unit_rb,
+                    csr_out->rowpointer, csr_out->columnindex, csr_out->value, nullptr, nullptr, nullptr, g_ablate);
+        }
     } else {
         TSG_TRY(cx.get(&C.tile_csr_Ptr, nb1 * TM));
         TSG_TRY(cx.get(&C.tile_csr_Col, (size_t)nnzC + 1));
         TSG_TRY(cx.get(&C.tile_csr_Value, (size_t)nnzC + 1));
         if (nnzC > 0)
-            k_step3<TM, TN, false, true><<<gu, WG, 0, s>>>(uoff, urow, tilemA, V, C.tile_ptr, C.tile_columnidx,
-                                                           C.tile_nnz, nullptr, nullptr, nullptr, nullptr,
-                                                           C.tile_csr_Ptr, C.tile_csr_Col, C.tile_csr_Value,
-                                                           g_ablate);
+            k_step3<TM, TN, false, true, false><<<gu, WG, 0, s>>>(
+                uoff, urow, tilemA, V, E, C.tile_ptr, C.tile_columnidx, C.tile_nnz, C.mask, nullptr, nullptr,
+                nullptr, nullptr, C.tile_csr_Ptr, C.tile_csr_Col, C.tile_csr_Value, g_ablate);
     }
+    cx.put(esplit);
+    cx.put(ebase);
     TSG_HIP(hipGetLastError());
     cx.put(uoff);
     cx.put(urow);

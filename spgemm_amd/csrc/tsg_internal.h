@@ -84,9 +84,11 @@ int dev_csr2tile_row_major(Context &cx, const tsg_dev_csr &A, int tm, int tn, ts
                            hipStream_t s);
 int dev_csr2tile_col_major(Context &cx, const tsg_dev_csr &B, int tm, int tn, tsg_dev_tiles &out,
                            hipStream_t s);
-// csr_out != nullptr: step 3 also scatters C into CSR (tile2csr fused into its epilogue)
+// csr_out != nullptr: step 3 also scatters C into CSR (tile2csr fused into its epilogue).
+// Acsr/Bcsr (nullable): the CSR operands, enabling step 3's element-streaming value pass.
 int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_dev_tiles &C,
-                   tsg_stats *st, hipStream_t s, hipEvent_t *ev_marks, tsg_dev_csr *csr_out);
+                   tsg_stats *st, hipStream_t s, hipEvent_t *ev_marks, tsg_dev_csr *csr_out,
+                   const tsg_dev_csr *Acsr = nullptr, const tsg_dev_csr *Bcsr = nullptr);
 int dev_tile2csr(Context &cx, const tsg_dev_tiles &C, tsg_dev_csr &out, hipStream_t s);
 
 // read a device int / long long synchronously through pinned memory
