@@ -15,9 +15,9 @@ import numpy as np
 def tile_row_work(rowptr_a, col_a, rowptr_b, m, tile_m):
     """Element-level intermediate products per A tile row (sum of B row lengths)."""
     blen = np.diff(rowptr_b.astype(np.int64))
-    per_entry = blen[col_a]
-    per_row = np.add.reduceat(per_entry, rowptr_a[:-1]) if len(per_entry) else np.zeros(m, np.int64)
-    per_row = np.where(np.diff(rowptr_a) > 0, per_row, 0)
+    cum = np.concatenate([[0], np.cumsum(blen[col_a])])
+    rp = np.asarray(rowptr_a, dtype=np.int64)
+    per_row = cum[rp[1:]] - cum[rp[:-1]]
     tilem = (m + tile_m - 1) // tile_m
     pad = np.zeros(tilem * tile_m, dtype=np.int64)
     pad[:m] = per_row

@@ -1,0 +1,108 @@
+"""Multi-rank path on CPU (gloo, world_size 2 and 3): work partition of A's tile
+rows, row slicing, per-rank block products and the gather of C row blocks to
+rank 0 (spgemm_amd/dist.py).  On the GPU the per-rank block
+product is the HIP pipeline and the backend is nccl (= RCCL); here each rank's
+block is computed by the oracle so the partition/gather logic is checked
+against the oracle's full product without a GPU.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import _oracle as O
+from spgemm_amd import dist as tdist
+from spgemm_amd import synth
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _matrix(kind):
+    if kind == "powerlaw":
+        return synth.random_csr(700, 700, density=0.004, seed=5)
+    if kind == "aat":
+        return synth.random_csr(300, 520, density=0.01, seed=9)
+    return synth.random_csr(2, 2, density=0.0, seed=1)  # all-empty
+
+
+def _worker(rank, world, port, kind, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m, n, rp, ci, vv = _matrix(kind)
+        if kind == "aat":
+            oB = O.transpose(O.OMat.from_csr(m, n, rp, ci, vv))
+        else:
+            oB = O.OMat.from_csr(m, n, rp, ci, vv)
+        mb, nb, rpb, cib, vvb = oB.csr()
+        work = tdist.tile_row_work(rp, ci, rpb, m, 16)
+        parts = tdist.partition_tile_rows(work, world)
+        t0, t1 = parts[rank]
+        mblk, rpk, cik, vvk = tdist.slice_rows(m, rp, ci, vv, t0 * 16, t1 * 16)
+        Ck = O.gustavson(O.OMat.from_csr(mblk, n, rpk, cik, vvk), oB)
+        _, _, crp, cci, cvv = Ck.csr()
+        out = tdist.gather_csr_blocks(torch.from_numpy(crp.copy()), torch.from_numpy(cci.copy()),
+                                      torch.from_numpy(cvv.copy()), rank, world)
+        if rank == 0:
+            q.put(("ok", parts, [x.numpy() for x in out]))
+        else:
+            assert out is None
+    except Exception as e:  # surface worker failures to the parent
+        q.put(("err", repr(e), None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("kind", ["powerlaw", "aat", "empty"])
+def test_row_block_partition_and_gather_matches_full_product(world, kind):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, kind, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    status, parts, got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert status == "ok", parts
+    m, n, rp, ci, vv = _matrix(kind)
+    oA = O.OMat.from_csr(m, n, rp, ci, vv)
+    oB = O.transpose(oA) if kind == "aat" else O.OMat.alias(oA)
+    _, _, erp, eci, evv = O.gustavson(oA, oB).csr()
+    # the ranges tile [0, tilem) contiguously
+    tilem = (m + 15) // 16
+    assert parts[0][0] == 0 and parts[-1][1] == tilem
+    assert all(parts[r][1] == parts[r + 1][0] for r in range(world - 1))
+    np.testing.assert_array_equal(got[0], erp)
+    np.testing.assert_array_equal(got[1], eci)
+    np.testing.assert_array_equal(got[2], evv)
+
+
+def test_partition_balances_work():
+    work = np.array([100, 1, 1, 1, 1, 100, 1, 1, 1, 1] * 10, dtype=np.int64)
+    parts = tdist.partition_tile_rows(work, 4)
+    loads = [work[a:b].sum() for a, b in parts]
+    assert max(loads) <= 1.3 * (work.sum() / 4)
+    # more ranks than tile rows: trailing ranks get empty ranges, still contiguous
+    parts = tdist.partition_tile_rows(np.array([5, 5]), 4)
+    assert parts[0][0] == 0 and parts[-1][1] == 2
+    assert all(a <= b for a, b in parts)
+
+
+def test_tile_row_work_is_nnzcub_per_tile_row():
+    m, n, rp, ci, vv = synth.random_csr(100, 100, density=0.05, seed=2)
+    w = tdist.tile_row_work(rp, ci, rp, m, 16)
+    blen = np.diff(rp)
+    ref = [sum(int(blen[ci[p]]) for p in range(rp[r0], rp[min(r0 + 16, m)])) for r0 in range(0, m, 16)]
+    np.testing.assert_array_equal(w, ref)
