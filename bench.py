@@ -78,6 +78,22 @@ def cpu_baseline(m, n, rp, ci, vv, mb, nb, rpb, cib, vvb, budget_s):
                       f"({cub} of the intermediate products), {t:.1f} s"}
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/<round>_pmc.json, written by tools/profile.sh: 2*FETCH_SIZE +
+    WRITE_SIZE, separate --pmc passes).  (None, None) when absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    hits = [v for k, v in d.items() if kernel in k and v.get("hbm_bytes_per_dispatch")]
+    if not hits:
+        return None, None
+    best = max(hits, key=lambda v: v["dispatches"] or 0)
+    return int(best["hbm_bytes_per_dispatch"]), os.path.relpath(files[-1], REPO)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -165,7 +181,12 @@ def main():
     dev_ms = med["t_csr2tile_ms"] + med["t_step1_ms"] + med["t_step2_ms"] + med["t_step3_ms"] + med["t_tile2csr_ms"]
     # SURVEY §8d algorithmic bytes (src/external/cusparse/main.cu:205-208), this rank's share
     b_alg = 4.0 * (mblk + 1) + 12.0 * len(ciblk) + 4.0 * (mb + 1) + 12.0 * len(cib) + 4.0 * (mblk + 1) + 12.0 * c.nnz
-    achieved = b_alg / (dev_ms * 1e-3) / 1e9
+    achieved_pipe = b_alg / (dev_ms * 1e-3) / 1e9
+    # dominant kernel: step 3 (reads the CSR operands, writes the CSR result = B_alg's
+    # terms), timed with HIP events around its launch on the call's stream
+    k3_ms = med["t_step3_kernel_ms"]
+    achieved = b_alg / (k3_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic("k_step3")
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -184,11 +205,15 @@ def main():
                        "numtileA": int(med["numtileA"]), "numblkC": int(med["numblkC"]),
                        "parallelism": f"row-block{world}" if world > 1 else "single"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                         "kernel": "device pipeline per step (B_alg of SURVEY §8d / HIP-event device time)",
-                         "algorithmic_bytes": int(b_alg), "device_ms": round(dev_ms, 4)},
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                         "traffic_source": traffic_src,
+                         "kernel": "k_step3 (numeric + fused tile2csr): B_alg of SURVEY §8d / HIP-event kernel time",
+                         "algorithmic_bytes": int(b_alg), "kernel_ms": round(k3_ms, 4),
+                         "pipeline": {"achieved": round(achieved_pipe, 2),
+                                      "frac": round(achieved_pipe / HBM_PEAK_GBS, 5),
+                                      "device_ms": round(dev_ms, 4)}},
             "stage_ms": {k: round(med[k], 4) for k in ("t_csr2tile_ms", "t_step1_ms", "t_step2_ms",
-                                                        "t_step3_ms", "t_tile2csr_ms", "t_malloc_ms",
+                                                        "t_step3_ms", "t_step3_kernel_ms", "t_tile2csr_ms", "t_malloc_ms",
                                                         "t_kern_ms", "t_e2e_ms")},
             "gflops_kern": round(2.0 * nnzcub_total / (med["t_kern_ms"] * 1e-3) / 1e9, 3) if world == 1 else None,
             "cpu_baseline": cpu,

@@ -75,6 +75,7 @@ typedef struct tsg_stats {
     long long nnzCub;      /* sum_{a in A} rowlen_B(col(a))                     */
     long long numtileA, numtileB, numblkC, nnzC;
     long long tile_products; /* tile-level intermediate products (step-1 work)  */
+    double t_step3_kernel_ms;  /* the step-3 numeric kernel alone (dominant kernel) */
 } tsg_stats;
 
 /* ---------------- library / device ---------------- */

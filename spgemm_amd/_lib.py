@@ -46,7 +46,8 @@ class Stats(C.Structure):
     _fields_ = [(n, C.c_double) for n in (
         "t_csr2tile_ms", "t_step1_ms", "t_step2_ms", "t_step3_ms", "t_tile2csr_ms",
         "t_malloc_ms", "t_kern_ms", "t_e2e_ms")] + [(n, C.c_longlong) for n in (
-            "nnzCub", "numtileA", "numtileB", "numblkC", "nnzC", "tile_products")]
+            "nnzCub", "numtileA", "numtileB", "numblkC", "nnzC", "tile_products")] + [
+            ("t_step3_kernel_ms", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -640,6 +640,7 @@ int tsg_dev_spgemm(tsg_context *ctx, const tsg_dev_csr *A, const tsg_dev_csr *B,
     st.t_step1_ms = ev_ms(cx.ev[0], cx.ev[1]);
     st.t_step2_ms = ev_ms(cx.ev[1], cx.ev[2]);
     st.t_step3_ms = ev_ms(cx.ev[2], cx.ev[3]);
+    st.t_step3_kernel_ms = ev_ms(cx.ev[4], cx.ev[5]);
     st.t_tile2csr_ms = ev_ms(cx.ev[3], cx.ev[10]);
     st.t_kern_ms = ev_ms(cx.ev[0], cx.ev[3]);
     st.t_e2e_ms = std::chrono::duration<double, std::milli>(h1 - h0).count();

@@ -923,9 +923,16 @@ __global__ void k_units_per_row(const int *Cptr, int tilem, int *nunits) {
     if (blockIdx.x == 0 && threadIdx.x == 0) nunits[tilem] = 0;
 }
 
-__global__ void k_unit_rows(const int *uoff, int tilem, int *urow) {
-    for (int i = blockIdx.x * WG + threadIdx.x; i < tilem; i += gridDim.x * WG)
-        for (int u = uoff[i]; u < uoff[i + 1]; ++u) urow[u] = i;
+// unit -> C tile row (urow) and the unit table {i, t0, nu, q << 9 | ns} of step 3
+__global__ void k_unit_rows(const int *uoff, const int *Cptr, int tilem, int *urow, int4 *utab) {
+    for (int i = blockIdx.x * WG + threadIdx.x; i < tilem; i += gridDim.x * WG) {
+        const int u0 = uoff[i], nu = uoff[i + 1] - u0, c0 = Cptr[i], c1 = Cptr[i + 1];
+        for (int q = 0; q < nu; ++q) {
+            urow[u0 + q] = i;
+            const int t0 = c0 + q * CH;
+            utab[u0 + q] = make_int4(i, t0, nu, (q << 9) | min(CH, c1 - t0));
+        }
+    }
 }
 
 // per (tile row, r): exclusive prefix of the unit row counts along the row's
@@ -1008,7 +1015,7 @@ template <int TM>
 __global__ void k_esplit_counts(const int *uoff, const int *rpA, int m, int tilem, long long *ebase) {
     for (int i = blockIdx.x * WG + threadIdx.x; i < tilem; i += gridDim.x * WG) {
         const int e0 = rpA[i * TM], e1 = rpA[min((long)(i + 1) * TM, (long)m)];
-        ebase[i] = (long long)(uoff[i + 1] - uoff[i]) * (e1 - e0);
+        ebase[i] = (long long)(uoff[i + 1] - uoff[i] + 1) * (e1 - e0);
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) ebase[tilem] = 0;
 }
@@ -1035,6 +1042,7 @@ __global__ __launch_bounds__(WG) void k_esplit(int m, const int *rpA, const int 
             if (q) pos = gallop_ge(ciB, pos, be, Ccol[Cptr[i] + q * CH] * TM);
             out[(long)q * ei] = pos;
         }
+        out[(long)nu * ei] = be;
     }
 }
 
@@ -1168,7 +1176,7 @@ __global__ __launch_bounds__(WG) void k_step2(const int *uoff, const int *urow, 
                 nz += c;
             }
             nnzC[t0 + j] = nz;
-            if (nz) {  // C row masks of non-empty tiles (device-internal, as in the reference)
+            {  // C row masks (all-zero for empty tiles); step 3 reads them back
                 static_assert((CM<TM>::TW32 % 4) == 0, "mask tile must be whole uint4");
                 const uint4 *src = reinterpret_cast<const uint4 *>(tile);
                 uint4 *dst = reinterpret_cast<uint4 *>(maskC + (size_t)(t0 + j) * CM<TM>::TW);
@@ -1208,67 +1216,139 @@ __device__ __forceinline__ int lds_rank(const u32 *tile, int r, int x) {
     return rank;
 }
 
+// k-th (0-based) set column of a row word (MSB-first: bit 15-c = column c)
+__device__ __forceinline__ int kth_col16(u32 v, int k) {
+    u32 w = __brev(v) >> 16;  // bit c = column c
+    for (int t = 0; t < k; ++t) w &= w - 1;
+    return __ffs(w) - 1;
+}
+
 template <int TM, int TN, bool WCSR, bool WTILE, bool ELEM>
-__global__ __launch_bounds__(WG) void k_step3(const int *uoff, const int *urow, int tilem, ABView V, ECsr E,
-                                              const int *Cptr, const int *Ccol, const int *nnzoff, const u16 *maskC,
-                                              const int *unit_rb, const int *rowptr, int *csr_col, double *csr_val,
-                                              u16 *PtrC, u16 *ColC, double *ValC, int ablate) {
-    constexpr int MW = CM<TM>::MW, TW32 = CM<TM>::TW32;
-    constexpr int LANES = WG / TM;  // P phase: TM rows x LANES contiguous tile blocks
+__global__ __launch_bounds__(WG) void k_step3(const int4 *utab, int nunits, ABView V, ECsr E, const int *Ccol,
+                                              const int *nnzoff, const u16 *maskC, const int *unit_rb,
+                                              const int *rowptr, int *csr_col, double *csr_val, u16 *PtrC,
+                                              u16 *ColC, double *ValC, int ablate) {
+    constexpr int MW = CM<TM>::MW, TW32 = CM<TM>::TW32, NV4 = TW32 / 4, NP = TM / 4;
+    static_assert(CH == WG, "one C tile per thread");
+    static_assert(TW32 % 4 == 0 && TM % 4 == 0, "mask tiles are whole uint4");
     __shared__ __align__(16) u32 s_mask[CH * TW32];
     __shared__ __align__(16) double acc[S3_NZCAP];
     __shared__ __align__(16) double s_va[WG];
-    __shared__ int s_ccol[S3_NZCAP];
+    __shared__ u16 s_pre[(CH + 1) * TM];  // [j][r]: row-r nonzeros of the unit's tiles [0, j)
     __shared__ int s_cols[CH];
-    __shared__ int s_off[CH + 1];
-    __shared__ u16 s_pre[CH * TM];
+    __shared__ int s_off[CH + 1];         // [j]: nonzeros of the unit's tiles [0, j)
+    __shared__ int s_rp[TM + 1];          // A CSR row starts of the tile row (ELEM)
     __shared__ unsigned char s_r[WG];
-    __shared__ int s_cnt[TM];
-    __shared__ int s_rowoff[TM + 1];
+    __shared__ int s_rowoff[TM + 1];      // per pass: CSR-order row offsets
+    __shared__ int s_rowbase[TM];         // per pass: rowoff[r] - pre[s_lo][r]
     __shared__ int s_carry[TM];
+    __shared__ u64 s_red64[WAVES * NP];
+    __shared__ int s_red[WAVES];
     __shared__ ProdLds L;
-    const int nunits = uoff[tilem];
+    const int j = threadIdx.x;
     for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
-        const int i = urow[u];
-        const int t0 = Cptr[i] + (u - uoff[i]) * CH;
-        const int ns = min(CH, Cptr[i + 1] - t0);
-        const int nzbase = nnzoff[t0];
-        if (nnzoff[t0 + ns] == nzbase) continue;  // uniform: the unit's tiles are all empty
-        const int q = u - uoff[i], nu = uoff[i + 1] - uoff[i];
-        for (int j = threadIdx.x; j < ns; j += WG) s_cols[j] = Ccol[t0 + j];
-        for (int j = threadIdx.x; j <= ns; j += WG) s_off[j] = nnzoff[t0 + j] - nzbase;
-        if (threadIdx.x < TM) s_carry[threadIdx.x] = WCSR ? unit_rb[(long)u * TM + threadIdx.x] : 0;
-        __syncthreads();
-        // C row masks written by step 2 (non-empty tiles only; empty tiles -> 0)
-        for (int x = threadIdx.x; x < ns * (TW32 / 4); x += WG) {
-            const int j = x / (TW32 / 4), k = x - j * (TW32 / 4);
-            uint4 v = make_uint4(0u, 0u, 0u, 0u);
-            if (s_off[j + 1] > s_off[j]) v = reinterpret_cast<const uint4 *>(maskC + (size_t)(t0 + j) * CM<TM>::TW)[k];
-            reinterpret_cast<uint4 *>(s_mask)[x] = v;
-        }
-        __syncthreads();
-        if (WTILE) {  // Ptr of every non-empty tile (u16 x TM, vector stores)
-            for (int j = threadIdx.x; j < ns; j += WG) {
-                if (s_off[j + 1] == s_off[j]) continue;
-                const u32 *tile = s_mask + j * TW32;
-                u16 p[TM];
-                int run = 0;
+        const int4 ut = utab[u];
+        const int i = ut.x, t0 = ut.y, nu = ut.z, q = ut.w >> 9, ns = ut.w & 511;
+        // ---- load: C masks (written by step 2) + columns; thread j owns tile j
+        u32 w[TW32];
+        int col = 0;
+        if (j < ns) {
+            const uint4 *src = reinterpret_cast<const uint4 *>(maskC + (size_t)(t0 + j) * CM<TM>::TW);
 #pragma unroll
-                for (int r = 0; r < TM; ++r) {
-                    p[r] = (u16)run;
-#pragma unroll
-                    for (int w = 0; w < MW; ++w) run += __popc(lds_row_word<TM>(tile, r, w));
-                }
-                uint4 *dst = reinterpret_cast<uint4 *>(PtrC + (size_t)(t0 + j) * TM);
-#pragma unroll
-                for (int k = 0; k < TM / 8; ++k)
-                    dst[k] = make_uint4(p[8 * k] | ((u32)p[8 * k + 1] << 16), p[8 * k + 2] | ((u32)p[8 * k + 3] << 16),
-                                        p[8 * k + 4] | ((u32)p[8 * k + 5] << 16),
-                                        p[8 * k + 6] | ((u32)p[8 * k + 7] << 16));
+            for (int k = 0; k < NV4; ++k) {
+                const uint4 v = src[k];
+                w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
             }
+            col = Ccol[t0 + j];
+        } else {
+#pragma unroll
+            for (int k = 0; k < TW32; ++k) w[k] = 0u;
         }
+        if (threadIdx.x < TM) s_carry[threadIdx.x] = WCSR ? unit_rb[(long)u * TM + threadIdx.x] : 0;
+        if (ELEM && threadIdx.x <= TM) s_rp[threadIdx.x] = E.rpA[min(i * TM + (int)threadIdx.x, E.m)];
+#pragma unroll
+        for (int k = 0; k < NV4; ++k)
+            reinterpret_cast<uint4 *>(s_mask + j * TW32)[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2],
+                                                                         w[4 * k + 3]);
+        s_cols[j] = col;
+        // ---- per-row counts (packed 4 x 16 bit) and tile totals, block-scanned over tiles
+        u64 pk[NP];
+        int tt = 0;
+#pragma unroll
+        for (int g = 0; g < NP; ++g) pk[g] = 0;
+#pragma unroll
+        for (int r = 0; r < TM; ++r) {
+            int c = 0;
+#pragma unroll
+            for (int ww = 0; ww < MW; ++ww) {
+                const int k = r * MW + ww;
+                c += __popc((w[k >> 1] >> ((k & 1) * 16)) & 0xffffu);
+            }
+            pk[r >> 2] += (u64)c << (16 * (r & 3));
+            tt += c;
+        }
+        u64 ipk[NP];
+#pragma unroll
+        for (int g = 0; g < NP; ++g) ipk[g] = wave_incl_scan(pk[g]);
+        int itt = wave_incl_scan(tt);
+        if (lane_id() == 63) {
+#pragma unroll
+            for (int g = 0; g < NP; ++g) s_red64[wave_id() * NP + g] = ipk[g];
+            s_red[wave_id()] = itt;
+        }
+        __syncthreads();
+        u64 tot64[NP];
+        int ttot = 0, toff = 0;
+#pragma unroll
+        for (int g = 0; g < NP; ++g) tot64[g] = 0;
+#pragma unroll
+        for (int wv = 0; wv < WAVES; ++wv) {
+            const bool before = wv < wave_id();
+#pragma unroll
+            for (int g = 0; g < NP; ++g) {
+                const u64 v = s_red64[wv * NP + g];
+                if (before) ipk[g] += v;
+                tot64[g] += v;
+            }
+            const int v = s_red[wv];
+            if (before) toff += v;
+            ttot += v;
+        }
+#pragma unroll
+        for (int r = 0; r < TM; ++r) {
+            const int g = r >> 2, sh = 16 * (r & 3);
+            s_pre[j * TM + r] = (u16)(((ipk[g] - pk[g]) >> sh) & 0xffffu);
+            if (j == WG - 1) s_pre[CH * TM + r] = (u16)((tot64[g] >> sh) & 0xffffu);
+        }
+        s_off[j] = toff + itt - tt;
+        if (j == WG - 1) s_off[CH] = ttot;
+        if (ttot == 0) {  // uniform: every tile of the unit is empty
+            __syncthreads();
+            continue;
+        }
+        if (WTILE && j < ns && tt > 0) {  // Ptr of the non-empty tile j (u16 x TM, vector stores)
+            u16 pp[TM];
+            int run = 0;
+#pragma unroll
+            for (int r = 0; r < TM; ++r) {
+                pp[r] = (u16)run;
+#pragma unroll
+                for (int ww = 0; ww < MW; ++ww) {
+                    const int k = r * MW + ww;
+                    run += __popc((w[k >> 1] >> ((k & 1) * 16)) & 0xffffu);
+                }
+            }
+            uint4 *dst = reinterpret_cast<uint4 *>(PtrC + (size_t)(t0 + j) * TM);
+#pragma unroll
+            for (int k = 0; k < TM / 8; ++k)
+                dst[k] = make_uint4(pp[8 * k] | ((u32)pp[8 * k + 1] << 16), pp[8 * k + 2] | ((u32)pp[8 * k + 3] << 16),
+                                    pp[8 * k + 4] | ((u32)pp[8 * k + 5] << 16),
+                                    pp[8 * k + 6] | ((u32)pp[8 * k + 7] << 16));
+        }
+        const int nzbase = WTILE ? nnzoff[t0] : 0;
+        __syncthreads();
         for (int s_lo = 0; s_lo < ns;) {
-            int lo = s_lo + 1, hi = ns;  // largest s_hi with nnz(s_lo..s_hi) <= NZCAP
+            int lo = s_lo + 1, hi = ns;  // largest s_hi with nnz(tiles s_lo..s_hi-1) <= NZCAP
             while (lo < hi) {
                 const int mid = (lo + hi + 1) >> 1;
                 if (s_off[mid] - s_off[s_lo] <= S3_NZCAP) lo = mid; else hi = mid - 1;
@@ -1279,72 +1359,44 @@ __global__ __launch_bounds__(WG) void k_step3(const int *uoff, const int *urow, 
                 s_lo = s_hi;
                 continue;
             }
-            // P: per-row counts, row offsets, per-(tile,row) prefixes, CSR columns
-            {
-                const int r = threadIdx.x / LANES, l = threadIdx.x - (threadIdx.x / LANES) * LANES;
-                const int nt = s_hi - s_lo, blk = (nt + LANES - 1) / LANES;
-                const int sb = s_lo + min(nt, l * blk), se = s_lo + min(nt, l * blk + blk);
-                int tot = 0;
-                for (int sx = sb; sx < se; ++sx)
-#pragma unroll
-                    for (int w = 0; w < MW; ++w) tot += __popc(lds_row_word<TM>(s_mask + sx * TW32, r, w));
-                int inc = tot;
-#pragma unroll
-                for (int d = 1; d < LANES; d <<= 1) {
-                    const int y = __shfl_up(inc, d, LANES);
-                    if (l >= d) inc += y;
+            int cnt_r = 0;
+            if (threadIdx.x < 64) {  // wave 0: per-row counts of the pass and their offsets
+                const int r = threadIdx.x;
+                const int p0 = r < TM ? (int)s_pre[s_lo * TM + r] : 0;
+                cnt_r = r < TM ? (int)s_pre[s_hi * TM + r] - p0 : 0;
+                const int inc = wave_incl_scan(cnt_r);
+                if (r < TM) {
+                    s_rowoff[r] = inc - cnt_r;
+                    s_rowbase[r] = inc - cnt_r - p0;
                 }
-                if (l == LANES - 1) s_cnt[r] = inc;
-                __syncthreads();
-                if (threadIdx.x == 0) {
-                    int run = 0;
-                    for (int rr = 0; rr < TM; ++rr) {
-                        s_rowoff[rr] = run;
-                        run += s_cnt[rr];
-                    }
-                    s_rowoff[TM] = run;
-                }
-                __syncthreads();
-                int pre = inc - tot;
-                int pos = s_rowoff[r] + pre;
-                for (int sx = sb; sx < se; ++sx) {
-                    s_pre[sx * TM + r] = (u16)pre;
-                    const int cb = s_cols[sx] * TM;
-#pragma unroll
-                    for (int w = 0; w < MW; ++w) {
-                        u32 v = lds_row_word<TM>(s_mask + sx * TW32, r, w);
-                        pre += __popc(v);
-                        while (v) {
-                            const int hb = 31 - __clz(v);  // highest set bit = lowest column (MSB-first)
-                            s_ccol[pos++] = cb + w * 16 + (15 - hb);
-                            v &= ~(1u << hb);
-                        }
-                    }
-                }
-                for (int e = threadIdx.x; e < nz; e += WG) acc[e] = 0.0;
-                __syncthreads();
+                if (r == TM - 1) s_rowoff[TM] = inc;
             }
-            // V: values
+            for (int e = threadIdx.x; e < nz; e += WG) acc[e] = 0.0;
+            __syncthreads();
+            // ---- V: values
             if (!(ablate & 4)) {
                 if (ELEM) {
-                    // stream each A entry's B CSR row segment inside the unit's columns
-                    const int e0 = E.rpA[i * TM];
-                    const int ei = E.rpA[min((long)(i + 1) * TM, (long)E.m)] - e0;
+                    const int e0 = s_rp[0], ei = s_rp[TM] - e0;
+                    const int *spbase = E.esplit + E.ebase[i];
+                    const bool narrow = s_lo > 0 || s_hi < ns;
+                    const int clo = s_cols[s_lo] * TM, chi = (s_cols[s_hi - 1] + 1) * TM;
                     for (int eb = 0; eb < ei; eb += WG) {
                         const int na = min(WG, ei - eb);
                         int bs = 0, len = 0;
                         if (threadIdx.x < na) {
                             const int p = e0 + eb + threadIdx.x;
-                            int lo2 = i * TM, hi2 = min((i + 1) * TM, E.m) - 1;  // row of entry p
-                            while (lo2 < hi2) {
-                                const int mid = (lo2 + hi2 + 1) >> 1;
-                                if (E.rpA[mid] <= p) lo2 = mid; else hi2 = mid - 1;
-                            }
-                            s_r[threadIdx.x] = (unsigned char)(lo2 - i * TM);
+                            int r = 0;
+#pragma unroll
+                            for (int rr = 1; rr < TM; ++rr) r += (s_rp[rr] <= p) ? 1 : 0;
+                            s_r[threadIdx.x] = (unsigned char)r;
                             s_va[threadIdx.x] = E.vA[p];
-                            const int *sp = E.esplit + E.ebase[i] + (eb + threadIdx.x);
+                            const int *sp = spbase + (eb + threadIdx.x);
                             bs = sp[(long)q * ei];
-                            const int be = (q + 1 < nu) ? sp[(long)(q + 1) * ei] : E.rpB[E.ciA[p] + 1];
+                            int be = sp[(long)(q + 1) * ei];
+                            if (narrow) {
+                                bs = lower_bound_dev(E.ciB, bs, be, clo);
+                                be = lower_bound_dev(E.ciB, bs, be, chi);
+                            }
                             len = be - bs;
                         }
                         int tot;
@@ -1360,11 +1412,13 @@ __global__ __launch_bounds__(WG) void k_step3(const int *uoff, const int *urow, 
                             }
                             const int pb = L.bs[lo3] + (it - L.off[lo3]);
                             const int x = E.ciB[pb];
+                            const double vb = E.vB[pb];
                             const int sl = lower_bound_dev(s_cols, s_lo, s_hi, x / TM);
-                            if (sl >= s_hi || s_cols[sl] != x / TM) continue;  // other pass of this unit
+                            if (sl >= s_hi || s_cols[sl] != x / TM) continue;  // other pass
                             const int r = s_r[lo3];
-                            const int rb = s_rowoff[r] + (int)s_pre[sl * TM + r];
-                            atomicAdd(&acc[rb + lds_rank<TM>(s_mask + sl * TW32, r, x % TM)], s_va[lo3] * E.vB[pb]);
+                            atomicAdd(&acc[s_rowbase[r] + (int)s_pre[sl * TM + r] +
+                                           lds_rank<TM>(s_mask + sl * TW32, r, x % TM)],
+                                      s_va[lo3] * vb);
                         }
                         __syncthreads();
                     }
@@ -1374,7 +1428,7 @@ __global__ __launch_bounds__(WG) void k_step3(const int *uoff, const int *urow, 
                         const int na = min(WG, a1 - ab);
                         const int tot = unit_setup(V, i, q, nu, a0, ab, na, L);
                         unit_items(V, ab, na, tot, s_cols, ns, L, [&](int a, int b, int sl) {
-                            if (sl < s_lo || sl >= s_hi || s_off[sl + 1] == s_off[sl]) return;
+                            if (sl < s_lo || sl >= s_hi) return;
                             const int *br = V.rowsBrm + (size_t)b * (TN + 1);
                             const u32 *tile = s_mask + sl * TW32;
                             const int q1 = V.Annz[a + 1];
@@ -1384,7 +1438,7 @@ __global__ __launch_bounds__(WG) void k_step3(const int *uoff, const int *urow, 
                                 const int ks = br[c], ke = br[c + 1];
                                 if (ks >= ke) continue;
                                 const double va = V.ValA[qa];
-                                const int rb = s_rowoff[r] + (int)s_pre[sl * TM + r];
+                                const int rb = s_rowbase[r] + (int)s_pre[sl * TM + r];
                                 for (int kb = ks; kb < ke; ++kb)
                                     atomicAdd(&acc[rb + lds_rank<TM>(tile, r, V.ColB[kb])], va * V.ValB[kb]);
                             }
@@ -1393,31 +1447,46 @@ __global__ __launch_bounds__(WG) void k_step3(const int *uoff, const int *urow, 
                     }
                 }
             }
-            // W: outputs of the pass
+            // ---- W: outputs of the pass
             if (WCSR && !(ablate & 8)) {
                 for (int e = threadIdx.x; e < nz; e += WG) {
                     int r = 0;
 #pragma unroll
                     for (int rr = 1; rr < TM; ++rr) r += (s_rowoff[rr] <= e) ? 1 : 0;
+                    const int kk = e - s_rowbase[r];  // rank of e inside row r of the unit
+                    int lo4 = s_lo, hi4 = s_hi - 1;   // tile holding it: last with pre <= kk
+                    while (lo4 < hi4) {
+                        const int mid = (lo4 + hi4 + 1) >> 1;
+                        if ((int)s_pre[mid * TM + r] <= kk) lo4 = mid; else hi4 = mid - 1;
+                    }
+                    int b = kk - (int)s_pre[lo4 * TM + r];
+                    int cl = 0;
+#pragma unroll
+                    for (int ww = 0; ww < MW; ++ww) {
+                        const u32 v = lds_row_word<TM>(s_mask + lo4 * TW32, r, ww);
+                        const int pc = __popc(v);
+                        if (b >= 0 && b < pc) cl = ww * 16 + kth_col16(v, b);
+                        b -= pc;
+                    }
                     const int dst = rowptr[(long)i * TM + r] + s_carry[r] + (e - s_rowoff[r]);
-                    csr_col[dst] = s_ccol[e];
+                    csr_col[dst] = s_cols[lo4] * TM + cl;
                     csr_val[dst] = acc[e];
                 }
             }
             if (WTILE) {
-                for (int j = s_lo + threadIdx.x; j < s_hi; j += WG) {
-                    if (s_off[j + 1] == s_off[j]) continue;
-                    const u32 *tile = s_mask + j * TW32;
-                    int out = nzbase + s_off[j];
+                for (int jt = s_lo + threadIdx.x; jt < s_hi; jt += WG) {
+                    if (s_off[jt + 1] == s_off[jt]) continue;
+                    const u32 *tile = s_mask + jt * TW32;
+                    int out = nzbase + s_off[jt];
 #pragma unroll
                     for (int r = 0; r < TM; ++r) {
-                        int k = s_rowoff[r] + (int)s_pre[j * TM + r];
+                        int k = s_rowbase[r] + (int)s_pre[jt * TM + r];
 #pragma unroll
-                        for (int w = 0; w < MW; ++w) {
-                            u32 v = lds_row_word<TM>(tile, r, w);
+                        for (int ww = 0; ww < MW; ++ww) {
+                            u32 v = lds_row_word<TM>(tile, r, ww);
                             while (v) {
                                 const int hb = 31 - __clz(v);
-                                ColC[out] = (u16)(w * 16 + (15 - hb));
+                                ColC[out] = (u16)(ww * 16 + (15 - hb));
                                 ValC[out++] = acc[k++];
                                 v &= ~(1u << hb);
                             }
@@ -1426,7 +1495,7 @@ __global__ __launch_bounds__(WG) void k_step3(const int *uoff, const int *urow, 
                 }
             }
             __syncthreads();
-            if (threadIdx.x < TM) s_carry[threadIdx.x] += s_cnt[threadIdx.x];
+            if (threadIdx.x < TM) s_carry[threadIdx.x] += cnt_r;
             __syncthreads();
             s_lo = s_hi;
         }
@@ -1486,15 +1555,17 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     if (ev) TSG_HIP(hipEventRecord(ev[1], s));
     // ---- step 2 ----
     int *uoff = nullptr, *urow = nullptr, *unit_rc = nullptr, *unit_rb = nullptr;
+    int4 *utab = nullptr;
     const long maxu = (long)numblkC / CH + tilemA + 1;
     TSG_TRY(cx.get(&uoff, (size_t)tilemA + 1));
     TSG_TRY(cx.get(&urow, (size_t)maxu));
+    TSG_TRY(cx.get(&utab, (size_t)maxu));
     TSG_TRY(cx.get(&unit_rc, (size_t)maxu * TM));
     TSG_TRY(cx.get(&C.tile_nnz, nb1));
     TSG_TRY(cx.get(&C.mask, nb1 * CM<TM>::TW));
     k_units_per_row<<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(C.tile_ptr, tilemA, uoff);
     TSG_TRY(scan_exclusive_i32(cx, uoff, (long)tilemA + 1, s));
-    k_unit_rows<<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(uoff, tilemA, urow);
+    k_unit_rows<<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(uoff, C.tile_ptr, tilemA, urow, utab);
     k_set_i32<<<1, 1, 0, s>>>(C.tile_nnz + numblkC, 0);
     TSG_HIP(hipGetLastError());
     // split points of every A tile's B row at its C tile row's unit boundaries
@@ -1579,30 +1650,38 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
         csr_out->nnz = nnzC;
         TSG_TRY(cx.get(&csr_out->columnindex, (size_t)nnzC + 1));
         TSG_TRY(cx.get(&csr_out->value, (size_t)nnzC + 1));
-        if (nnzC > 0) {
-            if (elem)
-                k_step3<TM, TN, true, false, true><<<gu, WG, 0, s>>>(
-                    uoff, urow, tilemA, V, E, C.tile_ptr, C.tile_columnidx, C.tile_nnz, C.mask, unit_rb,
-                    csr_out->rowpointer, csr_out->columnindex, csr_out->value, nullptr, nullptr, nullptr, g_ablate);
-            else
-                k_step3<TM, TN, true, false, false><<<gu, WG, 0, s>>>(
-                    uoff, urow, tilemA, V, E, C.tile_ptr, C.tile_columnidx, C.tile_nnz, C.mask, unit_rb,
-                    csr_out->rowpointer, csr_out->columnindex, csr_out->value, nullptr, nullptr, nullptr, g_ablate);
-        }
     } else {
         TSG_TRY(cx.get(&C.tile_csr_Ptr, nb1 * TM));
         TSG_TRY(cx.get(&C.tile_csr_Col, (size_t)nnzC + 1));
         TSG_TRY(cx.get(&C.tile_csr_Value, (size_t)nnzC + 1));
+    }
+    int nunits = 0;
+    TSG_TRY(read_i32(cx, uoff + tilemA, &nunits, s));
+    if (ev) TSG_HIP(hipEventRecord(ev[4], s));
+    if (csr_out) {
+        if (nnzC > 0) {
+            if (elem)
+                k_step3<TM, TN, true, false, true><<<gu, WG, 0, s>>>(
+                    utab, nunits, V, E, C.tile_columnidx, C.tile_nnz, C.mask, unit_rb,
+                    csr_out->rowpointer, csr_out->columnindex, csr_out->value, nullptr, nullptr, nullptr, g_ablate);
+            else
+                k_step3<TM, TN, true, false, false><<<gu, WG, 0, s>>>(
+                    utab, nunits, V, E, C.tile_columnidx, C.tile_nnz, C.mask, unit_rb,
+                    csr_out->rowpointer, csr_out->columnindex, csr_out->value, nullptr, nullptr, nullptr, g_ablate);
+        }
+    } else {
         if (nnzC > 0)
             k_step3<TM, TN, false, true, false><<<gu, WG, 0, s>>>(
-                uoff, urow, tilemA, V, E, C.tile_ptr, C.tile_columnidx, C.tile_nnz, C.mask, nullptr, nullptr,
+                utab, nunits, V, E, C.tile_columnidx, C.tile_nnz, C.mask, nullptr, nullptr,
                 nullptr, nullptr, C.tile_csr_Ptr, C.tile_csr_Col, C.tile_csr_Value, g_ablate);
     }
+    TSG_HIP(hipGetLastError());
+    if (ev) TSG_HIP(hipEventRecord(ev[5], s));
     cx.put(esplit);
     cx.put(ebase);
-    TSG_HIP(hipGetLastError());
     cx.put(uoff);
     cx.put(urow);
+    cx.put(utab);
     cx.put(unit_rc);
     cx.put(unit_rb);
     cx.put(split);

@@ -192,3 +192,24 @@ def test_device_api_matches_host_api():
         c2, _ = ctx.spgemm(dA, dA)
         assert_csr_equal(ctx.to_host(c2), got)
     ctx.close()
+
+
+@pytest.mark.parametrize("aat", [0, 1])
+def test_cli_reports_reference_lines(aat, tmp_path):
+    """./test -d 0 -aat X <mtx> 16 16 prints the reference's key lines with the
+    oracle's nnzCub / nnzC and writes the CSV (creating the directory)."""
+    import re
+    import subprocess
+    cli = os.path.join(os.path.dirname(T._lib.LIB_PATH), "..", "bin", "test")
+    path = os.path.join(FIXTURES, "banded_36x36.mtx")
+    out = tmp_path / "data"
+    r = subprocess.run([cli, "-d", "0", "-aat", str(aat), path, "16", "16"], capture_output=True, text=True,
+                       timeout=300, env=dict(os.environ, TSG_DATA_DIR=str(out)))
+    assert r.returncode == 0, r.stderr
+    oA = O.OMat.load(path)
+    oB = O.transpose(oA) if aat else O.OMat.alias(oA)
+    ref = O.gustavson(oA, oB)
+    assert f"SpGEMM nnzCub = {O.nnzcub(oA, oB)}" in r.stdout
+    assert re.search(rf"nnzC = {ref.s.nnz}\b", r.stdout), r.stdout
+    assert re.search(r"TileSpGEMM runtime is [0-9.]+ ms, gflops = [0-9.]+", r.stdout), r.stdout
+    assert any(out.iterdir())

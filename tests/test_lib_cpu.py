@@ -88,3 +88,24 @@ def test_mmio_reader_errors(L, tmp_path):
     oob.write_text("%%MatrixMarket matrix coordinate real general\n2 2 1\n3 1 1.0\n")
     with pytest.raises(_lib.TsgError):
         T.mmio_allinone(str(oob))
+
+
+CLI = os.path.join(os.path.dirname(_lib.LIB_PATH), "..", "bin", "test")
+
+
+def _cli(*args, env=None):
+    import subprocess
+    return subprocess.run([CLI, *args], capture_output=True, text=True, timeout=120, env=env)
+
+
+def test_cli_usage_exits_zero():
+    # fewer than 7 args: usage line and exit 0 (src/main.cu:16-20)
+    r = _cli()
+    assert r.returncode == 0 and "./test -d 0 -aat 0 matrix.mtx" in r.stdout
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="GPU present")
+def test_cli_fails_loudly_without_device(tmp_path):
+    r = _cli("-d", "0", "-aat", "0", os.path.join(FIXTURES, "banded_36x36.mtx"), "16", "16",
+             env=dict(os.environ, TSG_DATA_DIR=str(tmp_path)))
+    assert r.returncode != 0 and "no HIP device" in r.stderr

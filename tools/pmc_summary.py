@@ -1,0 +1,80 @@
+"""Summarise a tools/profile.sh run into profiles/<tag>_*:
+  <tag>_kernel_stats.csv   rocprofv3 --stats kernel table (copied)
+  <tag>_kernel_stats.txt   per-kernel calls / avg us / per-step us / share
+  <tag>_pmc.json           per kernel: dispatches, avg duration (trace), HBM bytes
+                           per dispatch = 2*FETCH_SIZE + WRITE_SIZE (KiB -> B; the
+                           FETCH_SIZE x2 is the gfx950 correction, MI355X_MICROARCH.md)
+  <tag>_bench.json         the bench line printed under the stats run
+usage: python tools/pmc_summary.py gpurun_out/<tag> <tag> <dispatches_per_kernel_per_run>"""
+import collections
+import csv
+import glob
+import json
+import os
+import re
+import shutil
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def short(name):
+    return re.sub(r"\(.*", "", name).replace("void ", "").strip()
+
+
+def counters(d, counter):
+    f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    acc = collections.defaultdict(list)
+    if not f:
+        return acc
+    for r in csv.DictReader(open(f[0])):
+        if r["Counter_Name"] == counter:
+            acc[short(r["Kernel_Name"])].append(float(r["Counter_Value"]) * 1024.0)
+    return acc
+
+
+def main():
+    src, tag = sys.argv[1], sys.argv[2]
+    prof = os.path.join(REPO, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    stats = glob.glob(os.path.join(src, "stats", "**", "*kernel_stats.csv"), recursive=True)
+    trace = glob.glob(os.path.join(src, "stats", "**", "*kernel_trace.csv"), recursive=True)
+    out = {}
+    if stats:
+        shutil.copy(stats[0], os.path.join(prof, f"{tag}_kernel_stats.csv"))
+        sys.path.insert(0, os.path.join(REPO, "tools"))
+        import kstats
+        import io
+        import contextlib
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            sys.argv = ["kstats", stats[0]]
+            kstats.main()
+        open(os.path.join(prof, f"{tag}_kernel_stats.txt"), "w").write(buf.getvalue())
+    dur = collections.defaultdict(list)
+    if trace:
+        for r in csv.DictReader(open(trace[0])):
+            dur[short(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    fetch = counters(os.path.join(src, "pmc_fetch"), "FETCH_SIZE")
+    write = counters(os.path.join(src, "pmc_write"), "WRITE_SIZE")
+    for k in sorted(set(dur) | set(fetch) | set(write)):
+        f, w = fetch.get(k, []), write.get(k, [])
+        out[k] = {
+            "dispatches": len(dur.get(k, [])),
+            "avg_us": round(sum(dur[k]) / len(dur[k]), 2) if dur.get(k) else None,
+            "fetch_bytes_per_dispatch": round(2.0 * sum(f) / len(f)) if f else None,
+            "write_bytes_per_dispatch": round(sum(w) / len(w)) if w else None,
+        }
+        if f and w:
+            out[k]["hbm_bytes_per_dispatch"] = out[k]["fetch_bytes_per_dispatch"] + out[k]["write_bytes_per_dispatch"]
+    json.dump(out, open(os.path.join(prof, f"{tag}_pmc.json"), "w"), indent=1, sort_keys=True)
+    log = os.path.join(src, "stats.log")
+    if os.path.exists(log):
+        for line in open(log):
+            if line.startswith("{\"metric\""):
+                open(os.path.join(prof, f"{tag}_bench.json"), "w").write(line)
+    print(f"wrote profiles/{tag}_*")
+
+
+if __name__ == "__main__":
+    main()
