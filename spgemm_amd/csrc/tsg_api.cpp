@@ -616,6 +616,10 @@ static void release_tiles(Context &cx, tsg_dev_tiles &t) {
     t = tsg_dev_tiles{};
 }
 
+// Step 2 streams element products when A averages fewer nonzeros per tile than
+// this (one 16-bit row-mask OR per A nonzero and B tile otherwise wins).
+static constexpr double kStep2ElemMaxTileDensity = 16.0;
+
 int tsg_dev_spgemm(tsg_context *ctx, const tsg_dev_csr *A, const tsg_dev_csr *B, int tm, int tn,
                    void *stream, tsg_dev_csr *C, tsg_stats *stats) {
     if (!ctx || !A || !B || !C || !valid_tiles(tm, tn) || A->n != B->m) return TSG_ERR_INVALID;
@@ -626,11 +630,40 @@ int tsg_dev_spgemm(tsg_context *ctx, const tsg_dev_csr *A, const tsg_dev_csr *B,
     tsg_dev_tiles tA, tB, tC;
     auto h0 = std::chrono::steady_clock::now();
     TSG_HIP(hipEventRecord(cx.ev[8], s));
-    TSG_TRY(dev_csr2tile_row_major(cx, *A, tm, tn, tA, s));
-    TSG_TRY(dev_csr2tile_col_major(cx, *B, tm, tn, tB, s));
+    // Element streaming (steps 2/3 straight from the CSR operands) needs B's rows
+    // column-sorted.  Sparse tiles (few nonzeros per A tile, e.g. web graphs) then
+    // need only the tile STRUCTURE of A and B; denser tiles keep the full
+    // csr2tile payloads for step 2's tile-level mask ORs.
+    bool bsorted = false;
+    TSG_TRY(dev_rows_sorted(cx, *B, &bsorted, s));
+    const bool alias = A->rowpointer == B->rowpointer && A->columnindex == B->columnindex && A->m == B->m &&
+                       A->n == B->n && tm == tn;
+    bool s2elem = false, b_is_a = false;
+    if (bsorted) {
+        TSG_TRY(dev_tile_structure(cx, *A, tm, tn, tA, s));
+        const char *md = getenv("TSG_STEP2_MODE");
+        if (md && !strcmp(md, "elem")) s2elem = true;
+        else if (md && !strcmp(md, "tile")) s2elem = false;
+        else s2elem = (double)A->nnz < kStep2ElemMaxTileDensity * (double)tA.numtile;
+        if (s2elem) {
+            if (alias) {
+                tB = tA;
+                b_is_a = true;
+            } else {
+                TSG_TRY(dev_tile_structure(cx, *B, tn, tm, tB, s));
+            }
+        } else {
+            release_tiles(cx, tA);
+        }
+    }
+    if (!s2elem) {
+        TSG_TRY(dev_csr2tile_row_major(cx, *A, tm, tn, tA, s));
+        TSG_TRY(dev_csr2tile_col_major(cx, *B, tm, tn, tB, s));
+    }
     TSG_HIP(hipEventRecord(cx.ev[9], s));
     // tile2csr is fused into step 3's epilogue on this path (C tiles stay materialised)
-    TSG_TRY(dev_tilespgemm(cx, tA, tB, tC, &st, s, cx.ev, C, A, B));
+    TSG_TRY(dev_tilespgemm(cx, tA, tB, tC, &st, s, cx.ev, C, bsorted ? A : nullptr, bsorted ? B : nullptr,
+                           s2elem));
     TSG_HIP(hipEventRecord(cx.ev[10], s));
     TSG_HIP(hipEventSynchronize(cx.ev[10]));
     auto h1 = std::chrono::steady_clock::now();
@@ -647,6 +680,7 @@ int tsg_dev_spgemm(tsg_context *ctx, const tsg_dev_csr *A, const tsg_dev_csr *B,
     st.t_malloc_ms = st.t_e2e_ms - ev_ms(cx.ev[8], cx.ev[10]);
     if (st.t_malloc_ms < 0) st.t_malloc_ms = 0;
     release_tiles(cx, tA);
+    if (b_is_a) tB = tsg_dev_tiles{};
     release_tiles(cx, tB);
     release_tiles(cx, tC);
     if (stats) *stats = st;

@@ -879,6 +879,122 @@ __global__ void k_rows_from_units(const int *unit_off, int tilem, int nwin, int 
     for (int i = blockIdx.x * WG + threadIdx.x; i <= tilem; i += gridDim.x * WG) Cptr[i] = unit_off[(long)i * nwin];
 }
 
+// Tile structure only (tile_ptr + ascending distinct tile_columnidx per tile
+// row) straight from CSR, the structural half of csr2tile (csr2tile.h:6-120):
+// unit = (tile row i, window of `win` tile columns), LDS bitmask of the tile
+// columns hit by the tile row's entries.  PASS 0 counts, PASS 1 emits.
+template <int PASS>
+__global__ __launch_bounds__(WG) void k_tstruct(const int *rowptr, const int *col, int m, int tr, int tc, int tilem,
+                                                int tilen, int nwin, int win, int *unit_cnt, const int *unit_off,
+                                                int *tcol) {
+    __shared__ u32 bm[S1_MAXWORDS];
+    __shared__ int red[WAVES];
+    const int nunits = tilem * nwin;
+    const int words = win >> 5;
+    const int wpt = words / WG;
+    for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
+        const int i = u / nwin, w = u - i * nwin;
+        const int p0 = rowptr[i * tr], p1 = rowptr[min((i + 1) * tr, m)];
+        if (p0 == p1) {
+            if (PASS == 0 && threadIdx.x == 0) unit_cnt[u] = 0;
+            continue;
+        }
+        const int clo = w * win;
+        for (int x = threadIdx.x; x < words; x += WG) bm[x] = 0u;
+        __syncthreads();
+        for (int p = p0 + threadIdx.x; p < p1; p += WG) {
+            const int c = col[p] / tc - clo;
+            if ((unsigned)c < (unsigned)win) atomicOr(&bm[c >> 5], 1u << (c & 31));
+        }
+        __syncthreads();
+        int cnt = 0;
+        for (int x = 0; x < wpt; ++x) cnt += __popc(bm[threadIdx.x * wpt + x]);
+        if (PASS == 0) {
+            const int tot = block_sum(cnt, red);
+            if (threadIdx.x == 0) unit_cnt[u] = tot;
+        } else {
+            int tot;
+            int off = block_excl_scan(cnt, &tot, red) + unit_off[u];
+            for (int x = 0; x < wpt; ++x) {
+                const int wi = threadIdx.x * wpt + x;
+                u32 v = bm[wi];
+                while (v) {
+                    tcol[off++] = clo + wi * 32 + __ffs(v) - 1;
+                    v &= v - 1;
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+static void window_for(int tilen, int *win, int *nwin) {
+    int w = ((tilen + 8191) / 8192) * 8192;
+    if (w < 8192) w = 8192;
+    if (w > 65536) w = 65536;
+    *win = w;
+    *nwin = (tilen + w - 1) / w;
+}
+
+int dev_tile_structure(Context &cx, const tsg_dev_csr &M, int tr, int tc, tsg_dev_tiles &out, hipStream_t s) {
+    out = tsg_dev_tiles{};
+    out.m = M.m; out.n = M.n; out.nnz = M.nnz;
+    out.tile_m = tr; out.tile_n = tc;
+    out.tilem = (M.m + tr - 1) / tr;
+    out.tilen = (M.n + tc - 1) / tc;
+    int win, nwin;
+    window_for(out.tilen, &win, &nwin);
+    if ((long)out.tilem * nwin >= (1L << 31) - 1) return TSG_ERR_UNSUPPORTED;
+    const long nunits = (long)out.tilem * nwin;
+    int *ucnt = nullptr;
+    TSG_TRY(cx.get(&ucnt, (size_t)nunits + 1));
+    TSG_TRY(cx.get(&out.tile_ptr, (size_t)out.tilem + 1));
+    TSG_HIP(hipMemsetAsync(ucnt + nunits, 0, sizeof(int), s));
+    const int g = grid_for(nunits, 1, 16384);
+    if (out.tilem > 0)
+        k_tstruct<0><<<g, WG, 0, s>>>(M.rowpointer, M.columnindex, M.m, tr, tc, out.tilem, out.tilen, nwin, win,
+                                      ucnt, nullptr, nullptr);
+    TSG_HIP(hipGetLastError());
+    TSG_TRY(scan_exclusive_i32(cx, ucnt, nunits + 1, s));
+    k_rows_from_units<<<grid_for(out.tilem + 1, WG, 4096), WG, 0, s>>>(ucnt, out.tilem, nwin, out.tile_ptr);
+    TSG_TRY(read_i32(cx, out.tile_ptr + out.tilem, &out.numtile, s));
+    TSG_TRY(cx.get(&out.tile_columnidx, (size_t)out.numtile + 1));
+    if (out.tilem > 0)
+        k_tstruct<1><<<g, WG, 0, s>>>(M.rowpointer, M.columnindex, M.m, tr, tc, out.tilem, out.tilen, nwin, win,
+                                      nullptr, ucnt, out.tile_columnidx);
+    TSG_HIP(hipGetLastError());
+    cx.put(ucnt);
+    return TSG_OK;
+}
+
+// flag = 1 when some CSR row is not column-sorted (ascending, duplicates allowed)
+__global__ __launch_bounds__(WG) void k_rows_unsorted2(const int *rp, const int *ci, int m, int *flag) {
+    const int nnz = rp[m];
+    for (int p = blockIdx.x * WG + threadIdx.x + 1; p < nnz; p += gridDim.x * WG) {
+        if (ci[p] >= ci[p - 1]) continue;
+        int lo = 0, hi = m;  // is p a row start?  (first R with rp[R] >= p)
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (rp[mid] < p) lo = mid + 1; else hi = mid;
+        }
+        if (rp[lo] != p) *flag = 1;
+    }
+}
+
+int dev_rows_sorted(Context &cx, const tsg_dev_csr &M, bool *sorted, hipStream_t s) {
+    int *flag = nullptr;
+    TSG_TRY(cx.get(&flag, 1));
+    TSG_HIP(hipMemsetAsync(flag, 0, sizeof(int), s));
+    if (M.m > 0 && M.nnz > 1)
+        k_rows_unsorted2<<<grid_for(M.nnz, WG, 16384), WG, 0, s>>>(M.rowpointer, M.columnindex, M.m, flag);
+    TSG_HIP(hipGetLastError());
+    int f = 0;
+    TSG_TRY(read_i32(cx, flag, &f, s));
+    cx.put(flag);
+    *sorted = (f == 0);
+    return TSG_OK;
+}
+
 // ---------------------------------------------------------------------------
 // Steps 2 and 3 share one chunking: unit = (C tile row i, <= CH consecutive C
 // tiles of that row), units are independent workgroup tasks.  A unit's (A
@@ -1046,15 +1162,6 @@ __global__ __launch_bounds__(WG) void k_esplit(int m, const int *rpA, const int 
     }
 }
 
-__global__ __launch_bounds__(WG) void k_rows_unsorted(const int *rp, const int *ci, int m, int *flag) {
-    for (int R = blockIdx.x * WG + threadIdx.x; R < m; R += gridDim.x * WG)
-        for (int p = rp[R] + 1; p < rp[R + 1]; ++p)
-            if (ci[p] < ci[p - 1]) {
-                *flag = 1;
-                break;
-            }
-}
-
 // Products of A tiles [ab, ab+na) (row i, unit q of nu, A tiles from a0) that
 // fall in the unit's column range, from the precomputed split points:
 // bs[], off[] (exclusive scan of the counts, off[na] = total).
@@ -1141,25 +1248,87 @@ __device__ __forceinline__ bool unit_masks(const ABView &V, int i, int q, int nu
 // ---------------------------------------------------------------------------
 // step 2: per-tile nnz and per-unit per-row counts (-> CSR row pointers)
 // ---------------------------------------------------------------------------
-template <int TM, int TN>
-__global__ __launch_bounds__(WG) void k_step2(const int *uoff, const int *urow, int tilem, ABView V, const int *Cptr,
-                                              const int *Ccol, int *nnzC, int *unit_rc, u16 *maskC) {
+// Stream the element products of one unit straight from the CSR operands: for
+// every A entry p of C tile row i (row r of the tile row) and every B entry pb
+// of B row col(p) inside the unit's column range (split points precomputed by
+// k_esplit; narrowed to columns [clo, chi) when `narrow`), call f(r, slot, pb),
+// slot = p's index in the current batch of WG A entries (s_va[slot] = A value
+// when s_va != nullptr).  Balanced over the workgroup by an LDS scan of the
+// segment lengths (consecutive products -> consecutive lanes: coalesced B reads).
+template <int TM, class F>
+__device__ __forceinline__ void elem_stream(const ECsr &E, int i, int q, const int *s_rp, bool narrow, int clo,
+                                            int chi, unsigned char *s_r, double *s_va, ProdLds &L, F &&f) {
+    const int e0 = s_rp[0], ei = s_rp[TM] - e0;
+    const int *spbase = E.esplit + E.ebase[i];
+    for (int eb = 0; eb < ei; eb += WG) {
+        const int na = min(WG, ei - eb);
+        int bs = 0, len = 0;
+        if (threadIdx.x < na) {
+            const int p = e0 + eb + threadIdx.x;
+            int r = 0;
+#pragma unroll
+            for (int rr = 1; rr < TM; ++rr) r += (s_rp[rr] <= p) ? 1 : 0;
+            s_r[threadIdx.x] = (unsigned char)r;
+            if (s_va) s_va[threadIdx.x] = E.vA[p];
+            const int *sp = spbase + (eb + threadIdx.x);
+            bs = sp[(long)q * ei];
+            int be = sp[(long)(q + 1) * ei];
+            if (narrow) {
+                bs = lower_bound_dev(E.ciB, bs, be, clo);
+                be = lower_bound_dev(E.ciB, bs, be, chi);
+            }
+            len = be - bs;
+        }
+        int tot;
+        const int off = block_excl_scan(len, &tot, L.red);
+        L.bs[threadIdx.x] = bs;
+        L.off[threadIdx.x] = off;
+        __syncthreads();
+        for (int it = threadIdx.x; it < tot; it += WG) {
+            int lo = 0, hi = na - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (L.off[mid] <= it) lo = mid; else hi = mid - 1;
+            }
+            f((int)s_r[lo], lo, L.bs[lo] + (it - L.off[lo]));
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// step 2: C tile masks, per-tile nnz and per-unit per-row counts (-> CSR row
+// pointers).  ELEM: masks from the CSR element products (sparse tiles);
+// otherwise from the tile products (B row masks ORed per A nonzero).
+// ---------------------------------------------------------------------------
+template <int TM, int TN, bool ELEM>
+__global__ __launch_bounds__(WG) void k_step2(const int4 *utab, int nunits, ABView V, ECsr E, const int *Ccol,
+                                              int *nnzC, int *unit_rc, u16 *maskC) {
     constexpr int MW = CM<TM>::MW, TW32 = CM<TM>::TW32;
     __shared__ __align__(16) u32 s_mask[CH * TW32];
     __shared__ int s_cols[CH];
     __shared__ int s_rc[TM];
+    __shared__ int s_rp[TM + 1];
+    __shared__ unsigned char s_r[WG];
     __shared__ ProdLds L;
-    const int nunits = uoff[tilem];
     for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
-        const int i = urow[u];
-        const int t0 = Cptr[i] + (u - uoff[i]) * CH;
-        const int ns = min(CH, Cptr[i + 1] - t0);
+        const int4 ut = utab[u];
+        const int i = ut.x, t0 = ut.y, nu = ut.z, q = ut.w >> 9, ns = ut.w & 511;
         unit_load_cols_zero<TM>(Ccol, t0, ns, s_cols, s_mask);
         if (threadIdx.x < TM) s_rc[threadIdx.x] = 0;
+        if (ELEM && threadIdx.x <= TM) s_rp[threadIdx.x] = E.rpA[min(i * TM + (int)threadIdx.x, E.m)];
         __syncthreads();
-        int tot;
-        unit_masks<TM, TN>(V, i, u - uoff[i], uoff[i + 1] - uoff[i], V.Aptr[i], V.Aptr[i + 1], s_cols, ns, s_mask, L,
-                           &tot);
+        if (ELEM) {
+            elem_stream<TM>(E, i, q, s_rp, false, 0, 0, s_r, nullptr, L, [&](int r, int, int pb) {
+                const int x = E.ciB[pb];
+                const int sl = lower_bound_dev(s_cols, 0, ns, x / TM);  // step 1 covers every product
+                const int c = x % TM, k = r * MW + (c >> 4);
+                atomicOr(&s_mask[sl * TW32 + (k >> 1)], (0x8000u >> (c & 15)) << ((k & 1) * 16));
+            });
+        } else {
+            int tot;
+            unit_masks<TM, TN>(V, i, q, nu, V.Aptr[i], V.Aptr[i + 1], s_cols, ns, s_mask, L, &tot);
+        }
         int rc[TM];
 #pragma unroll
         for (int r = 0; r < TM; ++r) rc[r] = 0;
@@ -1376,52 +1545,17 @@ __global__ __launch_bounds__(WG) void k_step3(const int4 *utab, int nunits, ABVi
             // ---- V: values
             if (!(ablate & 4)) {
                 if (ELEM) {
-                    const int e0 = s_rp[0], ei = s_rp[TM] - e0;
-                    const int *spbase = E.esplit + E.ebase[i];
                     const bool narrow = s_lo > 0 || s_hi < ns;
                     const int clo = s_cols[s_lo] * TM, chi = (s_cols[s_hi - 1] + 1) * TM;
-                    for (int eb = 0; eb < ei; eb += WG) {
-                        const int na = min(WG, ei - eb);
-                        int bs = 0, len = 0;
-                        if (threadIdx.x < na) {
-                            const int p = e0 + eb + threadIdx.x;
-                            int r = 0;
-#pragma unroll
-                            for (int rr = 1; rr < TM; ++rr) r += (s_rp[rr] <= p) ? 1 : 0;
-                            s_r[threadIdx.x] = (unsigned char)r;
-                            s_va[threadIdx.x] = E.vA[p];
-                            const int *sp = spbase + (eb + threadIdx.x);
-                            bs = sp[(long)q * ei];
-                            int be = sp[(long)(q + 1) * ei];
-                            if (narrow) {
-                                bs = lower_bound_dev(E.ciB, bs, be, clo);
-                                be = lower_bound_dev(E.ciB, bs, be, chi);
-                            }
-                            len = be - bs;
-                        }
-                        int tot;
-                        const int off = block_excl_scan(len, &tot, L.red);
-                        L.bs[threadIdx.x] = bs;
-                        L.off[threadIdx.x] = off;
-                        __syncthreads();
-                        for (int it = threadIdx.x; it < tot; it += WG) {
-                            int lo3 = 0, hi3 = na - 1;
-                            while (lo3 < hi3) {
-                                const int mid = (lo3 + hi3 + 1) >> 1;
-                                if (L.off[mid] <= it) lo3 = mid; else hi3 = mid - 1;
-                            }
-                            const int pb = L.bs[lo3] + (it - L.off[lo3]);
-                            const int x = E.ciB[pb];
-                            const double vb = E.vB[pb];
-                            const int sl = lower_bound_dev(s_cols, s_lo, s_hi, x / TM);
-                            if (sl >= s_hi || s_cols[sl] != x / TM) continue;  // other pass
-                            const int r = s_r[lo3];
-                            atomicAdd(&acc[s_rowbase[r] + (int)s_pre[sl * TM + r] +
-                                           lds_rank<TM>(s_mask + sl * TW32, r, x % TM)],
-                                      s_va[lo3] * vb);
-                        }
-                        __syncthreads();
-                    }
+                    elem_stream<TM>(E, i, q, s_rp, narrow, clo, chi, s_r, s_va, L, [&](int r, int slot, int pb) {
+                        const int x = E.ciB[pb];
+                        const double vb = E.vB[pb];
+                        const int sl = lower_bound_dev(s_cols, s_lo, s_hi, x / TM);
+                        if (sl >= s_hi || s_cols[sl] != x / TM) return;  // another pass's tile
+                        atomicAdd(&acc[s_rowbase[r] + (int)s_pre[sl * TM + r] +
+                                       lds_rank<TM>(s_mask + sl * TW32, r, x % TM)],
+                                  s_va[slot] * vb);
+                    });
                 } else {
                     const int a0 = V.Aptr[i], a1 = V.Aptr[i + 1];
                     for (int ab = a0; ab < a1; ab += WG) {
@@ -1508,11 +1642,17 @@ static int g_ablate = -1;
 
 int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_dev_tiles &C,
                    tsg_stats *st, hipStream_t s, hipEvent_t *ev, tsg_dev_csr *csr_out, const tsg_dev_csr *Acsr,
-                   const tsg_dev_csr *Bcsr) {
+                   const tsg_dev_csr *Bcsr, bool step2_elem) {
     if (g_ablate < 0) g_ablate = getenv("TSG_ABLATE") ? atoi(getenv("TSG_ABLATE")) : 0;
     constexpr int TM = 16, TN = 16;
     if (A.tile_m != TM || A.tile_n != TN || B.tile_m != TN || B.tile_n != TM) return TSG_ERR_UNSUPPORTED;
-    if (A.n != B.m || !B.rm_mask || !B.rm_rowstart) return TSG_ERR_INVALID;
+    // element streaming needs the CSR operands (B rows column-sorted: caller's check)
+    const bool have_csr = Acsr && Bcsr && Acsr->m == A.m && Bcsr->m == B.m && Acsr->nnz > 0;
+    const bool s3elem = csr_out && have_csr && !(g_ablate & 16);
+    const bool s2elem = step2_elem && have_csr;
+    const bool tilepay = !(s2elem && s3elem);  // some step reads the tile payloads
+    if (A.n != B.m) return TSG_ERR_INVALID;
+    if (tilepay && (!B.rm_mask || !B.rm_rowstart || !A.tile_csr_Col || !A.tile_nnz)) return TSG_ERR_INVALID;
     const int tilemA = A.tilem, tilenB = B.tilen;
     C = tsg_dev_tiles{};
     C.m = A.m; C.n = B.n; C.tile_m = TM; C.tile_n = TM;
@@ -1568,33 +1708,60 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     k_unit_rows<<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(uoff, C.tile_ptr, tilemA, urow, utab);
     k_set_i32<<<1, 1, 0, s>>>(C.tile_nnz + numblkC, 0);
     TSG_HIP(hipGetLastError());
-    // split points of every A tile's B row at its C tile row's unit boundaries
+    int nunits = 0;
+    TSG_TRY(read_i32(cx, uoff + tilemA, &nunits, s));
+    const int gu = grid_for(maxu, 1, 16384);
+    // tile-product split points: every A tile's B tile row cut at its C tile row's unit boundaries
     long long *sbase = nullptr;
     int *split = nullptr;
-    TSG_TRY(cx.get(&sbase, (size_t)tilemA + 1));
-    k_split_counts<<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(uoff, A.tile_ptr, tilemA, sbase);
-    TSG_TRY(scan_exclusive_i64(cx, sbase, (long)tilemA + 1, s));
-    long long nsplit = 0;
-    TSG_TRY(read_i64(cx, sbase + tilemA, &nsplit, s));
-    TSG_TRY(cx.get(&split, (size_t)nsplit + 1));
-    int *trowA = A.tile_rowidx;
-    if (!trowA) {
-        TSG_TRY(cx.get(&trowA, (size_t)A.numtile + 1));
-        k_crow<<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(A.tile_ptr, tilemA, trowA);
+    if (tilepay) {
+        TSG_TRY(cx.get(&sbase, (size_t)tilemA + 1));
+        k_split_counts<<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(uoff, A.tile_ptr, tilemA, sbase);
+        TSG_TRY(scan_exclusive_i64(cx, sbase, (long)tilemA + 1, s));
+        long long nsplit = 0;
+        TSG_TRY(read_i64(cx, sbase + tilemA, &nsplit, s));
+        TSG_TRY(cx.get(&split, (size_t)nsplit + 1));
+        int *trowA = A.tile_rowidx;
+        if (!trowA) {
+            TSG_TRY(cx.get(&trowA, (size_t)A.numtile + 1));
+            k_crow<<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(A.tile_ptr, tilemA, trowA);
+        }
+        if (A.numtile > 0)
+            k_unit_splits<<<grid_for(A.numtile, WG, 8192), WG, 0, s>>>(A.numtile, trowA, A.tile_ptr,
+                                                                      A.tile_columnidx, B.tile_ptr, B.tile_columnidx,
+                                                                      uoff, C.tile_ptr, C.tile_columnidx, sbase, split);
+        TSG_HIP(hipGetLastError());
+        if (trowA != A.tile_rowidx) cx.put(trowA);
     }
-    if (A.numtile > 0)
-        k_unit_splits<<<grid_for(A.numtile, WG, 8192), WG, 0, s>>>(A.numtile, trowA, A.tile_ptr, A.tile_columnidx,
-                                                                  B.tile_ptr, B.tile_columnidx, uoff, C.tile_ptr,
-                                                                  C.tile_columnidx, sbase, split);
-    TSG_HIP(hipGetLastError());
-    if (trowA != A.tile_rowidx) cx.put(trowA);
     const ABView V{A.tile_ptr, A.tile_columnidx, A.tile_nnz, A.tile_csr_Col, A.tile_csr_Value,
                    B.tile_ptr, B.tile_columnidx, B.rm_mask, B.rm_rowstart, B.tile_csr_Col, B.tile_csr_Value,
                    split, sbase};
-    const int gu = grid_for(maxu, 1, 16384);
-    if (numblkC > 0)
-        k_step2<TM, TN><<<gu, WG, 0, s>>>(uoff, urow, tilemA, V, C.tile_ptr, C.tile_columnidx, C.tile_nnz, unit_rc,
-                                          C.mask);
+    // element split points: every A entry's B CSR row cut at the unit boundaries (+ row end)
+    ECsr E{};
+    int *esplit = nullptr;
+    long long *ebase = nullptr;
+    if (s2elem || s3elem) {
+        TSG_TRY(cx.get(&ebase, (size_t)tilemA + 1));
+        k_esplit_counts<TM><<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(uoff, Acsr->rowpointer, A.m, tilemA, ebase);
+        TSG_TRY(scan_exclusive_i64(cx, ebase, (long)tilemA + 1, s));
+        long long ne = 0;
+        TSG_TRY(read_i64(cx, ebase + tilemA, &ne, s));
+        TSG_TRY(cx.get(&esplit, (size_t)ne + 1));
+        k_esplit<TM><<<grid_for(Acsr->nnz, WG, 16384), WG, 0, s>>>(A.m, Acsr->rowpointer, Acsr->columnindex,
+                                                                   Bcsr->rowpointer, Bcsr->columnindex, uoff,
+                                                                   C.tile_ptr, C.tile_columnidx, ebase, esplit);
+        TSG_HIP(hipGetLastError());
+        E = ECsr{A.m, Acsr->rowpointer, Acsr->columnindex, Acsr->value, Bcsr->rowpointer, Bcsr->columnindex,
+                 Bcsr->value, esplit, ebase};
+    }
+    if (numblkC > 0) {
+        if (s2elem)
+            k_step2<TM, TN, true><<<gu, WG, 0, s>>>(utab, nunits, V, E, C.tile_columnidx, C.tile_nnz, unit_rc,
+                                                    C.mask);
+        else
+            k_step2<TM, TN, false><<<gu, WG, 0, s>>>(utab, nunits, V, E, C.tile_columnidx, C.tile_nnz, unit_rc,
+                                                     C.mask);
+    }
     TSG_HIP(hipGetLastError());
     TSG_TRY(scan_exclusive_i32(cx, C.tile_nnz, (long)numblkC + 1, s));
     if (csr_out) {
@@ -1614,38 +1781,6 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     C.nnz = nnzC;
     if (ev) TSG_HIP(hipEventRecord(ev[2], s));
     // ---- step 3 ----
-    // Element-streaming values when the CSR operands are at hand and B's rows
-    // are column-sorted (split points need sorted rows); else the tile path.
-    ECsr E{};
-    int *esplit = nullptr;
-    long long *ebase = nullptr;
-    bool elem = csr_out && Acsr && Bcsr && Acsr->m == A.m && Bcsr->m == B.m && Acsr->nnz > 0 && !(g_ablate & 16);
-    if (elem) {
-        int *flag = nullptr;
-        TSG_TRY(cx.get(&flag, 1));
-        TSG_HIP(hipMemsetAsync(flag, 0, sizeof(int), s));
-        if (Bcsr->m > 0)
-            k_rows_unsorted<<<grid_for(Bcsr->m, WG, 8192), WG, 0, s>>>(Bcsr->rowpointer, Bcsr->columnindex, Bcsr->m,
-                                                                       flag);
-        int unsorted = 0;
-        TSG_TRY(read_i32(cx, flag, &unsorted, s));
-        cx.put(flag);
-        elem = !unsorted;
-    }
-    if (elem) {
-        TSG_TRY(cx.get(&ebase, (size_t)tilemA + 1));
-        k_esplit_counts<TM><<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(uoff, Acsr->rowpointer, A.m, tilemA, ebase);
-        TSG_TRY(scan_exclusive_i64(cx, ebase, (long)tilemA + 1, s));
-        long long ne = 0;
-        TSG_TRY(read_i64(cx, ebase + tilemA, &ne, s));
-        TSG_TRY(cx.get(&esplit, (size_t)ne + 1));
-        k_esplit<TM><<<grid_for(Acsr->nnz, WG, 16384), WG, 0, s>>>(A.m, Acsr->rowpointer, Acsr->columnindex,
-                                                                   Bcsr->rowpointer, Bcsr->columnindex, uoff,
-                                                                   C.tile_ptr, C.tile_columnidx, ebase, esplit);
-        TSG_HIP(hipGetLastError());
-        E = ECsr{A.m, Acsr->rowpointer, Acsr->columnindex, Acsr->value, Bcsr->rowpointer, Bcsr->columnindex,
-                 Bcsr->value, esplit, ebase};
-    }
     if (csr_out) {
         csr_out->nnz = nnzC;
         TSG_TRY(cx.get(&csr_out->columnindex, (size_t)nnzC + 1));
@@ -1655,12 +1790,10 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
         TSG_TRY(cx.get(&C.tile_csr_Col, (size_t)nnzC + 1));
         TSG_TRY(cx.get(&C.tile_csr_Value, (size_t)nnzC + 1));
     }
-    int nunits = 0;
-    TSG_TRY(read_i32(cx, uoff + tilemA, &nunits, s));
     if (ev) TSG_HIP(hipEventRecord(ev[4], s));
     if (csr_out) {
         if (nnzC > 0) {
-            if (elem)
+            if (s3elem)
                 k_step3<TM, TN, true, false, true><<<gu, WG, 0, s>>>(
                     utab, nunits, V, E, C.tile_columnidx, C.tile_nnz, C.mask, unit_rb,
                     csr_out->rowpointer, csr_out->columnindex, csr_out->value, nullptr, nullptr, nullptr, g_ablate);

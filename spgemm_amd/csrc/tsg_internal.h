@@ -85,10 +85,18 @@ int dev_csr2tile_row_major(Context &cx, const tsg_dev_csr &A, int tm, int tn, ts
 int dev_csr2tile_col_major(Context &cx, const tsg_dev_csr &B, int tm, int tn, tsg_dev_tiles &out,
                            hipStream_t s);
 // csr_out != nullptr: step 3 also scatters C into CSR (tile2csr fused into its epilogue).
-// Acsr/Bcsr (nullable): the CSR operands, enabling step 3's element-streaming value pass.
+// Acsr/Bcsr (nullable; B's rows column-sorted): the CSR operands, enabling the
+// element-streaming passes -- step 3's values always, step 2's masks when
+// step2_elem.  A and B then only need their tile structure (tile_ptr,
+// tile_columnidx) unless some step still reads the tile payloads.
 int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_dev_tiles &C,
                    tsg_stats *st, hipStream_t s, hipEvent_t *ev_marks, tsg_dev_csr *csr_out,
-                   const tsg_dev_csr *Acsr = nullptr, const tsg_dev_csr *Bcsr = nullptr);
+                   const tsg_dev_csr *Acsr = nullptr, const tsg_dev_csr *Bcsr = nullptr,
+                   bool step2_elem = false);
+// tile_ptr + tile_columnidx of a CSR's tiling (tr x tc tiles), no payload
+int dev_tile_structure(Context &cx, const tsg_dev_csr &M, int tr, int tc, tsg_dev_tiles &out, hipStream_t s);
+// whether every CSR row is column-sorted (synchronous)
+int dev_rows_sorted(Context &cx, const tsg_dev_csr &M, bool *sorted, hipStream_t s);
 int dev_tile2csr(Context &cx, const tsg_dev_tiles &C, tsg_dev_csr &out, hipStream_t s);
 
 // read a device int / long long synchronously through pinned memory

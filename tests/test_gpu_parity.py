@@ -213,3 +213,32 @@ def test_cli_reports_reference_lines(aat, tmp_path):
     assert re.search(rf"nnzC = {ref.s.nnz}\b", r.stdout), r.stdout
     assert re.search(r"TileSpGEMM runtime is [0-9.]+ ms, gflops = [0-9.]+", r.stdout), r.stdout
     assert any(out.iterdir())
+
+
+@pytest.mark.parametrize("mode", ["elem", "tile"])
+@pytest.mark.parametrize("case", ["rand_sparse", "rand_dense", "banded", "rect_aat", "unsorted"])
+def test_step2_modes_match_oracle(mode, case, monkeypatch):
+    """Both step-2 variants of the device pipeline (element-streamed masks from
+    the CSR operands vs tile-level mask ORs) give the oracle's product; an
+    unsorted B falls back to the tile payload path in either mode."""
+    monkeypatch.setenv("TSG_STEP2_MODE", mode)
+    if case == "rand_sparse":
+        m, n, rp, ci, vv = synth.random_csr(5000, 5000, density=0.0008, seed=21)
+    elif case == "rand_dense":
+        m, n, rp, ci, vv = synth.random_csr(600, 600, density=0.2, seed=22)
+    elif case == "banded":
+        m, n, rp, ci, vv = synth.cant(n=3000, half_band=40)
+    elif case == "rect_aat":
+        m, n, rp, ci, vv = synth.random_csr(700, 2500, density=0.004, seed=23)
+    else:
+        m, n, rp, ci, vv = synth.random_csr(1500, 1500, density=0.01, seed=24, unsorted=True, dups=True)
+    A = T.Matrix.from_csr(m, n, rp, ci, vv)
+    oA = O.OMat.from_csr(m, n, rp, ci, vv)
+    if case == "rect_aat":
+        B, oB = T.transpose(A), O.transpose(oA)
+    else:
+        B, oB = T.Matrix.alias(A), O.OMat.alias(oA)
+    Cm, st = T.spgemm(A, B)
+    ref = O.gustavson(oA, oB)
+    assert_csr_equal(Cm.csr(), ref.csr())
+    assert st["nnzC"] == ref.s.nnz
