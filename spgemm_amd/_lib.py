@@ -12,6 +12,8 @@ import subprocess
 PKG = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG)
 LIB_PATH = os.path.join(PKG, "lib", "libtsg.so")
+# A/B diagnostics only: load another build of the same C ABI
+LIB_PATH = os.environ.get("TSG_LIB_PATH", LIB_PATH)
 HEADER = os.path.join(REPO, "include", "tsg.h")
 
 TSG_OK = 0

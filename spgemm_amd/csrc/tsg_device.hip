@@ -968,6 +968,19 @@ int dev_tile_structure(Context &cx, const tsg_dev_csr &M, int tr, int tc, tsg_de
 }
 
 // flag = 1 when some CSR row is not column-sorted (ascending, duplicates allowed)
+// per unit: {e0, ei, esplit offset of its boundary row (lo, hi)} so step 2/3 can
+// issue the split-point loads together with the unit's other loads
+template <int TM>
+__global__ void k_unit_etab(const int4 *utab, int nunits, const int *rpA, int m, const long long *ebase, int4 *etab) {
+    for (int u = blockIdx.x * WG + threadIdx.x; u < nunits; u += gridDim.x * WG) {
+        const int4 ut = utab[u];
+        const int i = ut.x, q = ut.w >> 9;
+        const int e0 = rpA[i * TM], ei = rpA[min((i + 1) * TM, m)] - e0;
+        const long long off = ebase[i] + (long long)q * ei;
+        etab[u] = make_int4(e0, ei, (int)(off & 0xffffffffll), (int)(off >> 32));
+    }
+}
+
 __global__ __launch_bounds__(WG) void k_rows_unsorted2(const int *rp, const int *ci, int m, int *flag) {
     const int nnz = rp[m];
     for (int p = blockIdx.x * WG + threadIdx.x + 1; p < nnz; p += gridDim.x * WG) {
@@ -1255,11 +1268,33 @@ __device__ __forceinline__ bool unit_masks(const ABView &V, int i, int q, int nu
 // slot = p's index in the current batch of WG A entries (s_va[slot] = A value
 // when s_va != nullptr).  Balanced over the workgroup by an LDS scan of the
 // segment lengths (consecutive products -> consecutive lanes: coalesced B reads).
+// first batch of a unit's element stream, loaded at the unit's start together
+// with its masks (one dependent HBM round trip less per unit)
+struct EPre {
+    int bs, be;
+    double va;
+};
+
+__device__ __forceinline__ const int *etab_split(const ECsr &E, int4 ue) {
+    return E.esplit + (((long long)(unsigned)ue.z) | ((long long)ue.w << 32));
+}
+
+__device__ __forceinline__ EPre epre_load(const ECsr &E, int4 ue, bool with_va) {
+    EPre p{0, 0, 0.0};
+    if ((int)threadIdx.x < ue.y) {
+        const int *sp = etab_split(E, ue) + threadIdx.x;
+        p.bs = sp[0];
+        p.be = sp[ue.y];
+        if (with_va) p.va = E.vA[ue.x + threadIdx.x];
+    }
+    return p;
+}
+
 template <int TM, class F>
-__device__ __forceinline__ void elem_stream(const ECsr &E, int i, int q, const int *s_rp, bool narrow, int clo,
-                                            int chi, unsigned char *s_r, double *s_va, ProdLds &L, F &&f) {
-    const int e0 = s_rp[0], ei = s_rp[TM] - e0;
-    const int *spbase = E.esplit + E.ebase[i];
+__device__ __forceinline__ void elem_stream(const ECsr &E, int4 ue, const EPre &pre, const int *s_rp, bool narrow,
+                                            int clo, int chi, unsigned char *s_r, double *s_va, ProdLds &L, F &&f) {
+    const int e0 = ue.x, ei = ue.y;
+    const int *sp0 = etab_split(E, ue);
     for (int eb = 0; eb < ei; eb += WG) {
         const int na = min(WG, ei - eb);
         int bs = 0, len = 0;
@@ -1269,10 +1304,17 @@ __device__ __forceinline__ void elem_stream(const ECsr &E, int i, int q, const i
 #pragma unroll
             for (int rr = 1; rr < TM; ++rr) r += (s_rp[rr] <= p) ? 1 : 0;
             s_r[threadIdx.x] = (unsigned char)r;
-            if (s_va) s_va[threadIdx.x] = E.vA[p];
-            const int *sp = spbase + (eb + threadIdx.x);
-            bs = sp[(long)q * ei];
-            int be = sp[(long)(q + 1) * ei];
+            int be;
+            if (eb == 0) {
+                bs = pre.bs;
+                be = pre.be;
+                if (s_va) s_va[threadIdx.x] = pre.va;
+            } else {
+                const int *sp = sp0 + (eb + threadIdx.x);
+                bs = sp[0];
+                be = sp[ei];
+                if (s_va) s_va[threadIdx.x] = E.vA[p];
+            }
             if (narrow) {
                 bs = lower_bound_dev(E.ciB, bs, be, clo);
                 be = lower_bound_dev(E.ciB, bs, be, chi);
@@ -1302,8 +1344,8 @@ __device__ __forceinline__ void elem_stream(const ECsr &E, int i, int q, const i
 // otherwise from the tile products (B row masks ORed per A nonzero).
 // ---------------------------------------------------------------------------
 template <int TM, int TN, bool ELEM>
-__global__ __launch_bounds__(WG) void k_step2(const int4 *utab, int nunits, ABView V, ECsr E, const int *Ccol,
-                                              int *nnzC, int *unit_rc, u16 *maskC) {
+__global__ __launch_bounds__(WG) void k_step2(const int4 *utab, const int4 *etab, int nunits, ABView V, ECsr E,
+                                              const int *Ccol, int *nnzC, int *unit_rc, u16 *maskC) {
     constexpr int MW = CM<TM>::MW, TW32 = CM<TM>::TW32;
     __shared__ __align__(16) u32 s_mask[CH * TW32];
     __shared__ int s_cols[CH];
@@ -1311,15 +1353,26 @@ __global__ __launch_bounds__(WG) void k_step2(const int4 *utab, int nunits, ABVi
     __shared__ int s_rp[TM + 1];
     __shared__ unsigned char s_r[WG];
     __shared__ ProdLds L;
+    int4 ut_n = make_int4(0, 0, 0, 0), ue_n = make_int4(0, 0, 0, 0);
+    if ((int)blockIdx.x < nunits) {
+        ut_n = utab[blockIdx.x];
+        if (ELEM) ue_n = etab[blockIdx.x];
+    }
     for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
-        const int4 ut = utab[u];
+        const int4 ut = ut_n, ue = ue_n;
+        if (u + (int)gridDim.x < nunits) {  // next unit's table entries, in flight during this one
+            ut_n = utab[u + gridDim.x];
+            if (ELEM) ue_n = etab[u + gridDim.x];
+        }
         const int i = ut.x, t0 = ut.y, nu = ut.z, q = ut.w >> 9, ns = ut.w & 511;
+        EPre pre{0, 0, 0.0};
+        if (ELEM) pre = epre_load(E, ue, false);
         unit_load_cols_zero<TM>(Ccol, t0, ns, s_cols, s_mask);
         if (threadIdx.x < TM) s_rc[threadIdx.x] = 0;
         if (ELEM && threadIdx.x <= TM) s_rp[threadIdx.x] = E.rpA[min(i * TM + (int)threadIdx.x, E.m)];
         __syncthreads();
         if (ELEM) {
-            elem_stream<TM>(E, i, q, s_rp, false, 0, 0, s_r, nullptr, L, [&](int r, int, int pb) {
+            elem_stream<TM>(E, ue, pre, s_rp, false, 0, 0, s_r, nullptr, L, [&](int r, int, int pb) {
                 const int x = E.ciB[pb];
                 const int sl = lower_bound_dev(s_cols, 0, ns, x / TM);  // step 1 covers every product
                 const int c = x % TM, k = r * MW + (c >> 4);
@@ -1392,8 +1445,24 @@ __device__ __forceinline__ int kth_col16(u32 v, int k) {
     return __ffs(w) - 1;
 }
 
+// TSG_ABLATE & 64: per-phase shader-clock totals of k_step3 (thread 0 of each
+// workgroup; diagnostics, printed by dev_tilespgemm)
+// (compiled in only with -DTSG_PROF_BUILD)
+__device__ unsigned long long g_prof[8];
+#ifdef TSG_PROF_BUILD
+#define PROF_MARK(k)                                                         \
+    if ((ablate & 64) && threadIdx.x == 0) {                                 \
+        const u64 _t = __builtin_amdgcn_s_memtime();                         \
+        atomicAdd(&g_prof[k], _t - prof_t);                                  \
+        prof_t = _t;                                                         \
+    }
+#else
+#define PROF_MARK(k)
+#endif
+
 template <int TM, int TN, bool WCSR, bool WTILE, bool ELEM>
-__global__ __launch_bounds__(WG) void k_step3(const int4 *utab, int nunits, ABView V, ECsr E, const int *Ccol,
+__global__ __launch_bounds__(WG) void k_step3(const int4 *utab, const int4 *etab, int nunits, int mrows, ABView V,
+                                              ECsr E, const int *Ccol,
                                               const int *nnzoff, const u16 *maskC, const int *unit_rb,
                                               const int *rowptr, int *csr_col, double *csr_val, u16 *PtrC,
                                               u16 *ColC, double *ValC, int ablate) {
@@ -1411,13 +1480,29 @@ __global__ __launch_bounds__(WG) void k_step3(const int4 *utab, int nunits, ABVi
     __shared__ int s_rowoff[TM + 1];      // per pass: CSR-order row offsets
     __shared__ int s_rowbase[TM];         // per pass: rowoff[r] - pre[s_lo][r]
     __shared__ int s_carry[TM];
+    __shared__ int s_rowptr[TM];
     __shared__ u64 s_red64[WAVES * NP];
     __shared__ int s_red[WAVES];
     __shared__ ProdLds L;
     const int j = threadIdx.x;
+#ifdef TSG_PROF_BUILD
+    u64 prof_t = (ablate & 64) ? __builtin_amdgcn_s_memtime() : 0;
+#endif
+    int4 ut_n = make_int4(0, 0, 0, 0), ue_n = make_int4(0, 0, 0, 0);
+    if ((int)blockIdx.x < nunits) {
+        ut_n = utab[blockIdx.x];
+        if (ELEM) ue_n = etab[blockIdx.x];
+    }
     for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
-        const int4 ut = utab[u];
+        PROF_MARK(7);
+        const int4 ut = ut_n, ue = ue_n;
+        if (u + (int)gridDim.x < nunits) {  // next unit's table entries, in flight during this one
+            ut_n = utab[u + gridDim.x];
+            if (ELEM) ue_n = etab[u + gridDim.x];
+        }
         const int i = ut.x, t0 = ut.y, nu = ut.z, q = ut.w >> 9, ns = ut.w & 511;
+        EPre pre{0, 0, 0.0};
+        if (ELEM && !(ablate & 4)) pre = epre_load(E, ue, true);
         // ---- load: C masks (written by step 2) + columns; thread j owns tile j
         u32 w[TW32];
         int col = 0;
@@ -1433,7 +1518,10 @@ __global__ __launch_bounds__(WG) void k_step3(const int4 *utab, int nunits, ABVi
 #pragma unroll
             for (int k = 0; k < TW32; ++k) w[k] = 0u;
         }
-        if (threadIdx.x < TM) s_carry[threadIdx.x] = WCSR ? unit_rb[(long)u * TM + threadIdx.x] : 0;
+        if (threadIdx.x < TM) {
+            s_carry[threadIdx.x] = WCSR ? unit_rb[(long)u * TM + threadIdx.x] : 0;
+            if (WCSR) s_rowptr[threadIdx.x] = rowptr[min(i * TM + (int)threadIdx.x, mrows)];
+        }
         if (ELEM && threadIdx.x <= TM) s_rp[threadIdx.x] = E.rpA[min(i * TM + (int)threadIdx.x, E.m)];
 #pragma unroll
         for (int k = 0; k < NV4; ++k)
@@ -1466,6 +1554,7 @@ __global__ __launch_bounds__(WG) void k_step3(const int4 *utab, int nunits, ABVi
             s_red[wave_id()] = itt;
         }
         __syncthreads();
+        PROF_MARK(0);
         u64 tot64[NP];
         int ttot = 0, toff = 0;
 #pragma unroll
@@ -1516,6 +1605,7 @@ __global__ __launch_bounds__(WG) void k_step3(const int4 *utab, int nunits, ABVi
         }
         const int nzbase = WTILE ? nnzoff[t0] : 0;
         __syncthreads();
+        PROF_MARK(1);
         for (int s_lo = 0; s_lo < ns;) {
             int lo = s_lo + 1, hi = ns;  // largest s_hi with nnz(tiles s_lo..s_hi-1) <= NZCAP
             while (lo < hi) {
@@ -1542,12 +1632,13 @@ __global__ __launch_bounds__(WG) void k_step3(const int4 *utab, int nunits, ABVi
             }
             for (int e = threadIdx.x; e < nz; e += WG) acc[e] = 0.0;
             __syncthreads();
+            PROF_MARK(2);
             // ---- V: values
             if (!(ablate & 4)) {
                 if (ELEM) {
                     const bool narrow = s_lo > 0 || s_hi < ns;
                     const int clo = s_cols[s_lo] * TM, chi = (s_cols[s_hi - 1] + 1) * TM;
-                    elem_stream<TM>(E, i, q, s_rp, narrow, clo, chi, s_r, s_va, L, [&](int r, int slot, int pb) {
+                    elem_stream<TM>(E, ue, pre, s_rp, narrow, clo, chi, s_r, s_va, L, [&](int r, int slot, int pb) {
                         const int x = E.ciB[pb];
                         const double vb = E.vB[pb];
                         const int sl = lower_bound_dev(s_cols, s_lo, s_hi, x / TM);
@@ -1581,6 +1672,7 @@ __global__ __launch_bounds__(WG) void k_step3(const int4 *utab, int nunits, ABVi
                     }
                 }
             }
+            PROF_MARK(3);
             // ---- W: outputs of the pass
             if (WCSR && !(ablate & 8)) {
                 for (int e = threadIdx.x; e < nz; e += WG) {
@@ -1602,7 +1694,7 @@ __global__ __launch_bounds__(WG) void k_step3(const int4 *utab, int nunits, ABVi
                         if (b >= 0 && b < pc) cl = ww * 16 + kth_col16(v, b);
                         b -= pc;
                     }
-                    const int dst = rowptr[(long)i * TM + r] + s_carry[r] + (e - s_rowoff[r]);
+                    const int dst = s_rowptr[r] + s_carry[r] + (e - s_rowoff[r]);
                     csr_col[dst] = s_cols[lo4] * TM + cl;
                     csr_val[dst] = acc[e];
                 }
@@ -1631,6 +1723,7 @@ __global__ __launch_bounds__(WG) void k_step3(const int4 *utab, int nunits, ABVi
             __syncthreads();
             if (threadIdx.x < TM) s_carry[threadIdx.x] += cnt_r;
             __syncthreads();
+            PROF_MARK(4);
             s_lo = s_hi;
         }
     }
@@ -1740,6 +1833,7 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     ECsr E{};
     int *esplit = nullptr;
     long long *ebase = nullptr;
+    int4 *etab = nullptr;
     if (s2elem || s3elem) {
         TSG_TRY(cx.get(&ebase, (size_t)tilemA + 1));
         k_esplit_counts<TM><<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(uoff, Acsr->rowpointer, A.m, tilemA, ebase);
@@ -1753,13 +1847,18 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
         TSG_HIP(hipGetLastError());
         E = ECsr{A.m, Acsr->rowpointer, Acsr->columnindex, Acsr->value, Bcsr->rowpointer, Bcsr->columnindex,
                  Bcsr->value, esplit, ebase};
+        TSG_TRY(cx.get(&etab, (size_t)maxu));
+        if (nunits > 0)
+            k_unit_etab<TM><<<grid_for(nunits, WG, 8192), WG, 0, s>>>(utab, nunits, Acsr->rowpointer, A.m, ebase,
+                                                                      etab);
+        TSG_HIP(hipGetLastError());
     }
     if (numblkC > 0) {
         if (s2elem)
-            k_step2<TM, TN, true><<<gu, WG, 0, s>>>(utab, nunits, V, E, C.tile_columnidx, C.tile_nnz, unit_rc,
+            k_step2<TM, TN, true><<<gu, WG, 0, s>>>(utab, etab, nunits, V, E, C.tile_columnidx, C.tile_nnz, unit_rc,
                                                     C.mask);
         else
-            k_step2<TM, TN, false><<<gu, WG, 0, s>>>(utab, nunits, V, E, C.tile_columnidx, C.tile_nnz, unit_rc,
+            k_step2<TM, TN, false><<<gu, WG, 0, s>>>(utab, etab, nunits, V, E, C.tile_columnidx, C.tile_nnz, unit_rc,
                                                      C.mask);
     }
     TSG_HIP(hipGetLastError());
@@ -1790,28 +1889,43 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
         TSG_TRY(cx.get(&C.tile_csr_Col, (size_t)nnzC + 1));
         TSG_TRY(cx.get(&C.tile_csr_Value, (size_t)nnzC + 1));
     }
+    if (g_ablate & 64) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        TSG_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_prof), z, sizeof(z), 0, hipMemcpyHostToDevice, s));
+    }
     if (ev) TSG_HIP(hipEventRecord(ev[4], s));
     if (csr_out) {
         if (nnzC > 0) {
             if (s3elem)
                 k_step3<TM, TN, true, false, true><<<gu, WG, 0, s>>>(
-                    utab, nunits, V, E, C.tile_columnidx, C.tile_nnz, C.mask, unit_rb,
+                    utab, etab, nunits, A.m, V, E, C.tile_columnidx, C.tile_nnz, C.mask, unit_rb,
                     csr_out->rowpointer, csr_out->columnindex, csr_out->value, nullptr, nullptr, nullptr, g_ablate);
             else
                 k_step3<TM, TN, true, false, false><<<gu, WG, 0, s>>>(
-                    utab, nunits, V, E, C.tile_columnidx, C.tile_nnz, C.mask, unit_rb,
+                    utab, etab, nunits, A.m, V, E, C.tile_columnidx, C.tile_nnz, C.mask, unit_rb,
                     csr_out->rowpointer, csr_out->columnindex, csr_out->value, nullptr, nullptr, nullptr, g_ablate);
         }
     } else {
         if (nnzC > 0)
             k_step3<TM, TN, false, true, false><<<gu, WG, 0, s>>>(
-                utab, nunits, V, E, C.tile_columnidx, C.tile_nnz, C.mask, nullptr, nullptr,
+                utab, etab, nunits, A.m, V, E, C.tile_columnidx, C.tile_nnz, C.mask, nullptr, nullptr,
                 nullptr, nullptr, C.tile_csr_Ptr, C.tile_csr_Col, C.tile_csr_Value, g_ablate);
     }
     TSG_HIP(hipGetLastError());
     if (ev) TSG_HIP(hipEventRecord(ev[5], s));
+    if (g_ablate & 64) {
+        unsigned long long pr[8];
+        TSG_HIP(hipMemcpyFromSymbolAsync(pr, HIP_SYMBOL(g_prof), sizeof(pr), 0, hipMemcpyDeviceToHost, s));
+        TSG_HIP(hipStreamSynchronize(s));
+        double tot = 0;
+        for (int k = 0; k < 8; ++k) tot += (double)pr[k];
+        fprintf(stderr, "k_step3 phases (%% of WG-0 clock): load %.1f prologue %.1f passinit %.1f values %.1f "
+                "write %.1f gap %.1f  total %.3g\n", 100 * pr[0] / tot, 100 * pr[1] / tot, 100 * pr[2] / tot,
+                100 * pr[3] / tot, 100 * pr[4] / tot, 100 * pr[7] / tot, tot);
+    }
     cx.put(esplit);
     cx.put(ebase);
+    cx.put(etab);
     cx.put(uoff);
     cx.put(urow);
     cx.put(utab);
