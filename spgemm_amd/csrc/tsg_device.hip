@@ -825,11 +825,29 @@ __device__ __forceinline__ long for_each_product(int a0, int a1, const int *colA
 // ---------------------------------------------------------------------------
 constexpr int S1_MAXWORDS = 2048;  // 65536 tile columns per window
 
+// thread t's wpt (1, 2, 4 or 8) consecutive bitmask words as vector LDS reads
+// (scalar strided reads would put up to 8 lanes on one bank)
+__device__ __forceinline__ void bm_words(const u32 *bm, int wpt, u32 *w) {
+    const int t = threadIdx.x;
+    if (wpt == 8) {
+        const uint4 a = reinterpret_cast<const uint4 *>(bm)[2 * t], b = reinterpret_cast<const uint4 *>(bm)[2 * t + 1];
+        w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+    } else if (wpt == 4) {
+        const uint4 a = reinterpret_cast<const uint4 *>(bm)[t];
+        w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+    } else if (wpt == 2) {
+        const uint2 a = reinterpret_cast<const uint2 *>(bm)[t];
+        w[0] = a.x; w[1] = a.y;
+    } else {
+        w[0] = bm[t];
+    }
+}
+
 template <int PASS>
 __global__ __launch_bounds__(WG) void k_step1(const int *Aptr, const int *Acol, const int *Bptr, const int *Bcol,
                                               int tilemA, int tilenB, int nwin, int win, int *unit_cnt,
                                               const int *unit_off, int *Ccol, u64 *prod_total) {
-    __shared__ u32 bm[S1_MAXWORDS];
+    __shared__ __align__(16) u32 bm[S1_MAXWORDS];
     __shared__ ProdLds L;
     __shared__ int red[WAVES];
     const int nunits = tilemA * nwin;
@@ -852,8 +870,10 @@ __global__ __launch_bounds__(WG) void k_step1(const int *Aptr, const int *Acol, 
             atomicOr(&bm[c >> 5], 1u << (c & 31));
         });
         if (PASS == 0) my_items += (threadIdx.x == 0) ? it : 0;
+        u32 wv[8];
+        bm_words(bm, wpt, wv);
         int cnt = 0;
-        for (int q = 0; q < wpt; ++q) cnt += __popc(bm[threadIdx.x * wpt + q]);
+        for (int q = 0; q < wpt; ++q) cnt += __popc(wv[q]);
         if (PASS == 0) {
             int tot = block_sum(cnt, red);
             if (threadIdx.x == 0) unit_cnt[u] = tot;
@@ -861,8 +881,8 @@ __global__ __launch_bounds__(WG) void k_step1(const int *Aptr, const int *Acol, 
             int tot;
             int off = block_excl_scan(cnt, &tot, red) + unit_off[u];
             for (int q = 0; q < wpt; ++q) {
-                int wi = threadIdx.x * wpt + q;
-                u32 x = bm[wi];
+                const int wi = threadIdx.x * wpt + q;
+                u32 x = wv[q];
                 while (x) {
                     int b = __ffs(x) - 1;
                     Ccol[off++] = clo + wi * 32 + b;
@@ -887,7 +907,7 @@ template <int PASS>
 __global__ __launch_bounds__(WG) void k_tstruct(const int *rowptr, const int *col, int m, int tr, int tc, int tilem,
                                                 int tilen, int nwin, int win, int *unit_cnt, const int *unit_off,
                                                 int *tcol) {
-    __shared__ u32 bm[S1_MAXWORDS];
+    __shared__ __align__(16) u32 bm[S1_MAXWORDS];
     __shared__ int red[WAVES];
     const int nunits = tilem * nwin;
     const int words = win >> 5;
@@ -907,8 +927,10 @@ __global__ __launch_bounds__(WG) void k_tstruct(const int *rowptr, const int *co
             if ((unsigned)c < (unsigned)win) atomicOr(&bm[c >> 5], 1u << (c & 31));
         }
         __syncthreads();
+        u32 wv[8];
+        bm_words(bm, wpt, wv);
         int cnt = 0;
-        for (int x = 0; x < wpt; ++x) cnt += __popc(bm[threadIdx.x * wpt + x]);
+        for (int x = 0; x < wpt; ++x) cnt += __popc(wv[x]);
         if (PASS == 0) {
             const int tot = block_sum(cnt, red);
             if (threadIdx.x == 0) unit_cnt[u] = tot;
@@ -917,7 +939,7 @@ __global__ __launch_bounds__(WG) void k_tstruct(const int *rowptr, const int *co
             int off = block_excl_scan(cnt, &tot, red) + unit_off[u];
             for (int x = 0; x < wpt; ++x) {
                 const int wi = threadIdx.x * wpt + x;
-                u32 v = bm[wi];
+                u32 v = wv[x];
                 while (v) {
                     tcol[off++] = clo + wi * 32 + __ffs(v) - 1;
                     v &= v - 1;
@@ -929,9 +951,8 @@ __global__ __launch_bounds__(WG) void k_tstruct(const int *rowptr, const int *co
 }
 
 static void window_for(int tilen, int *win, int *nwin) {
-    int w = ((tilen + 8191) / 8192) * 8192;
-    if (w < 8192) w = 8192;
-    if (w > 65536) w = 65536;
+    int w = 8192;  // power-of-two multiple of 8192 (1, 2, 4 or 8 bitmask words per thread)
+    while (w < tilen && w < 65536) w <<= 1;
     *win = w;
     *nwin = (tilen + w - 1) / w;
 }
@@ -1386,25 +1407,31 @@ __global__ __launch_bounds__(WG) void k_step2(const int4 *utab, const int4 *etab
 #pragma unroll
         for (int r = 0; r < TM; ++r) rc[r] = 0;
         if (threadIdx.x < ns) {  // ns <= CH == WG
+            static_assert((CM<TM>::TW32 % 4) == 0, "mask tile must be whole uint4");
             const int j = threadIdx.x;
-            const u32 *tile = s_mask + j * TW32;
+            u32 w[TW32];  // the tile's words via vector LDS reads
+#pragma unroll
+            for (int k = 0; k < TW32 / 4; ++k) {
+                const uint4 v = reinterpret_cast<const uint4 *>(s_mask + j * TW32)[k];
+                w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+            }
             int nz = 0;
 #pragma unroll
             for (int r = 0; r < TM; ++r) {
                 int c = 0;
 #pragma unroll
-                for (int w = 0; w < MW; ++w) c += __popc(lds_row_word<TM>(tile, r, w));
+                for (int ww = 0; ww < MW; ++ww) {
+                    const int k = r * MW + ww;
+                    c += __popc((w[k >> 1] >> ((k & 1) * 16)) & 0xffffu);
+                }
                 rc[r] = c;
                 nz += c;
             }
             nnzC[t0 + j] = nz;
-            {  // C row masks (all-zero for empty tiles); step 3 reads them back
-                static_assert((CM<TM>::TW32 % 4) == 0, "mask tile must be whole uint4");
-                const uint4 *src = reinterpret_cast<const uint4 *>(tile);
-                uint4 *dst = reinterpret_cast<uint4 *>(maskC + (size_t)(t0 + j) * CM<TM>::TW);
+            // C row masks (all-zero for empty tiles); step 3 reads them back
+            uint4 *dst = reinterpret_cast<uint4 *>(maskC + (size_t)(t0 + j) * CM<TM>::TW);
 #pragma unroll
-                for (int k = 0; k < TW32 / 4; ++k) dst[k] = src[k];
-            }
+            for (int k = 0; k < TW32 / 4; ++k) dst[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
         }
 #pragma unroll
         for (int r = 0; r < TM; ++r) {
@@ -1472,7 +1499,8 @@ __global__ __launch_bounds__(WG) void k_step3(const int4 *utab, const int4 *etab
     __shared__ __align__(16) u32 s_mask[CH * TW32];
     __shared__ __align__(16) double acc[S3_NZCAP];
     __shared__ __align__(16) double s_va[WG];
-    __shared__ u16 s_pre[(CH + 1) * TM];  // [j][r]: row-r nonzeros of the unit's tiles [0, j)
+    constexpr int PS = CH + 2;            // s_pre row stride (u16): rows start on distinct banks
+    __shared__ u16 s_pre[PS * TM];        // [r][j]: row-r nonzeros of the unit's tiles [0, j)
     __shared__ int s_cols[CH];
     __shared__ int s_off[CH + 1];         // [j]: nonzeros of the unit's tiles [0, j)
     __shared__ int s_rp[TM + 1];          // A CSR row starts of the tile row (ELEM)
@@ -1575,8 +1603,8 @@ __global__ __launch_bounds__(WG) void k_step3(const int4 *utab, const int4 *etab
 #pragma unroll
         for (int r = 0; r < TM; ++r) {
             const int g = r >> 2, sh = 16 * (r & 3);
-            s_pre[j * TM + r] = (u16)(((ipk[g] - pk[g]) >> sh) & 0xffffu);
-            if (j == WG - 1) s_pre[CH * TM + r] = (u16)((tot64[g] >> sh) & 0xffffu);
+            s_pre[r * PS + j] = (u16)(((ipk[g] - pk[g]) >> sh) & 0xffffu);
+            if (j == WG - 1) s_pre[r * PS + CH] = (u16)((tot64[g] >> sh) & 0xffffu);
         }
         s_off[j] = toff + itt - tt;
         if (j == WG - 1) s_off[CH] = ttot;
@@ -1621,8 +1649,8 @@ __global__ __launch_bounds__(WG) void k_step3(const int4 *utab, const int4 *etab
             int cnt_r = 0;
             if (threadIdx.x < 64) {  // wave 0: per-row counts of the pass and their offsets
                 const int r = threadIdx.x;
-                const int p0 = r < TM ? (int)s_pre[s_lo * TM + r] : 0;
-                cnt_r = r < TM ? (int)s_pre[s_hi * TM + r] - p0 : 0;
+                const int p0 = r < TM ? (int)s_pre[r * PS + s_lo] : 0;
+                cnt_r = r < TM ? (int)s_pre[r * PS + s_hi] - p0 : 0;
                 const int inc = wave_incl_scan(cnt_r);
                 if (r < TM) {
                     s_rowoff[r] = inc - cnt_r;
@@ -1643,7 +1671,7 @@ __global__ __launch_bounds__(WG) void k_step3(const int4 *utab, const int4 *etab
                         const double vb = E.vB[pb];
                         const int sl = lower_bound_dev(s_cols, s_lo, s_hi, x / TM);
                         if (sl >= s_hi || s_cols[sl] != x / TM) return;  // another pass's tile
-                        atomicAdd(&acc[s_rowbase[r] + (int)s_pre[sl * TM + r] +
+                        atomicAdd(&acc[s_rowbase[r] + (int)s_pre[r * PS + sl] +
                                        lds_rank<TM>(s_mask + sl * TW32, r, x % TM)],
                                   s_va[slot] * vb);
                     });
@@ -1663,7 +1691,7 @@ __global__ __launch_bounds__(WG) void k_step3(const int4 *utab, const int4 *etab
                                 const int ks = br[c], ke = br[c + 1];
                                 if (ks >= ke) continue;
                                 const double va = V.ValA[qa];
-                                const int rb = s_rowbase[r] + (int)s_pre[sl * TM + r];
+                                const int rb = s_rowbase[r] + (int)s_pre[r * PS + sl];
                                 for (int kb = ks; kb < ke; ++kb)
                                     atomicAdd(&acc[rb + lds_rank<TM>(tile, r, V.ColB[kb])], va * V.ValB[kb]);
                             }
@@ -1683,9 +1711,9 @@ __global__ __launch_bounds__(WG) void k_step3(const int4 *utab, const int4 *etab
                     int lo4 = s_lo, hi4 = s_hi - 1;   // tile holding it: last with pre <= kk
                     while (lo4 < hi4) {
                         const int mid = (lo4 + hi4 + 1) >> 1;
-                        if ((int)s_pre[mid * TM + r] <= kk) lo4 = mid; else hi4 = mid - 1;
+                        if ((int)s_pre[r * PS + mid] <= kk) lo4 = mid; else hi4 = mid - 1;
                     }
-                    int b = kk - (int)s_pre[lo4 * TM + r];
+                    int b = kk - (int)s_pre[r * PS + lo4];
                     int cl = 0;
 #pragma unroll
                     for (int ww = 0; ww < MW; ++ww) {
@@ -1706,7 +1734,7 @@ __global__ __launch_bounds__(WG) void k_step3(const int4 *utab, const int4 *etab
                     int out = nzbase + s_off[jt];
 #pragma unroll
                     for (int r = 0; r < TM; ++r) {
-                        int k = s_rowbase[r] + (int)s_pre[jt * TM + r];
+                        int k = s_rowbase[r] + (int)s_pre[r * PS + jt];
 #pragma unroll
                         for (int ww = 0; ww < MW; ++ww) {
                             u32 v = lds_row_word<TM>(tile, r, ww);
@@ -1752,10 +1780,8 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     C.tilem = tilemA; C.tilen = tilenB;
     if (ev) TSG_HIP(hipEventRecord(ev[0], s));
     // ---- step 1 ----
-    int win = ((tilenB + 8191) / 8192) * 8192;
-    if (win < 8192) win = 8192;
-    if (win > 65536) win = 65536;
-    const int nwin = (tilenB + win - 1) / win;
+    int win, nwin;
+    window_for(tilenB, &win, &nwin);
     if ((long)tilemA * nwin >= (1L << 31) - 1) return TSG_ERR_UNSUPPORTED;
     const long nunits1 = (long)tilemA * nwin;
     int *ucnt = nullptr;
