@@ -78,16 +78,17 @@ def cpu_baseline(m, n, rp, ci, vv, mb, nb, rpb, cib, vvb, budget_s):
                       f"({cub} of the intermediate products), {t:.1f} s"}
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary
-    (profiles/<round>_pmc.json, written by tools/profile.sh: 2*FETCH_SIZE +
-    WRITE_SIZE, separate --pmc passes).  (None, None) when absent."""
+def pmc_traffic(kernel, workload):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary of
+    the same workload (profiles/<round>_pmc.json, written by tools/profile.sh:
+    2*FETCH_SIZE + WRITE_SIZE, separate --pmc passes).  (None, None) when absent."""
     import glob
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc.json")))
+    files = [f for f in files if json.load(open(f)).get("_workload") == workload]
     if not files:
         return None, None
     d = json.load(open(files[-1]))
-    hits = [v for k, v in d.items() if kernel in k and v.get("hbm_bytes_per_dispatch")]
+    hits = [v for k, v in d.items() if kernel in k and isinstance(v, dict) and v.get("hbm_bytes_per_dispatch")]
     if not hits:
         return None, None
     best = max(hits, key=lambda v: v["dispatches"] or 0)
@@ -103,6 +104,9 @@ def main():
     ap.add_argument("--mtx", default=os.environ.get("TSG_MTX"))
     ap.add_argument("--aat", type=int, default=None)
     ap.add_argument("--tile", type=int, default=16)
+    ap.add_argument("--rows", type=int, default=None,
+                    help="A = its first ROWS rows (B whole); default: all rows, or for configs whose "
+                         "full product exceeds int32 nnz(C) (lj) the largest prefix with nnzCub <= 1.5e9")
     ap.add_argument("--cpu-budget-s", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -130,6 +134,17 @@ def main():
     else:
         mb, nb, rpb, cib, vvb = m, n, rp, ci, vv
     tm = args.tile
+    full_m = m
+    rows = args.rows
+    if rows is None:
+        blen = np.diff(rpb.astype(np.int64))
+        cum = np.concatenate([[0], np.cumsum(blen[ci])])[rp]  # nnzCub of row prefixes
+        if cum[-1] > 1.5e9:  # C = A^2 would overflow int32 nnz (as in the reference)
+            rows = int(np.searchsorted(cum, 1.5e9, side="right") - 1) // tm * tm
+            log(f"full product infeasible (nnzCub {int(cum[-1])}); using rows [0,{rows})")
+    if rows is not None and rows < m:
+        m, rp, ci, vv = rows, rp[:rows + 1].copy(), ci[:rp[rows]].copy(), vv[:rp[rows]].copy()
+        name = f"{name} rows[0,{rows}) of {full_m}"
     nnzcub_total = nnzcub_rows(rp, ci, rpb, 0, m)
     if world > 1:
         work = tdist.tile_row_work(rp, ci, rpb, m, tm)
@@ -139,7 +154,7 @@ def main():
     else:
         mblk, rpblk, ciblk, vvblk = m, rp, ci, vv
     dA = DeviceCSR.from_host(mblk, n, rpblk, ciblk, vvblk)
-    dB = dA if (not aat and world == 1) else DeviceCSR.from_host(mb, nb, rpb, cib, vvb)
+    dB = dA if (not aat and world == 1 and m == full_m) else DeviceCSR.from_host(mb, nb, rpb, cib, vvb)
     ctx = Context(local)
     torch.cuda.synchronize()
 
@@ -186,7 +201,9 @@ def main():
     # terms), timed with HIP events around its launch on the call's stream
     k3_ms = med["t_step3_kernel_ms"]
     achieved = b_alg / (k3_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic("k_step3")
+    workload = (f"{name} C=A{'*A^T' if aat else '^2'} fp64, {tm}x{tm} tiles, "
+                "csr2tile+steps1-3+tile2csr (device CSR in -> device CSR out)")
+    traffic, traffic_src = pmc_traffic("k_step3", workload)
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -199,8 +216,7 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "strong" if world > 1 else "weak",
             "vs_baseline": None, "dtype": "f64", "data": data_kind,
-            "config": {"workload": f"{name} C=A{'*A^T' if aat else '^2'} fp64, {tm}x{tm} tiles, "
-                                   "csr2tile+steps1-3+tile2csr (device CSR in -> device CSR out)",
+            "config": {"workload": workload,
                        "m": m, "nnzA": int(len(ci)), "nnzCub": nnzcub_total, "nnzC": nnzC,
                        "numtileA": int(med["numtileA"]), "numblkC": int(med["numblkC"]),
                        "parallelism": f"row-block{world}" if world > 1 else "single"},

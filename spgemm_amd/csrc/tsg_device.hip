@@ -135,8 +135,8 @@ template <class T> __global__ __launch_bounds__(WG) void k_scan_reduce(const T *
     if (threadIdx.x == 0) part[blockIdx.x] = tot;
 }
 
-template <class T>
-__global__ __launch_bounds__(WG) void k_scan_apply(T *a, long n, const T *part) {
+template <class T, class P = T>
+__global__ __launch_bounds__(WG) void k_scan_apply(T *a, long n, const P *part) {
     __shared__ T tile[SCAN_TILE + SCAN_TILE / 16];
     __shared__ T red[WAVES];
     long base = (long)blockIdx.x * SCAN_TILE;
@@ -151,7 +151,7 @@ __global__ __launch_bounds__(WG) void k_scan_apply(T *a, long n, const T *part) 
 #pragma unroll
     for (int k = 0; k < SCAN_ITEMS; ++k) s += tile[scan_pad(threadIdx.x * SCAN_ITEMS + k)];
     T tot;
-    T off = block_excl_scan(s, &tot, red) + (part ? part[blockIdx.x] : T(0));
+    T off = block_excl_scan(s, &tot, red) + (part ? (T)part[blockIdx.x] : T(0));
 #pragma unroll
     for (int k = 0; k < SCAN_ITEMS; ++k) {
         int li = scan_pad(threadIdx.x * SCAN_ITEMS + k);
@@ -172,7 +172,7 @@ template <class T> static int scan_exclusive(Context &cx, T *a, long n, hipStrea
     if (n <= 0) return TSG_OK;
     long nb = (n + SCAN_TILE - 1) / SCAN_TILE;
     if (nb == 1) {
-        k_scan_apply<T><<<1, WG, 0, s>>>(a, n, nullptr);
+        k_scan_apply<T><<<1, WG, 0, s>>>(a, n, (const T *)nullptr);
         TSG_HIP(hipGetLastError());
         return TSG_OK;
     }
@@ -188,6 +188,45 @@ template <class T> static int scan_exclusive(Context &cx, T *a, long n, hipStrea
 }
 
 int scan_exclusive_i32(Context &cx, int *a, long n, hipStream_t s) { return scan_exclusive(cx, a, n, s); }
+
+__global__ __launch_bounds__(WG) void k_scan_reduce_wide(const int *a, long n, long long *part) {
+    __shared__ long long red[WAVES];
+    const long base = (long)blockIdx.x * SCAN_TILE;
+    long long s = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        const long i = base + k * WG + threadIdx.x;
+        if (i < n) s += a[i];
+    }
+    const long long tot = block_sum(s, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+__global__ void k_set_i64(long long *p, long long v);
+
+// int32 exclusive scan whose block partials run in int64: *total = the exact
+// sum (read back synchronously); TSG_ERR_OVERFLOW, with `a` left unscanned,
+// when it does not fit an int32 index (C tile counts, nnz(C)).
+int scan_exclusive_i32_total(Context &cx, int *a, long n, hipStream_t s, long long *total) {
+    *total = 0;
+    if (n <= 0) return TSG_OK;
+    const long nb = (n + SCAN_TILE - 1) / SCAN_TILE;
+    long long *part = nullptr;
+    TSG_TRY(cx.get(&part, (size_t)nb + 1));
+    k_scan_reduce_wide<<<(unsigned)nb, WG, 0, s>>>(a, n, part);
+    k_set_i64<<<1, 1, 0, s>>>(part + nb, 0);
+    TSG_HIP(hipGetLastError());
+    TSG_TRY(scan_exclusive(cx, part, nb + 1, s));
+    TSG_TRY(read_i64(cx, part + nb, total, s));
+    if (*total > 0x7fffffffll) {
+        cx.put(part);
+        return TSG_ERR_OVERFLOW;
+    }
+    k_scan_apply<int, long long><<<(unsigned)nb, WG, 0, s>>>(a, n, part);
+    TSG_HIP(hipGetLastError());
+    cx.put(part);
+    return TSG_OK;
+}
 int scan_exclusive_i64(Context &cx, long long *a, long n, hipStream_t s) {
     return scan_exclusive(cx, a, n, s);
 }
@@ -396,6 +435,7 @@ __global__ void k_strided_starts(const int *rowptr, int m, int stride, int nseg,
 }
 
 __global__ void k_set_i32(int *p, int v) { *p = v; }
+__global__ void k_set_i64(long long *p, long long v) { *p = v; }
 
 __global__ __launch_bounds__(WG) void k_nnzcub(const int *colA, long nnzA, const int *rowptrB,
                                                u64 *out) {
@@ -1364,9 +1404,27 @@ __device__ __forceinline__ void elem_stream(const ECsr &E, int4 ue, const EPre &
 // pointers).  ELEM: masks from the CSR element products (sparse tiles);
 // otherwise from the tile products (B row masks ORed per A nonzero).
 // ---------------------------------------------------------------------------
+// TSG_ABLATE & 64: per-phase shader-clock totals of k_step3 (thread 0 of each
+// workgroup; diagnostics, printed by dev_tilespgemm)
+// (compiled in only with -DTSG_PROF_BUILD)
+__device__ unsigned long long g_prof[16];  // [0,8) step 3, [8,16) step 2
+#ifdef TSG_PROF_BUILD
+#define PROF_MARK(k)                                                         \
+    if ((ablate & 64) && threadIdx.x == 0) {                                 \
+        const u64 _t = __builtin_amdgcn_s_memtime();                         \
+        atomicAdd(&g_prof[k], _t - prof_t);                                  \
+        prof_t = _t;                                                         \
+    }
+#else
+#define PROF_MARK(k)
+#endif
+
 template <int TM, int TN, bool ELEM>
 __global__ __launch_bounds__(WG) void k_step2(const int4 *utab, const int4 *etab, int nunits, ABView V, ECsr E,
-                                              const int *Ccol, int *nnzC, int *unit_rc, u16 *maskC) {
+                                              const int *Ccol, int *nnzC, int *unit_rc, u16 *maskC, int ablate) {
+#ifdef TSG_PROF_BUILD
+    u64 prof_t = (ablate & 64) ? __builtin_amdgcn_s_memtime() : 0;
+#endif
     constexpr int MW = CM<TM>::MW, TW32 = CM<TM>::TW32;
     __shared__ __align__(16) u32 s_mask[CH * TW32];
     __shared__ int s_cols[CH];
@@ -1374,24 +1432,58 @@ __global__ __launch_bounds__(WG) void k_step2(const int4 *utab, const int4 *etab
     __shared__ int s_rp[TM + 1];
     __shared__ unsigned char s_r[WG];
     __shared__ ProdLds L;
-    int4 ut_n = make_int4(0, 0, 0, 0), ue_n = make_int4(0, 0, 0, 0);
+    // Software pipeline over this workgroup's units (stride G): the unit tables
+    // run two units ahead and the unit's first loads (C tile columns, split
+    // points, A row starts) one unit ahead, so the dependent HBM round trips of
+    // a unit overlap the previous unit's work.
+    struct UData {
+        int col, rp;
+        EPre pre;
+    };
+    const int G = gridDim.x;
+    auto load_data = [&](int4 ut, int4 ue) {
+        UData d{0, 0, {0, 0, 0.0}};
+        const int t0 = ut.y, ns = ut.w & 511;
+        if ((int)threadIdx.x < ns) d.col = Ccol[t0 + threadIdx.x];
+        if (ELEM) {
+            d.pre = epre_load(E, ue, false);
+            if (threadIdx.x <= TM) d.rp = E.rpA[min(ut.x * TM + (int)threadIdx.x, E.m)];
+        }
+        return d;
+    };
+    int4 ut_a = make_int4(0, 0, 0, 0), ue_a = ut_a, ut_b = ut_a, ue_b = ut_a;
+    UData d_a{0, 0, {0, 0, 0.0}};
     if ((int)blockIdx.x < nunits) {
-        ut_n = utab[blockIdx.x];
-        if (ELEM) ue_n = etab[blockIdx.x];
+        ut_a = utab[blockIdx.x];
+        if (ELEM) ue_a = etab[blockIdx.x];
+        d_a = load_data(ut_a, ue_a);
     }
-    for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
-        const int4 ut = ut_n, ue = ue_n;
-        if (u + (int)gridDim.x < nunits) {  // next unit's table entries, in flight during this one
-            ut_n = utab[u + gridDim.x];
-            if (ELEM) ue_n = etab[u + gridDim.x];
+    if ((int)blockIdx.x + G < nunits) {
+        ut_b = utab[blockIdx.x + G];
+        if (ELEM) ue_b = etab[blockIdx.x + G];
+    }
+    for (int u = blockIdx.x; u < nunits; u += G) {
+        const int4 ut = ut_a, ue = ue_a;
+        const UData d = d_a;
+        if (u + G < nunits) d_a = load_data(ut_b, ue_b);
+        ut_a = ut_b;
+        ue_a = ue_b;
+        if (u + 2 * G < nunits) {
+            ut_b = utab[u + 2 * G];
+            if (ELEM) ue_b = etab[u + 2 * G];
         }
         const int i = ut.x, t0 = ut.y, nu = ut.z, q = ut.w >> 9, ns = ut.w & 511;
-        EPre pre{0, 0, 0.0};
-        if (ELEM) pre = epre_load(E, ue, false);
-        unit_load_cols_zero<TM>(Ccol, t0, ns, s_cols, s_mask);
+        const EPre pre = d.pre;
+        if ((int)threadIdx.x < ns) s_cols[threadIdx.x] = d.col;
+        {
+            uint4 *m4 = reinterpret_cast<uint4 *>(s_mask);
+            const int n4 = (ns * TW32 + 3) / 4;
+            for (int x = threadIdx.x; x < n4; x += WG) m4[x] = make_uint4(0u, 0u, 0u, 0u);
+        }
         if (threadIdx.x < TM) s_rc[threadIdx.x] = 0;
-        if (ELEM && threadIdx.x <= TM) s_rp[threadIdx.x] = E.rpA[min(i * TM + (int)threadIdx.x, E.m)];
+        if (ELEM && threadIdx.x <= TM) s_rp[threadIdx.x] = d.rp;
         __syncthreads();
+        PROF_MARK(8);
         if (ELEM) {
             elem_stream<TM>(E, ue, pre, s_rp, false, 0, 0, s_r, nullptr, L, [&](int r, int, int pb) {
                 const int x = E.ciB[pb];
@@ -1403,6 +1495,7 @@ __global__ __launch_bounds__(WG) void k_step2(const int4 *utab, const int4 *etab
             int tot;
             unit_masks<TM, TN>(V, i, q, nu, V.Aptr[i], V.Aptr[i + 1], s_cols, ns, s_mask, L, &tot);
         }
+        PROF_MARK(9);
         int rc[TM];
 #pragma unroll
         for (int r = 0; r < TM; ++r) rc[r] = 0;
@@ -1441,6 +1534,7 @@ __global__ __launch_bounds__(WG) void k_step2(const int4 *utab, const int4 *etab
         __syncthreads();
         if (threadIdx.x < TM) unit_rc[(long)u * TM + threadIdx.x] = s_rc[threadIdx.x];
         __syncthreads();
+        PROF_MARK(10);
     }
 }
 
@@ -1472,20 +1566,6 @@ __device__ __forceinline__ int kth_col16(u32 v, int k) {
     return __ffs(w) - 1;
 }
 
-// TSG_ABLATE & 64: per-phase shader-clock totals of k_step3 (thread 0 of each
-// workgroup; diagnostics, printed by dev_tilespgemm)
-// (compiled in only with -DTSG_PROF_BUILD)
-__device__ unsigned long long g_prof[8];
-#ifdef TSG_PROF_BUILD
-#define PROF_MARK(k)                                                         \
-    if ((ablate & 64) && threadIdx.x == 0) {                                 \
-        const u64 _t = __builtin_amdgcn_s_memtime();                         \
-        atomicAdd(&g_prof[k], _t - prof_t);                                  \
-        prof_t = _t;                                                         \
-    }
-#else
-#define PROF_MARK(k)
-#endif
 
 template <int TM, int TN, bool WCSR, bool WTILE, bool ELEM>
 __global__ __launch_bounds__(WG) void k_step3(const int4 *utab, const int4 *etab, int nunits, int mrows, ABView V,
@@ -1796,11 +1876,12 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
         k_step1<0><<<g1, WG, 0, s>>>(A.tile_ptr, A.tile_columnidx, B.tile_ptr, B.tile_columnidx, tilemA, tilenB,
                                      nwin, win, ucnt, nullptr, nullptr, prod);
     TSG_HIP(hipGetLastError());
-    TSG_TRY(scan_exclusive_i32(cx, ucnt, nunits1 + 1, s));
+    long long numblk64 = 0;
+    TSG_TRY(scan_exclusive_i32_total(cx, ucnt, nunits1 + 1, s, &numblk64));  // overflow: > INT_MAX C tiles
     k_rows_from_units<<<grid_for(tilemA + 1, WG, 4096), WG, 0, s>>>(ucnt, tilemA, nwin, C.tile_ptr);
     TSG_HIP(hipMemcpyAsync(cx.pinned64, prod, sizeof(u64), hipMemcpyDeviceToHost, s));
-    int numblkC = 0;
-    TSG_TRY(read_i32(cx, C.tile_ptr + tilemA, &numblkC, s));
+    TSG_HIP(hipStreamSynchronize(s));
+    const int numblkC = (int)numblk64;
     long long tile_products = cx.pinned64[0];
     C.numtile = numblkC;
     const size_t nb1 = (size_t)numblkC + 1;
@@ -1879,16 +1960,21 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
                                                                       etab);
         TSG_HIP(hipGetLastError());
     }
+    if (g_ablate & 64) {
+        unsigned long long z[16] = {};
+        TSG_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_prof), z, sizeof(z), 0, hipMemcpyHostToDevice, s));
+    }
     if (numblkC > 0) {
         if (s2elem)
             k_step2<TM, TN, true><<<gu, WG, 0, s>>>(utab, etab, nunits, V, E, C.tile_columnidx, C.tile_nnz, unit_rc,
-                                                    C.mask);
+                                                    C.mask, g_ablate);
         else
             k_step2<TM, TN, false><<<gu, WG, 0, s>>>(utab, etab, nunits, V, E, C.tile_columnidx, C.tile_nnz, unit_rc,
-                                                     C.mask);
+                                                     C.mask, g_ablate);
     }
     TSG_HIP(hipGetLastError());
-    TSG_TRY(scan_exclusive_i32(cx, C.tile_nnz, (long)numblkC + 1, s));
+    long long nnz64 = 0;
+    TSG_TRY(scan_exclusive_i32_total(cx, C.tile_nnz, (long)numblkC + 1, s, &nnz64));  // nnz(C) must fit int32
     if (csr_out) {
         csr_out->m = A.m;
         csr_out->n = B.n;
@@ -1901,8 +1987,7 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
         TSG_HIP(hipGetLastError());
         TSG_TRY(scan_exclusive_i32(cx, csr_out->rowpointer, (long)A.m + 1, s));
     }
-    int nnzC = 0;
-    TSG_TRY(read_i32(cx, C.tile_nnz + numblkC, &nnzC, s));
+    const int nnzC = (int)nnz64;
     C.nnz = nnzC;
     if (ev) TSG_HIP(hipEventRecord(ev[2], s));
     // ---- step 3 ----
@@ -1914,10 +1999,6 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
         TSG_TRY(cx.get(&C.tile_csr_Ptr, nb1 * TM));
         TSG_TRY(cx.get(&C.tile_csr_Col, (size_t)nnzC + 1));
         TSG_TRY(cx.get(&C.tile_csr_Value, (size_t)nnzC + 1));
-    }
-    if (g_ablate & 64) {
-        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        TSG_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_prof), z, sizeof(z), 0, hipMemcpyHostToDevice, s));
     }
     if (ev) TSG_HIP(hipEventRecord(ev[4], s));
     if (csr_out) {
@@ -1940,11 +2021,14 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     TSG_HIP(hipGetLastError());
     if (ev) TSG_HIP(hipEventRecord(ev[5], s));
     if (g_ablate & 64) {
-        unsigned long long pr[8];
+        unsigned long long pr[16];
         TSG_HIP(hipMemcpyFromSymbolAsync(pr, HIP_SYMBOL(g_prof), sizeof(pr), 0, hipMemcpyDeviceToHost, s));
         TSG_HIP(hipStreamSynchronize(s));
-        double tot = 0;
+        double tot = 0, tot2 = 0;
         for (int k = 0; k < 8; ++k) tot += (double)pr[k];
+        for (int k = 8; k < 16; ++k) tot2 += (double)pr[k];
+        fprintf(stderr, "k_step2 phases (%% of WG-0 clock): load %.1f stream %.1f tail %.1f  total %.3g\n",
+                100 * pr[8] / tot2, 100 * pr[9] / tot2, 100 * pr[10] / tot2, tot2);
         fprintf(stderr, "k_step3 phases (%% of WG-0 clock): load %.1f prologue %.1f passinit %.1f values %.1f "
                 "write %.1f gap %.1f  total %.3g\n", 100 * pr[0] / tot, 100 * pr[1] / tot, 100 * pr[2] / tot,
                 100 * pr[3] / tot, 100 * pr[4] / tot, 100 * pr[7] / tot, tot);

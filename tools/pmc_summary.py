@@ -73,6 +73,8 @@ def main():
         for line in open(log):
             if line.startswith("{\"metric\""):
                 open(os.path.join(prof, f"{tag}_bench.json"), "w").write(line)
+                out["_workload"] = json.loads(line)["config"]["workload"]
+    json.dump(out, open(os.path.join(prof, f"{tag}_pmc.json"), "w"), indent=1, sort_keys=True)
     print(f"wrote profiles/{tag}_*")
 
 
