@@ -109,6 +109,11 @@ def main():
                          "full product exceeds int32 nnz(C) (lj) the largest prefix with nnzCub <= 1.5e9")
     ap.add_argument("--cpu-budget-s", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--check", action="store_true",
+                    help="add a checksum of the (gathered) C of the last step to the JSON line")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collective backend for N>1 (nccl = RCCL over xGMI; gloo = host-staged "
+                         "rehearsal of the multi-rank path, e.g. several ranks on one GPU)")
     args = ap.parse_args()
 
     import torch
@@ -117,12 +122,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    torch.cuda.set_device(local)
+    dev_id = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev_id)
     dist = None
+    host_coll = args.backend == "gloo"  # gloo collectives take host tensors
+    red_dev = "cpu" if host_coll else "cuda"
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if host_coll:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_id))
 
     from spgemm_amd.device import Context, DeviceCSR
     from spgemm_amd import dist as tdist
@@ -155,15 +166,20 @@ def main():
         mblk, rpblk, ciblk, vvblk = m, rp, ci, vv
     dA = DeviceCSR.from_host(mblk, n, rpblk, ciblk, vvblk)
     dB = dA if (not aat and world == 1 and m == full_m) else DeviceCSR.from_host(mb, nb, rpb, cib, vvb)
-    ctx = Context(local)
+    ctx = Context(dev_id)
     torch.cuda.synchronize()
+
+    gathered = [None]
 
     def one_step():
         ctx.reset()
         c, st = ctx.spgemm(dA, dB, tm, tm)
         if world > 1:
-            cblk = ctx.to_torch(c)
-            tdist.gather_csr_blocks(cblk.rowptr, cblk.col, cblk.val, rank, world)
+            cblk = ctx.view_torch(c)  # zero-copy views of the context-owned C block
+            if host_coll:
+                gathered[0] = tdist.gather_csr_blocks(cblk.rowptr.cpu(), cblk.col.cpu(), cblk.val.cpu(), rank, world)
+            else:
+                gathered[0] = tdist.gather_csr_blocks(cblk.rowptr, cblk.col, cblk.val, rank, world)
         return c, st
 
     for _ in range(args.warmup):
@@ -181,10 +197,10 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        nz = torch.tensor([c.nnz], dtype=torch.int64, device="cuda")
+        nz = torch.tensor([c.nnz], dtype=torch.int64, device=red_dev)
         dist.all_reduce(nz)
         nnzC = int(nz.item())
     else:
@@ -234,6 +250,13 @@ def main():
             "gflops_kern": round(2.0 * nnzcub_total / (med["t_kern_ms"] * 1e-3) / 1e9, 3) if world == 1 else None,
             "cpu_baseline": cpu,
         }
+        if args.check:
+            if world > 1:
+                g_rp, g_ci, g_vv = (x.cpu().numpy() for x in gathered[0])
+            else:
+                g_rp, g_ci, g_vv = ctx.to_host(c)[2:]
+            out["check"] = {"nnz": int(len(g_ci)), "rowptr_sum": int(g_rp.astype(np.int64).sum()),
+                            "col_sum": int(g_ci.astype(np.int64).sum()), "val_sum": float(g_vv.sum())}
         print(json.dumps(out), flush=True)
     ctx.close()
     if dist:

@@ -86,6 +86,26 @@ class Context:
             check("tsg_memcpy_d2d", L.tsg_memcpy_d2d(self.ptr, vv.data_ptr(), c.value, 8 * c.nnz, stream))
         return DeviceCSR(c.m, c.n, rp, ci[: c.nnz], vv[: c.nnz])
 
+    def view_torch(self, c):
+        """Zero-copy torch views of a context-owned DevCSR (valid until the next
+        reset of this context), via __cuda_array_interface__."""
+        import torch
+
+        class _Buf:
+            def __init__(self, ptr, n, typestr):
+                self.__cuda_array_interface__ = {"shape": (n,), "typestr": typestr, "data": (ptr or 0, False),
+                                                 "version": 2, "strides": None}
+
+        dev = torch.device("cuda", torch.cuda.current_device())
+        rp = torch.as_tensor(_Buf(c.rowpointer, c.m + 1, "<i4"), device=dev)
+        if c.nnz:
+            ci = torch.as_tensor(_Buf(c.columnindex, c.nnz, "<i4"), device=dev)
+            vv = torch.as_tensor(_Buf(c.value, c.nnz, "<f8"), device=dev)
+        else:
+            ci = torch.empty(0, dtype=torch.int32, device=dev)
+            vv = torch.empty(0, dtype=torch.float64, device=dev)
+        return DeviceCSR(c.m, c.n, rp, ci, vv)
+
     def to_host(self, c, stream=None):
         rp = np.empty(c.m + 1, dtype=np.int32)
         ci = np.empty(max(c.nnz, 1), dtype=np.int32)
