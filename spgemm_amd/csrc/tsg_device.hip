@@ -1042,6 +1042,29 @@ __global__ void k_unit_etab(const int4 *utab, int nunits, const int *rpA, int m,
     }
 }
 
+// Element split points, one wave per unit (parallel over units x entries, no
+// per-entry walk over all units of a hub row): entry x of the unit's tile row
+// starts its segment at the first B row position reaching the unit's first
+// tile column; the last unit also writes the row ends.
+template <int TM>
+__global__ __launch_bounds__(WG) void k_esplit_units(const int4 *utab, const int4 *etab, int nunits, const int *ciA,
+                                                     const int *rpB, const int *ciB, const int *Ccol, int *esplit) {
+    const int lane = lane_id();
+    for (int u = (blockIdx.x * WG + threadIdx.x) >> 6; u < nunits; u += gridDim.x * WAVES) {
+        const int4 ut = utab[u], ue = etab[u];
+        const int t0 = ut.y, nu = ut.z, q = ut.w >> 9;
+        const int e0 = ue.x, ei = ue.y;
+        int *sp = esplit + (((long long)(unsigned)ue.z) | ((long long)ue.w << 32));
+        const int key = Ccol[t0] * TM;
+        for (int x = lane; x < ei; x += 64) {
+            const int k = ciA[e0 + x];
+            const int b0 = rpB[k], b1 = rpB[k + 1];
+            sp[x] = q == 0 ? b0 : lower_bound_dev(ciB, b0, b1, key);
+            if (q == nu - 1) sp[ei + x] = b1;
+        }
+    }
+}
+
 __global__ __launch_bounds__(WG) void k_rows_unsorted2(const int *rp, const int *ci, int m, int *flag) {
     const int nnz = rp[m];
     for (int p = blockIdx.x * WG + threadIdx.x + 1; p < nnz; p += gridDim.x * WG) {
@@ -1948,16 +1971,16 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
         long long ne = 0;
         TSG_TRY(read_i64(cx, ebase + tilemA, &ne, s));
         TSG_TRY(cx.get(&esplit, (size_t)ne + 1));
-        k_esplit<TM><<<grid_for(Acsr->nnz, WG, 16384), WG, 0, s>>>(A.m, Acsr->rowpointer, Acsr->columnindex,
-                                                                   Bcsr->rowpointer, Bcsr->columnindex, uoff,
-                                                                   C.tile_ptr, C.tile_columnidx, ebase, esplit);
-        TSG_HIP(hipGetLastError());
         E = ECsr{A.m, Acsr->rowpointer, Acsr->columnindex, Acsr->value, Bcsr->rowpointer, Bcsr->columnindex,
                  Bcsr->value, esplit, ebase};
         TSG_TRY(cx.get(&etab, (size_t)maxu));
-        if (nunits > 0)
+        if (nunits > 0) {
             k_unit_etab<TM><<<grid_for(nunits, WG, 8192), WG, 0, s>>>(utab, nunits, Acsr->rowpointer, A.m, ebase,
                                                                       etab);
+            k_esplit_units<TM><<<grid_for(nunits, WAVES, 16384), WG, 0, s>>>(
+                utab, etab, nunits, Acsr->columnindex, Bcsr->rowpointer, Bcsr->columnindex, C.tile_columnidx,
+                esplit);
+        }
         TSG_HIP(hipGetLastError());
     }
     if (g_ablate & 64) {
