@@ -238,6 +238,8 @@ static int upload_tiles(Context &cx, const tsg_smatrix *M, int tile_m, int tile_
 }
 
 static bool quiet() { return getenv("TSG_QUIET") != nullptr; }
+static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B, hipStream_t s, tsg_dev_csr *C,
+                        tsg_stats *stats);
 
 // ------------------------------------------------------------------ C ABI
 extern "C" {
@@ -414,7 +416,7 @@ int tsg_nnzcub(const tsg_smatrix *A, const tsg_smatrix *B, unsigned long long *o
 
 int tsg_csr2tile_row_major(tsg_smatrix *A, int tm, int tn) {
     if (!A || !valid_tiles(tm, tn)) return TSG_ERR_INVALID;
-    if (!tile_size_supported(tm, tn)) return TSG_ERR_UNSUPPORTED;
+    if (!tile_side_supported(tm) || !tile_side_supported(tn)) return TSG_ERR_UNSUPPORTED;
     tsg_context *c;
     TSG_TRY(default_ctx(&c));
     Context &cx = c->cx;
@@ -430,7 +432,7 @@ int tsg_csr2tile_row_major(tsg_smatrix *A, int tm, int tn) {
 
 int tsg_csr2tile_col_major(tsg_smatrix *B, int tm, int tn) {
     if (!B || !valid_tiles(tm, tn)) return TSG_ERR_INVALID;
-    if (!tile_size_supported(tm, tn)) return TSG_ERR_UNSUPPORTED;
+    if (!tile_side_supported(tm) || !tile_side_supported(tn)) return TSG_ERR_UNSUPPORTED;
     tsg_context *c;
     TSG_TRY(default_ctx(&c));
     Context &cx = c->cx;
@@ -451,19 +453,47 @@ int tsg_tilespgemm(tsg_smatrix *A, tsg_smatrix *B, tsg_smatrix *C, unsigned int 
                    double *time_step3, double *time_malloc, int tm, int tn) {
     (void)bmA; (void)bmB; (void)bmlen; (void)densityA; (void)densityB; (void)filename;
     if (!A || !B || !C || !valid_tiles(tm, tn)) return TSG_ERR_INVALID;
-    if (!tile_size_supported(tm, tn)) return TSG_ERR_UNSUPPORTED;
+    if (!tile_side_supported(tm) || !tile_side_supported(tn)) return TSG_ERR_UNSUPPORTED;
     if (A->n != B->m || !A->tile_ptr || !B->tile_ptr || !B->mask || !B->csc_tile_ptr) return TSG_ERR_INVALID;
+    const bool native = tile_size_supported(tm, tn);
+    // other tile sizes: C by the 16x16 pipeline from the CSR operands, re-tiled
+    if (!native && (!A->rowpointer || !A->columnindex || !A->value || !B->rowpointer || !B->columnindex ||
+                    !B->value))
+        return TSG_ERR_INVALID;
     tsg_context *c;
     TSG_TRY(default_ctx(&c));
     Context &cx = c->cx;
     hipStream_t s = 0;
     tsg_dev_tiles dA, dB, dC;
+    tsg_dev_csr cA, cB;
     TSG_TRY(upload_tiles(cx, A, tm, tn, false, dA, s));
     TSG_TRY(upload_tiles(cx, B, tn, tm, true, dB, s));
+    if (!native) {
+        TSG_TRY(upload_csr(cx, A, cA, s));
+        TSG_TRY(upload_csr(cx, B, cB, s));
+    }
     TSG_HIP(hipStreamSynchronize(s));
     tsg_stats st{};
     auto h0 = std::chrono::steady_clock::now();
-    int rc = dev_tilespgemm(cx, dA, dB, dC, &st, s, cx.ev, nullptr);
+    int rc;
+    if (native) {
+        rc = dev_tilespgemm(cx, dA, dB, dC, &st, s, cx.ev, nullptr);
+    } else {
+        dC = tsg_dev_tiles{};
+        dC.m = A->m; dC.n = B->n; dC.tile_m = tm; dC.tile_n = tm;
+        dC.tilem = dA.tilem; dC.tilen = dB.tilen;
+        long long tp = 0;
+        tsg_dev_csr cC;
+        tsg_dev_tiles cne;
+        rc = hipEventRecord(cx.ev[11], s) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
+        if (rc == TSG_OK) rc = dev_step1(cx, dA, dB, dC, &tp, s);
+        if (rc == TSG_OK) rc = hipEventRecord(cx.ev[12], s) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
+        if (rc == TSG_OK) rc = dev_spgemm16(cx, &cA, &cB, s, &cC, nullptr);
+        if (rc == TSG_OK) rc = hipEventRecord(cx.ev[13], s) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
+        if (rc == TSG_OK) rc = dev_csr2tile_row_major(cx, cC, tm, tm, cne, s);
+        if (rc == TSG_OK) rc = dev_retile_c(cx, cne, dC, s);
+        if (rc == TSG_OK) rc = hipEventRecord(cx.ev[14], s) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
+    }
     if (rc == TSG_OK) TSG_HIP(hipStreamSynchronize(s));
     auto h1 = std::chrono::steady_clock::now();
     if (rc == TSG_OK) rc = dev_tiles_finalize_c(cx, dC, s);
@@ -474,7 +504,9 @@ int tsg_tilespgemm(tsg_smatrix *A, tsg_smatrix *B, tsg_smatrix *C, unsigned int 
     }
     cx.pool.release_all_live();
     if (rc != TSG_OK) return rc;
-    const double t1 = ev_ms(cx.ev[0], cx.ev[1]), t2 = ev_ms(cx.ev[1], cx.ev[2]), t3 = ev_ms(cx.ev[2], cx.ev[3]);
+    const int e0 = native ? 0 : 11;  // re-tiled sizes: step 1 | 16x16 pipeline | re-tiling
+    const double t1 = ev_ms(cx.ev[e0], cx.ev[e0 + 1]), t2 = ev_ms(cx.ev[e0 + 1], cx.ev[e0 + 2]),
+                 t3 = ev_ms(cx.ev[e0 + 2], cx.ev[e0 + 3]);
     const double tk = std::chrono::duration<double, std::milli>(h1 - h0).count();
     if (time_step1) *time_step1 = t1;
     if (time_step2) *time_step2 = t2;
@@ -499,7 +531,7 @@ int tsg_tilespgemm(tsg_smatrix *A, tsg_smatrix *B, tsg_smatrix *C, unsigned int 
 int tsg_tile2csr(tsg_smatrix *C, int tm, int tn) {
     (void)tn;
     if (!C || !C->tile_ptr || !valid_tiles(tm, tm)) return TSG_ERR_INVALID;
-    if (!tile_size_supported(tm, tm)) return TSG_ERR_UNSUPPORTED;
+    if (!tile_side_supported(tm)) return TSG_ERR_UNSUPPORTED;
     tsg_context *c;
     TSG_TRY(default_ctx(&c));
     Context &cx = c->cx;
@@ -620,12 +652,11 @@ static void release_tiles(Context &cx, tsg_dev_tiles &t) {
 // this (one 16-bit row-mask OR per A nonzero and B tile otherwise wins).
 static constexpr double kStep2ElemMaxTileDensity = 16.0;
 
-int tsg_dev_spgemm(tsg_context *ctx, const tsg_dev_csr *A, const tsg_dev_csr *B, int tm, int tn,
-                   void *stream, tsg_dev_csr *C, tsg_stats *stats) {
-    if (!ctx || !A || !B || !C || !valid_tiles(tm, tn) || A->n != B->m) return TSG_ERR_INVALID;
-    if (!tile_size_supported(tm, tn)) return TSG_ERR_UNSUPPORTED;
-    Context &cx = ctx->cx;
-    hipStream_t s = (hipStream_t)stream;
+// CSR in -> CSR out through the 16x16 tiled pipeline (C does not depend on the
+// tile size; other sizes are a layout choice of the host tile API).
+static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B, hipStream_t s, tsg_dev_csr *C,
+                        tsg_stats *stats) {
+    const int tm = 16, tn = 16;
     tsg_stats st{};
     tsg_dev_tiles tA, tB, tC;
     auto h0 = std::chrono::steady_clock::now();
@@ -687,10 +718,17 @@ int tsg_dev_spgemm(tsg_context *ctx, const tsg_dev_csr *A, const tsg_dev_csr *B,
     return TSG_OK;
 }
 
+int tsg_dev_spgemm(tsg_context *ctx, const tsg_dev_csr *A, const tsg_dev_csr *B, int tm, int tn,
+                   void *stream, tsg_dev_csr *C, tsg_stats *stats) {
+    if (!ctx || !A || !B || !C || !valid_tiles(tm, tn) || A->n != B->m) return TSG_ERR_INVALID;
+    if (!tile_side_supported(tm) || !tile_side_supported(tn)) return TSG_ERR_UNSUPPORTED;
+    return dev_spgemm16(ctx->cx, A, B, (hipStream_t)stream, C, stats);
+}
+
 int tsg_spgemm_csr(const tsg_smatrix *A, const tsg_smatrix *B, tsg_smatrix *C, int tm, int tn,
                    tsg_stats *stats) {
     if (!A || !B || !C || A->n != B->m || !valid_tiles(tm, tn)) return TSG_ERR_INVALID;
-    if (!tile_size_supported(tm, tn)) return TSG_ERR_UNSUPPORTED;
+    if (!tile_side_supported(tm) || !tile_side_supported(tn)) return TSG_ERR_UNSUPPORTED;
     tsg_context *c;
     TSG_TRY(default_ctx(&c));
     Context &cx = c->cx;

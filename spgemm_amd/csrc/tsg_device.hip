@@ -794,19 +794,43 @@ static int csr2tile_impl(Context &cx, const tsg_dev_csr &M, bool colmajor, tsg_d
     return TSG_OK;
 }
 
+// The SpGEMM steps are built for 16x16 tiles; csr2tile / tile2csr for every
+// valid reference tile size with sides in {16, 32, 64}.
 bool tile_size_supported(int tm, int tn) { return tm == 16 && tn == 16; }
+bool tile_side_supported(int t) { return t == 16 || t == 32 || t == 64; }
+
+template <int TR>
+static int csr2tile_dispatch_c(Context &cx, const tsg_dev_csr &M, int tc, bool colmajor, tsg_dev_tiles &out,
+                               hipStream_t s) {
+    switch (tc) {
+    case 16: return csr2tile_impl<TR, 16>(cx, M, colmajor, out, s);
+    case 32: return csr2tile_impl<TR, 32>(cx, M, colmajor, out, s);
+    case 64: return csr2tile_impl<TR, 64>(cx, M, colmajor, out, s);
+    default: return TSG_ERR_UNSUPPORTED;
+    }
+}
+
+static int csr2tile_dispatch(Context &cx, const tsg_dev_csr &M, int tr, int tc, bool colmajor, tsg_dev_tiles &out,
+                             hipStream_t s) {
+    switch (tr) {
+    case 16: return csr2tile_dispatch_c<16>(cx, M, tc, colmajor, out, s);
+    case 32: return csr2tile_dispatch_c<32>(cx, M, tc, colmajor, out, s);
+    case 64: return csr2tile_dispatch_c<64>(cx, M, tc, colmajor, out, s);
+    default: return TSG_ERR_UNSUPPORTED;
+    }
+}
 
 int dev_csr2tile_row_major(Context &cx, const tsg_dev_csr &A, int tm, int tn, tsg_dev_tiles &out,
                            hipStream_t s) {
-    if (!tile_size_supported(tm, tn)) return TSG_ERR_UNSUPPORTED;
-    return csr2tile_impl<16, 16>(cx, A, false, out, s);
+    if (!tile_side_supported(tm) || !tile_side_supported(tn)) return TSG_ERR_UNSUPPORTED;
+    return csr2tile_dispatch(cx, A, tm, tn, false, out, s);
 }
 
 int dev_csr2tile_col_major(Context &cx, const tsg_dev_csr &B, int tm, int tn, tsg_dev_tiles &out,
                            hipStream_t s) {
-    if (!tile_size_supported(tm, tn)) return TSG_ERR_UNSUPPORTED;
+    if (!tile_side_supported(tm) || !tile_side_supported(tn)) return TSG_ERR_UNSUPPORTED;
     // B tiles are tn rows x tm cols
-    return csr2tile_impl<16, 16>(cx, B, true, out, s);
+    return csr2tile_dispatch(cx, B, tn, tm, true, out, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -1864,25 +1888,12 @@ __global__ __launch_bounds__(WG) void k_step3(const int4 *utab, const int4 *etab
 // step 3 so that their cost can be measured: 1 masks, 4 values, 8 CSR writes.
 static int g_ablate = -1;
 
-int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_dev_tiles &C,
-                   tsg_stats *st, hipStream_t s, hipEvent_t *ev, tsg_dev_csr *csr_out, const tsg_dev_csr *Acsr,
-                   const tsg_dev_csr *Bcsr, bool step2_elem) {
-    if (g_ablate < 0) g_ablate = getenv("TSG_ABLATE") ? atoi(getenv("TSG_ABLATE")) : 0;
-    constexpr int TM = 16, TN = 16;
-    if (A.tile_m != TM || A.tile_n != TN || B.tile_m != TN || B.tile_n != TM) return TSG_ERR_UNSUPPORTED;
-    // element streaming needs the CSR operands (B rows column-sorted: caller's check)
-    const bool have_csr = Acsr && Bcsr && Acsr->m == A.m && Bcsr->m == B.m && Acsr->nnz > 0;
-    const bool s3elem = csr_out && have_csr && !(g_ablate & 16);
-    const bool s2elem = step2_elem && have_csr;
-    const bool tilepay = !(s2elem && s3elem);  // some step reads the tile payloads
-    if (A.n != B.m) return TSG_ERR_INVALID;
-    if (tilepay && (!B.rm_mask || !B.rm_rowstart || !A.tile_csr_Col || !A.tile_nnz)) return TSG_ERR_INVALID;
+// Step 1 (C tile structure = tile-pattern product of A's and B's row-major tile
+// structures; includes tiles whose element product is empty, as the reference).
+// Works for any tile sizes: only tile_ptr / tile_columnidx are read.
+int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_dev_tiles &C,
+              long long *tile_products_out, hipStream_t s) {
     const int tilemA = A.tilem, tilenB = B.tilen;
-    C = tsg_dev_tiles{};
-    C.m = A.m; C.n = B.n; C.tile_m = TM; C.tile_n = TM;
-    C.tilem = tilemA; C.tilen = tilenB;
-    if (ev) TSG_HIP(hipEventRecord(ev[0], s));
-    // ---- step 1 ----
     int win, nwin;
     window_for(tilenB, &win, &nwin);
     if ((long)tilemA * nwin >= (1L << 31) - 1) return TSG_ERR_UNSUPPORTED;
@@ -1915,6 +1926,33 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     TSG_HIP(hipGetLastError());
     cx.put(ucnt);
     cx.put(prod);
+    *tile_products_out = tile_products;
+    return TSG_OK;
+}
+
+int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_dev_tiles &C,
+                   tsg_stats *st, hipStream_t s, hipEvent_t *ev, tsg_dev_csr *csr_out, const tsg_dev_csr *Acsr,
+                   const tsg_dev_csr *Bcsr, bool step2_elem) {
+    if (g_ablate < 0) g_ablate = getenv("TSG_ABLATE") ? atoi(getenv("TSG_ABLATE")) : 0;
+    constexpr int TM = 16, TN = 16;
+    if (A.tile_m != TM || A.tile_n != TN || B.tile_m != TN || B.tile_n != TM) return TSG_ERR_UNSUPPORTED;
+    // element streaming needs the CSR operands (B rows column-sorted: caller's check)
+    const bool have_csr = Acsr && Bcsr && Acsr->m == A.m && Bcsr->m == B.m && Acsr->nnz > 0;
+    const bool s3elem = csr_out && have_csr && !(g_ablate & 16);
+    const bool s2elem = step2_elem && have_csr;
+    const bool tilepay = !(s2elem && s3elem);  // some step reads the tile payloads
+    if (A.n != B.m) return TSG_ERR_INVALID;
+    if (tilepay && (!B.rm_mask || !B.rm_rowstart || !A.tile_csr_Col || !A.tile_nnz)) return TSG_ERR_INVALID;
+    const int tilemA = A.tilem, tilenB = B.tilen;
+    C = tsg_dev_tiles{};
+    C.m = A.m; C.n = B.n; C.tile_m = TM; C.tile_n = TM;
+    C.tilem = tilemA; C.tilen = tilenB;
+    if (ev) TSG_HIP(hipEventRecord(ev[0], s));
+    // ---- step 1 ----
+    long long tile_products = 0;
+    TSG_TRY(dev_step1(cx, A, B, C, &tile_products, s));
+    const int numblkC = C.numtile;
+    const size_t nb1 = (size_t)numblkC + 1;
     if (ev) TSG_HIP(hipEventRecord(ev[1], s));
     // ---- step 2 ----
     int *uoff = nullptr, *urow = nullptr, *unit_rc = nullptr, *unit_rb = nullptr;
@@ -2075,6 +2113,59 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     return TSG_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Re-tiling for tile sizes other than 16x16 (host tile API): the C CSR of the
+// 16x16 pipeline, tiled at tm x tm (csr2tile), is scattered into the step-1
+// C tile list of that size (which also holds the structurally empty tiles).
+// Payload order is the same in both lists (tiles ascending, then rows, then
+// columns), so Col/Value carry over; Ptr, mask and nnz move tile by tile.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(WG) void k_retile_scatter(int numne, const int *ne_row, const int *ne_col,
+                                                       const int *ne_nnz, const u16 *ne_Ptr, const u16 *ne_mask,
+                                                       int tm, const int *Cptr, const int *Ccol, int *cnt,
+                                                       u16 *Ptr, u16 *mask) {
+    const int mwords = tm * (tm / 16);
+    for (int t = blockIdx.x * WG + threadIdx.x; t < numne; t += gridDim.x * WG) {
+        const int i = ne_row[t];
+        const int p = lower_bound_dev(Ccol, Cptr[i], Cptr[i + 1], ne_col[t]);
+        cnt[p] = ne_nnz[t + 1] - ne_nnz[t];
+        for (int r = 0; r < tm; ++r) Ptr[(size_t)p * tm + r] = ne_Ptr[(size_t)t * tm + r];
+        for (int w = 0; w < mwords; ++w) mask[(size_t)p * mwords + w] = ne_mask[(size_t)t * mwords + w];
+    }
+}
+
+__global__ __launch_bounds__(WG) void k_col_local(const u16 *enc, long n, int tm, u16 *col) {
+    for (long k = (long)blockIdx.x * WG + threadIdx.x; k < n; k += (long)gridDim.x * WG) col[k] = enc[k] % tm;
+}
+
+int dev_retile_c(Context &cx, const tsg_dev_tiles &Cne, tsg_dev_tiles &C, hipStream_t s) {
+    const int tm = C.tile_m, mwords = tm * (tm / 16);
+    const size_t nb1 = (size_t)C.numtile + 1;
+    C.nnz = Cne.nnz;
+    TSG_TRY(cx.get(&C.tile_nnz, nb1));
+    TSG_TRY(cx.get(&C.tile_csr_Ptr, nb1 * tm));
+    TSG_TRY(cx.get(&C.mask, nb1 * mwords));
+    TSG_TRY(cx.get(&C.tile_csr_Col, (size_t)C.nnz + 1));
+    TSG_TRY(cx.get(&C.tile_csr_Value, (size_t)C.nnz + 1));
+    TSG_HIP(hipMemsetAsync(C.tile_nnz, 0, nb1 * sizeof(int), s));
+    TSG_HIP(hipMemsetAsync(C.tile_csr_Ptr, 0, nb1 * tm * sizeof(u16), s));
+    TSG_HIP(hipMemsetAsync(C.mask, 0, nb1 * mwords * sizeof(u16), s));
+    if (Cne.numtile > 0)
+        k_retile_scatter<<<grid_for(Cne.numtile, WG, 8192), WG, 0, s>>>(
+            Cne.numtile, Cne.tile_rowidx, Cne.tile_columnidx, Cne.tile_nnz, Cne.tile_csr_Ptr, Cne.mask, tm,
+            C.tile_ptr, C.tile_columnidx, C.tile_nnz, C.tile_csr_Ptr, C.mask);
+    TSG_HIP(hipGetLastError());
+    long long tot = 0;
+    TSG_TRY(scan_exclusive_i32_total(cx, C.tile_nnz, (long)nb1, s, &tot));
+    if (C.nnz > 0) {
+        k_col_local<<<grid_for(C.nnz, WG, 16384), WG, 0, s>>>(Cne.tile_csr_Col, C.nnz, tm, C.tile_csr_Col);
+        TSG_HIP(hipMemcpyAsync(C.tile_csr_Value, Cne.tile_csr_Value, (size_t)C.nnz * sizeof(double),
+                               hipMemcpyDeviceToDevice, s));
+    }
+    TSG_HIP(hipGetLastError());
+    return TSG_OK;
+}
+
 __global__ void k_zero_empty_ptr(const int *nnzoff, int numtile, int tm, u16 *Ptr, u16 *mask) {
     const int mw = tm / 16;
     for (long x = (long)blockIdx.x * WG + threadIdx.x; x < (long)numtile * tm; x += (long)gridDim.x * WG) {
@@ -2215,8 +2306,19 @@ __global__ __launch_bounds__(WG) void k_t2c_fill(const int *Cptr, const int *Cco
     }
 }
 
+template <int TM>
+static void t2c_launch_count(const tsg_dev_tiles &C, int *rowcnt, int g, hipStream_t s) {
+    k_t2c_count<TM><<<g, WG, 0, s>>>(C.tile_ptr, C.tilem, C.m, C.tile_nnz, C.tile_csr_Ptr, rowcnt);
+}
+
+template <int TM>
+static void t2c_launch_fill(const tsg_dev_tiles &C, tsg_dev_csr &out, int g, hipStream_t s) {
+    k_t2c_fill<TM><<<g, WG, 0, s>>>(C.tile_ptr, C.tile_columnidx, C.tilem, C.m, C.tile_nnz, C.tile_csr_Ptr,
+                                    C.tile_csr_Col, C.tile_csr_Value, out.rowpointer, out.columnindex, out.value);
+}
+
 int dev_tile2csr(Context &cx, const tsg_dev_tiles &C, tsg_dev_csr &out, hipStream_t s) {
-    if (C.tile_m != 16) return TSG_ERR_UNSUPPORTED;
+    if (!tile_side_supported(C.tile_m)) return TSG_ERR_UNSUPPORTED;
     out.m = C.m;
     out.n = C.n;
     out.nnz = C.nnz;
@@ -2225,14 +2327,18 @@ int dev_tile2csr(Context &cx, const tsg_dev_tiles &C, tsg_dev_csr &out, hipStrea
     TSG_TRY(cx.get(&out.value, (size_t)C.nnz + 1));
     TSG_HIP(hipMemsetAsync(out.rowpointer, 0, ((size_t)C.m + 1) * sizeof(int), s));
     const int g = grid_for(C.tilem, WAVES, 8192);
-    if (C.tilem > 0)
-        k_t2c_count<16><<<g, WG, 0, s>>>(C.tile_ptr, C.tilem, C.m, C.tile_nnz, C.tile_csr_Ptr, out.rowpointer);
+    if (C.tilem > 0) {
+        if (C.tile_m == 16) t2c_launch_count<16>(C, out.rowpointer, g, s);
+        else if (C.tile_m == 32) t2c_launch_count<32>(C, out.rowpointer, g, s);
+        else t2c_launch_count<64>(C, out.rowpointer, g, s);
+    }
     TSG_HIP(hipGetLastError());
     TSG_TRY(scan_exclusive_i32(cx, out.rowpointer, (long)C.m + 1, s));
-    if (C.tilem > 0 && C.nnz > 0)
-        k_t2c_fill<16><<<g, WG, 0, s>>>(C.tile_ptr, C.tile_columnidx, C.tilem, C.m, C.tile_nnz, C.tile_csr_Ptr,
-                                        C.tile_csr_Col, C.tile_csr_Value, out.rowpointer, out.columnindex,
-                                        out.value);
+    if (C.tilem > 0 && C.nnz > 0) {
+        if (C.tile_m == 16) t2c_launch_fill<16>(C, out, g, s);
+        else if (C.tile_m == 32) t2c_launch_fill<32>(C, out, g, s);
+        else t2c_launch_fill<64>(C, out, g, s);
+    }
     TSG_HIP(hipGetLastError());
     return TSG_OK;
 }

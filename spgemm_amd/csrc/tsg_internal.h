@@ -93,6 +93,11 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
                    tsg_stats *st, hipStream_t s, hipEvent_t *ev_marks, tsg_dev_csr *csr_out,
                    const tsg_dev_csr *Acsr = nullptr, const tsg_dev_csr *Bcsr = nullptr,
                    bool step2_elem = false);
+// step 1 alone: C tile structure (tile_ptr, tile_columnidx, numtile) of any tile size
+int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_dev_tiles &C,
+              long long *tile_products, hipStream_t s);
+// C payload for a step-1 structure C (tile_m set) from the non-empty tiles Cne of C's CSR
+int dev_retile_c(Context &cx, const tsg_dev_tiles &Cne, tsg_dev_tiles &C, hipStream_t s);
 // tile_ptr + tile_columnidx of a CSR's tiling (tr x tc tiles), no payload
 int dev_tile_structure(Context &cx, const tsg_dev_csr &M, int tr, int tc, tsg_dev_tiles &out, hipStream_t s);
 // whether every CSR row is column-sorted (synchronous)
@@ -103,6 +108,7 @@ int dev_tile2csr(Context &cx, const tsg_dev_tiles &C, tsg_dev_csr &out, hipStrea
 int read_i32(Context &cx, const int *d, int *h, hipStream_t s);
 int read_i64(Context &cx, const long long *d, long long *h, hipStream_t s);
 
-bool tile_size_supported(int tm, int tn);
+bool tile_size_supported(int tm, int tn);  // the SpGEMM steps (16x16)
+bool tile_side_supported(int t);         // csr2tile / tile2csr sides: 16, 32, 64
 
 }  // namespace tsg

@@ -21,7 +21,7 @@ RTOL = 1e-10
 TILE_KEYS = ("tile_ptr", "tile_columnidx", "tile_nnz", "tile_csr_Ptr", "tile_csr_Col", "tile_csr_Value", "mask")
 # C's masks are device-internal in the reference too (never copied back, src/tilespgemm-cuda.h:2749-2775)
 C_KEYS = TILE_KEYS[:-1]
-SUPPORTED = {(16, 16)}
+SUPPORTED = {(16, 16), (32, 16), (32, 32)}  # every tile size the goldens hold
 
 
 def g(npz, key):
@@ -194,8 +194,8 @@ def test_device_api_matches_host_api():
     ctx.close()
 
 
-@pytest.mark.parametrize("aat", [0, 1])
-def test_cli_reports_reference_lines(aat, tmp_path):
+@pytest.mark.parametrize("aat,tiles", [(0, ("16", "16")), (1, ("16", "16")), (0, ("32", "32")), (0, ("64", "16"))])
+def test_cli_reports_reference_lines(aat, tiles, tmp_path):
     """./test -d 0 -aat X <mtx> 16 16 prints the reference's key lines with the
     oracle's nnzCub / nnzC and writes the CSV (creating the directory)."""
     import re
@@ -203,7 +203,7 @@ def test_cli_reports_reference_lines(aat, tmp_path):
     cli = os.path.join(os.path.dirname(T._lib.LIB_PATH), "..", "bin", "test")
     path = os.path.join(FIXTURES, "banded_36x36.mtx")
     out = tmp_path / "data"
-    r = subprocess.run([cli, "-d", "0", "-aat", str(aat), path, "16", "16"], capture_output=True, text=True,
+    r = subprocess.run([cli, "-d", "0", "-aat", str(aat), path, *tiles], capture_output=True, text=True,
                        timeout=300, env=dict(os.environ, TSG_DATA_DIR=str(out)))
     assert r.returncode == 0, r.stderr
     oA = O.OMat.load(path)
