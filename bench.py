@@ -20,6 +20,10 @@ import time
 
 import numpy as np
 
+# CPU baseline threads stay on neighbouring cores; must be set
+# before any OpenMP runtime (torch's or the oracle's) initialises
+os.environ.setdefault("OMP_PROC_BIND", "close")
+
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
@@ -56,26 +60,49 @@ def nnzcub_rows(rp_a, ci_a, rp_b, r0, r1):
     return int(blen[ci_a[s:e]].sum())
 
 
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _timed_prefix(fn, m, budget_s):
+    """Run fn(rows) on a growing row prefix until it takes ~budget_s; (rows, seconds)."""
+    rows = min(m, 2000)
+    t0 = time.perf_counter()
+    fn(rows)
+    t = time.perf_counter() - t0
+    rows2 = int(min(m, max(rows, rows * budget_s / max(t, 1e-6))))
+    t0 = time.perf_counter()
+    fn(rows2)
+    return rows2, time.perf_counter() - t0
+
+
 def cpu_baseline(m, n, rp, ci, vv, mb, nb, rpb, cib, vvb, budget_s):
     """The reference's CPU SPA (spgemm_serialref_spa_new.h, clean-room oracle
-    restatement, both passes) on a bounded row prefix of the same workload."""
+    restatement, both passes; symbolic only) on a bounded row prefix of the same
+    workload, plus the oracle's numeric Gustavson timed beside it."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import _oracle as O
     A = O.OMat.from_csr(m, n, rp, ci, vv)
     B = O.OMat.from_csr(mb, nb, rpb, cib, vvb)
-    rows = min(m, 2000)
-    t0 = time.perf_counter()
-    O.spa(A, B, 0, rows)
-    t = time.perf_counter() - t0
-    rows2 = int(min(m, max(rows, rows * budget_s / max(t, 1e-6))))
-    t0 = time.perf_counter()
-    O.spa(A, B, 0, rows2)
-    t = time.perf_counter() - t0
-    cub = nnzcub_rows(rp, ci, rpb, 0, rows2)
-    return {"value": round(2.0 * cub / t / 1e9, 4), "unit": "GFLOPS", "cores": O.num_threads(),
+    rows, t = _timed_prefix(lambda r: O.spa(A, B, 0, r), m, budget_s)
+    cub = nnzcub_rows(rp, ci, rpb, 0, rows)
+    nrows, nt = _timed_prefix(lambda r: O.gustavson_rows(A, B, 0, r), m, budget_s / 2)
+    ncub = nnzcub_rows(rp, ci, rpb, 0, nrows)
+    thr = O.num_threads()
+    return {"value": round(2.0 * cub / t / 1e9, 4), "unit": "GFLOPS", "cores": thr,
             "kind": "port",
-            "sample": f"spgemm_spa restatement (count+fill passes), rows [0,{rows2}) of {m} "
-                      f"({cub} of the intermediate products), {t:.1f} s"}
+            "sample": f"spgemm_spa restatement (count+fill passes, symbolic), rows [0,{rows}) of {m} "
+                      f"({cub} of the intermediate products), {t:.1f} s; {thr} OpenMP threads "
+                      f"(OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND', 'unset')}) on {_cpu_model()}",
+            "numeric": {"value": round(2.0 * ncub / nt / 1e9, 4), "unit": "GFLOPS",
+                        "sample": f"oracle Gustavson (dense-row accumulator, fp64 values), rows [0,{nrows}), "
+                                  f"{nt:.1f} s"}}
 
 
 def pmc_traffic(kernel, workload):
@@ -209,6 +236,7 @@ def main():
     gflops = 2.0 * nnzcub_total * args.steps / elapsed / 1e9
 
     med = {k: float(np.median([s[k] for s in stats])) for k in stats[0]}
+    mins = {k: float(np.min([s[k] for s in stats])) for k in ("t_e2e_ms", "t_kern_ms")}
     dev_ms = med["t_csr2tile_ms"] + med["t_step1_ms"] + med["t_step2_ms"] + med["t_step3_ms"] + med["t_tile2csr_ms"]
     # SURVEY §8d algorithmic bytes (src/external/cusparse/main.cu:205-208), this rank's share
     b_alg = 4.0 * (mblk + 1) + 12.0 * len(ciblk) + 4.0 * (mb + 1) + 12.0 * len(cib) + 4.0 * (mblk + 1) + 12.0 * c.nnz
@@ -247,6 +275,7 @@ def main():
             "stage_ms": {k: round(med[k], 4) for k in ("t_csr2tile_ms", "t_step1_ms", "t_step2_ms",
                                                         "t_step3_ms", "t_step3_kernel_ms", "t_tile2csr_ms", "t_malloc_ms",
                                                         "t_kern_ms", "t_e2e_ms")},
+            "stage_ms_min": {k: round(v, 4) for k, v in mins.items()},
             "gflops_kern": round(2.0 * nnzcub_total / (med["t_kern_ms"] * 1e-3) / 1e9, 3) if world == 1 else None,
             "cpu_baseline": cpu,
         }
