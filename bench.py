@@ -197,16 +197,20 @@ def main():
     torch.cuda.synchronize()
 
     gathered = [None]
+    gather_ms = []
 
     def one_step():
         ctx.reset()
-        c, st = ctx.spgemm(dA, dB, tm, tm)
+        c, st = ctx.spgemm(dA, dB, tm, tm)  # returns with C complete on the device
         if world > 1:
+            g0 = time.perf_counter()
             cblk = ctx.view_torch(c)  # zero-copy views of the context-owned C block
             if host_coll:
                 gathered[0] = tdist.gather_csr_blocks(cblk.rowptr.cpu(), cblk.col.cpu(), cblk.val.cpu(), rank, world)
             else:
                 gathered[0] = tdist.gather_csr_blocks(cblk.rowptr, cblk.col, cblk.val, rank, world)
+                torch.cuda.synchronize()
+            gather_ms.append((time.perf_counter() - g0) * 1e3)
         return c, st
 
     for _ in range(args.warmup):
@@ -276,6 +280,7 @@ def main():
                                                         "t_step3_ms", "t_step3_kernel_ms", "t_tile2csr_ms", "t_malloc_ms",
                                                         "t_kern_ms", "t_e2e_ms")},
             "stage_ms_min": {k: round(v, 4) for k, v in mins.items()},
+            "gather_ms": round(float(np.median(gather_ms[-args.steps:])), 4) if gather_ms else None,
             "gflops_kern": round(2.0 * nnzcub_total / (med["t_kern_ms"] * 1e-3) / 1e9, 3) if world == 1 else None,
             "cpu_baseline": cpu,
         }

@@ -797,7 +797,7 @@ static int csr2tile_impl(Context &cx, const tsg_dev_csr &M, bool colmajor, tsg_d
 // The SpGEMM steps are built for 16x16 tiles; csr2tile / tile2csr for every
 // valid reference tile size with sides in {16, 32, 64}.
 bool tile_size_supported(int tm, int tn) { return tm == 16 && tn == 16; }
-bool tile_side_supported(int t) { return t == 16 || t == 32 || t == 64; }
+bool tile_side_supported(int t) { return t == 16 || t == 32 || t == 48 || t == 64; }
 
 template <int TR>
 static int csr2tile_dispatch_c(Context &cx, const tsg_dev_csr &M, int tc, bool colmajor, tsg_dev_tiles &out,
@@ -805,6 +805,7 @@ static int csr2tile_dispatch_c(Context &cx, const tsg_dev_csr &M, int tc, bool c
     switch (tc) {
     case 16: return csr2tile_impl<TR, 16>(cx, M, colmajor, out, s);
     case 32: return csr2tile_impl<TR, 32>(cx, M, colmajor, out, s);
+    case 48: return csr2tile_impl<TR, 48>(cx, M, colmajor, out, s);
     case 64: return csr2tile_impl<TR, 64>(cx, M, colmajor, out, s);
     default: return TSG_ERR_UNSUPPORTED;
     }
@@ -815,6 +816,7 @@ static int csr2tile_dispatch(Context &cx, const tsg_dev_csr &M, int tr, int tc, 
     switch (tr) {
     case 16: return csr2tile_dispatch_c<16>(cx, M, tc, colmajor, out, s);
     case 32: return csr2tile_dispatch_c<32>(cx, M, tc, colmajor, out, s);
+    case 48: return csr2tile_dispatch_c<48>(cx, M, tc, colmajor, out, s);
     case 64: return csr2tile_dispatch_c<64>(cx, M, tc, colmajor, out, s);
     default: return TSG_ERR_UNSUPPORTED;
     }
@@ -2330,6 +2332,7 @@ int dev_tile2csr(Context &cx, const tsg_dev_tiles &C, tsg_dev_csr &out, hipStrea
     if (C.tilem > 0) {
         if (C.tile_m == 16) t2c_launch_count<16>(C, out.rowpointer, g, s);
         else if (C.tile_m == 32) t2c_launch_count<32>(C, out.rowpointer, g, s);
+        else if (C.tile_m == 48) t2c_launch_count<48>(C, out.rowpointer, g, s);
         else t2c_launch_count<64>(C, out.rowpointer, g, s);
     }
     TSG_HIP(hipGetLastError());
@@ -2337,6 +2340,7 @@ int dev_tile2csr(Context &cx, const tsg_dev_tiles &C, tsg_dev_csr &out, hipStrea
     if (C.tilem > 0 && C.nnz > 0) {
         if (C.tile_m == 16) t2c_launch_fill<16>(C, out, g, s);
         else if (C.tile_m == 32) t2c_launch_fill<32>(C, out, g, s);
+        else if (C.tile_m == 48) t2c_launch_fill<48>(C, out, g, s);
         else t2c_launch_fill<64>(C, out, g, s);
     }
     TSG_HIP(hipGetLastError());

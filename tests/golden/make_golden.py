@@ -27,6 +27,9 @@ OUT = os.path.join(HERE, "ref")
 REF_UNITTEST = "/root/reference/UnitTest/CSR2TILE"
 DRIVER = os.path.join(REPO, "oracle", "_ref", "ref_driver")
 TILES = [(16, 16), (32, 16), (32, 32)]
+# the remaining reference tile sides (16 | t <= 64), on a subset of fixtures
+TILES_EXTRA = [(48, 16), (16, 48), (48, 48), (64, 64), (64, 16)]
+EXTRA_FIXTURES = ("x_powerlaw_400", "x_banded_500", "x_rect_50x130", "x_dense_48", "random_0.1_36x36")
 
 _DT = {"i": np.int32, "h": np.uint16, "d": np.float64, "q": np.int64}
 
@@ -81,7 +84,7 @@ def main():
                 continue  # src/main.cu:102-106
             if aat == 1 and m == n and sym:
                 continue  # src/main.cu:120-124
-            for tm, tn in TILES:
+            for tm, tn in TILES + (TILES_EXTRA if name in EXTRA_FIXTURES else []):
                 tmp = os.path.join(OUT, "_tmp.bin")
                 subprocess.check_call([DRIVER, mtx, str(aat), str(tm), str(tn), tmp],
                                       stdout=subprocess.DEVNULL)

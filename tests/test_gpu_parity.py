@@ -21,7 +21,7 @@ RTOL = 1e-10
 TILE_KEYS = ("tile_ptr", "tile_columnidx", "tile_nnz", "tile_csr_Ptr", "tile_csr_Col", "tile_csr_Value", "mask")
 # C's masks are device-internal in the reference too (never copied back, src/tilespgemm-cuda.h:2749-2775)
 C_KEYS = TILE_KEYS[:-1]
-SUPPORTED = {(16, 16), (32, 16), (32, 32)}  # every tile size the goldens hold
+SUPPORTED = {(16, 16), (32, 16), (32, 32), (48, 16), (16, 48), (48, 48), (64, 64), (64, 16)}  # all golden sizes
 
 
 def g(npz, key):
@@ -242,3 +242,33 @@ def test_step2_modes_match_oracle(mode, case, monkeypatch):
     ref = O.gustavson(oA, oB)
     assert_csr_equal(Cm.csr(), ref.csr())
     assert st["nnzC"] == ref.s.nnz
+
+
+@pytest.mark.parametrize("tm,tn", [(48, 16), (16, 48), (48, 48), (64, 64), (64, 16), (32, 64)])
+@pytest.mark.parametrize("aat", [0, 1])
+def test_other_tile_sizes_vs_oracle(tm, tn, aat):
+    """Every reference tile size (sides 16..64): csr2tile of A and B, the host
+    tilespgemm's C tiles and tile2csr, field by field against the oracle."""
+    mm, nn, rp, ci, vv = synth.random_csr(700, 700 if not aat else 420, density=0.01, seed=tm * 7 + tn + aat)
+    A = T.Matrix.from_csr(mm, nn, rp, ci, vv)
+    oA = O.OMat.from_csr(mm, nn, rp, ci, vv)
+    if aat:
+        B, oB = T.transpose(A), O.transpose(oA)
+    else:
+        B, oB = T.Matrix.alias(A), O.OMat.alias(oA)
+    T.csr2tile_row_major(A, tm, tn)
+    T.csr2tile_col_major(B, tm, tn)
+    O.csr2tile_row_major(oA, tm, tn)
+    O.csr2tile_col_major(oB, tm, tn)
+    at, oat = A.tiles(tm, tn // 16), oA.tiles(tm, tn // 16)
+    bt, obt = B.tiles(tn, tm // 16, csc=True), oB.tiles(tn, tm // 16, csc=True)
+    for k in TILE_KEYS:
+        np.testing.assert_array_equal(at[k], oat[k], err_msg="A " + k)
+        np.testing.assert_array_equal(bt[k], obt[k], err_msg="B " + k)
+    Cm, _ = T.tilespgemm(A, B, tm, tn)
+    oC = O.tilespgemm(oA, oB, tm, tn)
+    ct, oct_ = Cm.tiles(tm, tm // 16), O.c_tiles(oC, tm)
+    for k in C_KEYS:
+        np.testing.assert_array_equal(ct[k], oct_[k], err_msg="C " + k)
+    T.tile2csr(Cm, tm, tm)
+    assert_csr_equal(Cm.csr(), O.gustavson(oA, oB).csr())

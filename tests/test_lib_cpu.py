@@ -52,14 +52,6 @@ def test_fails_loudly_without_device(L):
         T.spgemm(A, T.Matrix.alias(A))
 
 
-def test_unbuilt_tile_side_is_unsupported(L):
-    # 48 is a valid reference tile side (16 | 48 <= 64) but not built here
-    A = T.Matrix.from_csr(2, 2, [0, 1, 2], [0, 1], [1.0, 2.0])
-    with pytest.raises(_lib.TsgError) as ei:
-        T.csr2tile_row_major(A, 48, 16)
-    assert ei.value.rc == -6
-
-
 def test_invalid_tile_size_rejected(L):
     A = T.Matrix.from_csr(2, 2, [0, 1, 2], [0, 1], [1.0, 2.0])
     for tm, tn in [(8, 16), (16, 24), (0, 16), (128, 16)]:
