@@ -4,12 +4,16 @@
 // host functions only move data and orchestrate.
 #include <hip/hip_runtime.h>
 
+#include <sys/stat.h>
+
+#include <algorithm>
 #include <cctype>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "tsg_internal.h"
@@ -273,9 +277,71 @@ const char *tsg_status_string(int st) {
 
 // ---- Matrix-Market reader: same CSR order as mmio_allinone
 // (src/mmio_highlevel.h:593-759).  Whole-file read + hand-rolled tokenizer.
+// Optional binary CSR cache (TSG_CSR_CACHE_DIR): <dir>/<name>.<bytes>.<mtime>.tsgcsr
+// holds {m, n, nnz, isSymmetric} + rowpointer + columnindex + value in the exact
+// mmio_allinone order, so a large .mtx (LiveJournal, mawi) is parsed once.
+static std::string csr_cache_path(const char *filename) {
+    const char *dir = getenv("TSG_CSR_CACHE_DIR");
+    struct stat st;
+    if (!dir || !*dir || stat(filename, &st) != 0) return std::string();
+    const char *base = strrchr(filename, '/');
+    base = base ? base + 1 : filename;
+    char tag[64];
+    snprintf(tag, sizeof(tag), ".%lld.%lld.tsgcsr", (long long)st.st_size, (long long)st.st_mtime);
+    return std::string(dir) + "/" + base + tag;
+}
+
+static bool csr_cache_read(const std::string &path, tsg_smatrix *A) {
+    FILE *f = path.empty() ? nullptr : fopen(path.c_str(), "rb");
+    if (!f) return false;
+    int hdr[4];
+    bool ok = fread(hdr, sizeof(int), 4, f) == 4 && hdr[0] >= 0 && hdr[1] >= 0 && hdr[2] >= 0;
+    if (ok) {
+        A->m = hdr[0]; A->n = hdr[1]; A->nnz = hdr[2]; A->isSymmetric = hdr[3];
+        A->rowpointer = (int *)malloc(((size_t)A->m + 1) * sizeof(int));
+        A->columnindex = (int *)malloc((size_t)(A->nnz ? A->nnz : 1) * sizeof(int));
+        A->value = (double *)malloc((size_t)(A->nnz ? A->nnz : 1) * sizeof(double));
+        ok = A->rowpointer && A->columnindex && A->value &&
+             fread(A->rowpointer, sizeof(int), (size_t)A->m + 1, f) == (size_t)A->m + 1 &&
+             fread(A->columnindex, sizeof(int), (size_t)A->nnz, f) == (size_t)A->nnz &&
+             fread(A->value, sizeof(double), (size_t)A->nnz, f) == (size_t)A->nnz;
+        if (!ok) {
+            free(A->rowpointer); free(A->columnindex); free(A->value);
+            memset(A, 0, sizeof(*A));
+        }
+    }
+    fclose(f);
+    return ok;
+}
+
+static void csr_cache_write(const std::string &path, const tsg_smatrix *A) {
+    if (path.empty()) return;
+    const std::string tmp = path + ".part";
+    FILE *f = fopen(tmp.c_str(), "wb");
+    if (!f) return;
+    const int hdr[4] = {A->m, A->n, A->nnz, A->isSymmetric};
+    bool ok = fwrite(hdr, sizeof(int), 4, f) == 4 &&
+              fwrite(A->rowpointer, sizeof(int), (size_t)A->m + 1, f) == (size_t)A->m + 1 &&
+              fwrite(A->columnindex, sizeof(int), (size_t)A->nnz, f) == (size_t)A->nnz &&
+              fwrite(A->value, sizeof(double), (size_t)A->nnz, f) == (size_t)A->nnz;
+    ok = (fclose(f) == 0) && ok;
+    if (ok) rename(tmp.c_str(), path.c_str());
+    else remove(tmp.c_str());
+}
+
+static int mmio_parse(const char *filename, tsg_smatrix *A);
+
 int tsg_mmio_allinone(const char *filename, tsg_smatrix *A) {
     if (!filename || !A) return TSG_ERR_INVALID;
     memset(A, 0, sizeof(*A));
+    const std::string cache = csr_cache_path(filename);
+    if (csr_cache_read(cache, A)) return TSG_OK;
+    const int rc = mmio_parse(filename, A);
+    if (rc == TSG_OK) csr_cache_write(cache, A);
+    return rc;
+}
+
+static int mmio_parse(const char *filename, tsg_smatrix *A) {
     FILE *f = fopen(filename, "rb");
     if (!f) return TSG_ERR_IO;
     fseek(f, 0, SEEK_END);
@@ -312,29 +378,71 @@ int tsg_mmio_allinone(const char *filename, tsg_smatrix *A) {
     long n = strtol(p, &q, 10); p = q;
     long nz = strtol(p, &q, 10); p = q;
     if (m < 0 || n < 0 || nz < 0 || m > 0x7fffffff || n > 0x7fffffff) return TSG_ERR_IO;
+    // Entry lines are parsed in parallel chunks cut at line starts (file order is
+    // kept: chunk c's entries follow chunk c-1's), then counted and placed serially.
     std::vector<int> ri((size_t)nz), ci((size_t)nz);
     std::vector<double> vv((size_t)nz);
     std::vector<long long> cnt((size_t)m + 1, 0);
-    for (long k = 0; k < nz; ++k) {
-        long i = strtol(p, &q, 10);
-        if (q == p) return TSG_ERR_IO;
-        p = q;
-        long j = strtol(p, &q, 10);
-        if (q == p) return TSG_ERR_IO;
-        p = q;
-        double x = 1.0;
-        if (is_real || is_cplx) {
-            x = strtod(p, &q); p = q;
-            if (is_cplx) { (void)strtod(p, &q); p = q; }
-        } else if (is_int) {
-            x = (double)strtol(p, &q, 10); p = q;
-        }
-        if (i < 1 || j < 1 || i > m || j > n) return TSG_ERR_IO;
-        ri[k] = (int)(i - 1);
-        ci[k] = (int)(j - 1);
-        vv[k] = x;
-        cnt[i - 1]++;
+    const size_t body = (size_t)(end - p);
+    int nth = (int)std::min<size_t>(std::max(1u, std::thread::hardware_concurrency()), 16);
+    nth = (int)std::max<size_t>(1, std::min<size_t>((size_t)nth, body / (1u << 22)));  // >= 4 MiB per chunk
+    std::vector<char *> cut(nth + 1);
+    cut[0] = p;
+    cut[nth] = end;
+    for (int c = 1; c < nth; ++c) {
+        char *x = p + body * c / nth;
+        if (x < cut[c - 1]) x = cut[c - 1];
+        char *nl = (char *)memchr(x, '\n', end - x);
+        cut[c] = nl ? nl + 1 : end;
     }
+    struct Part {
+        std::vector<int> i, j;
+        std::vector<double> x;
+        bool bad = false;
+    };
+    std::vector<Part> parts(nth);
+    auto parse = [&](int c) {
+        Part &P = parts[c];
+        char *a = cut[c], *e = cut[c + 1], *z;
+        while (true) {
+            while (a < e && isspace((unsigned char)*a)) ++a;
+            if (a >= e) break;
+            long i = strtol(a, &z, 10);
+            if (z == a) { P.bad = true; return; }
+            a = z;
+            long j = strtol(a, &z, 10);
+            if (z == a) { P.bad = true; return; }
+            a = z;
+            double x = 1.0;
+            if (is_real || is_cplx) {
+                x = strtod(a, &z); a = z;
+                if (is_cplx) { (void)strtod(a, &z); a = z; }
+            } else if (is_int) {
+                x = (double)strtol(a, &z, 10); a = z;
+            }
+            if (i < 1 || j < 1 || i > m || j > n) { P.bad = true; return; }
+            P.i.push_back((int)(i - 1));
+            P.j.push_back((int)(j - 1));
+            P.x.push_back(x);
+        }
+    };
+    {
+        std::vector<std::thread> th;
+        for (int c = 1; c < nth; ++c) th.emplace_back(parse, c);
+        parse(0);
+        for (auto &t : th) t.join();
+    }
+    long k = 0;
+    for (int c = 0; c < nth; ++c) {
+        const Part &P = parts[c];
+        if (P.bad || k + (long)P.i.size() > nz) return TSG_ERR_IO;
+        std::copy(P.i.begin(), P.i.end(), ri.begin() + k);
+        std::copy(P.j.begin(), P.j.end(), ci.begin() + k);
+        std::copy(P.x.begin(), P.x.end(), vv.begin() + k);
+        k += (long)P.i.size();
+    }
+    if (k != nz) return TSG_ERR_IO;
+    for (long e = 0; e < nz; ++e) cnt[ri[e]]++;
     if (sym)
         for (long k = 0; k < nz; ++k)
             if (ri[k] != ci[k]) cnt[ci[k]]++;

@@ -75,6 +75,51 @@ def test_mmio_reader_matches_oracle(L, path):
     np.testing.assert_array_equal(vv, ovv)
 
 
+@pytest.mark.parametrize("kind", ["real general", "pattern symmetric", "integer general"])
+def test_mmio_reader_parallel_chunks_match_oracle(L, tmp_path, kind):
+    """A file large enough for the multi-threaded parse (>= 4 MiB per chunk):
+    same CSR order and values as the oracle's mmio_allinone restatement."""
+    rng = np.random.default_rng(5)
+    m = 60000
+    nz = 900000
+    i = rng.integers(1, m + 1, nz)
+    j = rng.integers(1, m + 1, nz)
+    if "symmetric" in kind:
+        i, j = np.maximum(i, j), np.minimum(i, j)
+    path = tmp_path / "big.mtx"
+    with open(path, "w") as f:
+        f.write(f"%%MatrixMarket matrix coordinate {kind}\n% generated\n{m} {m} {nz}\n")
+        if kind.startswith("pattern"):
+            np.savetxt(f, np.stack([i, j], 1), fmt="%d")
+        elif kind.startswith("integer"):
+            np.savetxt(f, np.stack([i, j, rng.integers(-9, 10, nz)], 1), fmt="%d")
+        else:
+            np.savetxt(f, np.stack([i, j, rng.standard_normal(nz)], 1), fmt="%d %d %.17g")
+    assert os.path.getsize(path) > (8 << 20)
+    A = T.mmio_allinone(str(path))
+    ref = O.OMat.load(str(path), pos_mod10=False)  # file values, not k % 10
+    m1, n1, rp, ci, vv = A.csr()
+    m2, n2, orp, oci, ovv = ref.csr()
+    assert (m1, n1) == (m2, n2)
+    np.testing.assert_array_equal(rp, orp)
+    np.testing.assert_array_equal(ci, oci)
+    np.testing.assert_array_equal(vv, ovv)
+
+
+def test_mmio_csr_cache_roundtrip(L, tmp_path, monkeypatch):
+    path = os.path.join(FIXTURES, "x_powerlaw_400.mtx")
+    monkeypatch.setenv("TSG_CSR_CACHE_DIR", str(tmp_path))
+    first = T.mmio_allinone(path).csr()
+    files = list(tmp_path.glob("x_powerlaw_400.mtx.*.tsgcsr"))
+    assert len(files) == 1
+    second = T.mmio_allinone(path).csr()  # served from the cache
+    for a, b in zip(first, second):
+        np.testing.assert_array_equal(a, b)
+    monkeypatch.delenv("TSG_CSR_CACHE_DIR")
+    for a, b in zip(first, T.mmio_allinone(path).csr()):
+        np.testing.assert_array_equal(a, b)
+
+
 def test_mmio_reader_errors(L, tmp_path):
     bad = tmp_path / "bad.mtx"
     bad.write_text("%%MatrixMarket matrix array real general\n2 2\n1\n2\n3\n4\n")
