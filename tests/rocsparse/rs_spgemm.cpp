@@ -32,6 +32,9 @@ template <class T> static int up(T **d, const T *h, size_t n) {
     return 0;
 }
 
+static double g_last_ms = 0.0;  // device time of the last call's three stages (diagnostics)
+extern "C" double rs_last_ms() { return g_last_ms; }
+
 extern "C" int rs_spgemm(int m, int k, int n, int nnzA, const int *rpA, const int *ciA, const double *vA, int nnzB,
                          const int *rpB, const int *ciB, const double *vB, long long *nnzC_out, int **rpC,
                          int **ciC, double **vC) {
@@ -59,6 +62,10 @@ extern "C" int rs_spgemm(int m, int k, int n, int nnzA, const int *rpA, const in
     const rocsparse_operation nt = rocsparse_operation_none;
     size_t bsz = 0;
     void *buf = nullptr;
+    hipEvent_t e0, e1;
+    CK_HIP(hipEventCreate(&e0));
+    CK_HIP(hipEventCreate(&e1));
+    CK_HIP(hipEventRecord(e0, 0));
     CK_RS(rocsparse_spgemm(h, nt, nt, &alpha, A, B, &beta, D, C, f64, rocsparse_spgemm_alg_default,
                            rocsparse_spgemm_stage_buffer_size, &bsz, nullptr));
     CK_HIP(hipMalloc(&buf, bsz ? bsz : 1));
@@ -71,7 +78,13 @@ extern "C" int rs_spgemm(int m, int k, int n, int nnzA, const int *rpA, const in
     CK_RS(rocsparse_csr_set_pointers(C, dC_rp, dC_ci, dC_v));
     CK_RS(rocsparse_spgemm(h, nt, nt, &alpha, A, B, &beta, D, C, f64, rocsparse_spgemm_alg_default,
                            rocsparse_spgemm_stage_compute, &bsz, buf));
+    CK_HIP(hipEventRecord(e1, 0));
     CK_HIP(hipDeviceSynchronize());
+    float ms = 0.f;
+    CK_HIP(hipEventElapsedTime(&ms, e0, e1));
+    g_last_ms = ms;  // includes rocSPARSE's buffer/C allocations, as the stages need them
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
     *nnzC_out = nnzC;
     *rpC = (int *)malloc(((size_t)m + 1) * sizeof(int));
     *ciC = (int *)malloc((nnzC ? nnzC : 1) * sizeof(int));
