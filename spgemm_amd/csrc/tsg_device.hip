@@ -87,6 +87,28 @@ template <class T> __device__ __forceinline__ T block_excl_scan(T x, T *total, T
     return off + inc - x;
 }
 
+// workgroup min and max of x (red: 2*WAVES ints)
+__device__ __forceinline__ void block_minmax(int &mn, int &mx, int *red) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+        mn = min(mn, __shfl_xor(mn, d, 64));
+        mx = max(mx, __shfl_xor(mx, d, 64));
+    }
+    if (lane_id() == 0) {
+        red[wave_id()] = mn;
+        red[WAVES + wave_id()] = mx;
+    }
+    __syncthreads();
+    mn = red[0];
+    mx = red[WAVES];
+#pragma unroll
+    for (int w = 1; w < WAVES; ++w) {
+        mn = min(mn, red[w]);
+        mx = max(mx, red[WAVES + w]);
+    }
+    __syncthreads();
+}
+
 template <class T> __device__ __forceinline__ T block_sum(T x, T *red) {
     x = wave_sum(x);
     if (lane_id() == 0) red[wave_id()] = x;
@@ -909,6 +931,43 @@ __device__ __forceinline__ void bm_words(const u32 *bm, int wpt, u32 *w) {
     }
 }
 
+// Count (PASS 0) or emit (PASS 1) the set bits of bitmask words [wlo, whi]
+// (bit b of word w = column clo + 32*w + b).  The full window goes through the
+// vector reads; a narrower span (banded / local tile rows) touches only its
+// own words, so clearing and scanning cost O(span), not O(window).
+template <int PASS>
+__device__ __forceinline__ void bm_count_emit(const u32 *bm, int words, int wpt, int wlo, int whi, int clo,
+                                              int *red, int *unit_cnt, int u, int off0, int *out) {
+    u32 wv[8];
+    int base, nw;
+    if (wlo == 0 && whi == words - 1) {
+        bm_words(bm, wpt, wv);
+        base = threadIdx.x * wpt;
+        nw = wpt;
+    } else {
+        const int span = whi - wlo + 1, per = (span + WG - 1) / WG;
+        base = wlo + threadIdx.x * per;
+        nw = max(0, min(per, whi + 1 - base));
+        for (int q = 0; q < 8; ++q) wv[q] = q < nw ? bm[base + q] : 0u;  // per <= 8 (span <= 2048)
+    }
+    int cnt = 0;
+    for (int q = 0; q < nw; ++q) cnt += __popc(wv[q]);
+    if (PASS == 0) {
+        const int tot = block_sum(cnt, red);
+        if (threadIdx.x == 0) unit_cnt[u] = tot;
+    } else {
+        int tot;
+        int off = block_excl_scan(cnt, &tot, red) + off0;
+        for (int q = 0; q < nw; ++q) {
+            u32 x = wv[q];
+            while (x) {
+                out[off++] = clo + (base + q) * 32 + __ffs(x) - 1;
+                x &= x - 1;
+            }
+        }
+    }
+}
+
 template <int PASS>
 __global__ __launch_bounds__(WG) void k_step1(const int *Aptr, const int *Acol, const int *Bptr, const int *Bcol,
                                               int tilemA, int tilenB, int nwin, int win, int *unit_cnt,
@@ -928,7 +987,10 @@ __global__ __launch_bounds__(WG) void k_step1(const int *Aptr, const int *Acol, 
             continue;
         }
         const int clo = w * win, chi = min(clo + win, tilenB) - 1;
-        for (int q = threadIdx.x; q < words; q += WG) bm[q] = 0u;
+        // the whole window (a span bound from the B tile rows' first/last columns
+        // costs webbase more than it saves banded matrices)
+        const int wlo = 0, whi = words - 1;
+        for (int q = wlo + threadIdx.x; q <= whi; q += WG) bm[q] = 0u;
         __syncthreads();
         long it = for_each_product(a0, a1, Acol, Bptr, Bcol, clo, chi, nwin > 1, L, [&](int a, int b) {
             (void)a;
@@ -936,26 +998,7 @@ __global__ __launch_bounds__(WG) void k_step1(const int *Aptr, const int *Acol, 
             atomicOr(&bm[c >> 5], 1u << (c & 31));
         });
         if (PASS == 0) my_items += (threadIdx.x == 0) ? it : 0;
-        u32 wv[8];
-        bm_words(bm, wpt, wv);
-        int cnt = 0;
-        for (int q = 0; q < wpt; ++q) cnt += __popc(wv[q]);
-        if (PASS == 0) {
-            int tot = block_sum(cnt, red);
-            if (threadIdx.x == 0) unit_cnt[u] = tot;
-        } else {
-            int tot;
-            int off = block_excl_scan(cnt, &tot, red) + unit_off[u];
-            for (int q = 0; q < wpt; ++q) {
-                const int wi = threadIdx.x * wpt + q;
-                u32 x = wv[q];
-                while (x) {
-                    int b = __ffs(x) - 1;
-                    Ccol[off++] = clo + wi * 32 + b;
-                    x &= x - 1;
-                }
-            }
-        }
+        bm_count_emit<PASS>(bm, words, wpt, wlo, whi, clo, red, unit_cnt, u, PASS == 1 ? unit_off[u] : 0, Ccol);
         __syncthreads();
     }
     if (PASS == 0 && threadIdx.x == 0 && my_items) atomicAdd(prod_total, (u64)my_items);
@@ -975,6 +1018,7 @@ __global__ __launch_bounds__(WG) void k_tstruct(const int *rowptr, const int *co
                                                 int *tcol) {
     __shared__ __align__(16) u32 bm[S1_MAXWORDS];
     __shared__ int red[WAVES];
+    __shared__ int red2[2 * WAVES];
     const int nunits = tilem * nwin;
     const int words = win >> 5;
     const int wpt = words / WG;
@@ -986,32 +1030,29 @@ __global__ __launch_bounds__(WG) void k_tstruct(const int *rowptr, const int *co
             continue;
         }
         const int clo = w * win;
-        for (int x = threadIdx.x; x < words; x += WG) bm[x] = 0u;
+        int mn = 0x7fffffff, mx = -1;  // span of this window's tile columns
+        for (int p = p0 + threadIdx.x; p < p1; p += WG) {
+            const int c = col[p] / tc - clo;
+            if ((unsigned)c < (unsigned)win) {
+                mn = min(mn, c);
+                mx = max(mx, c);
+            }
+        }
+        block_minmax(mn, mx, red2);
+        if (mx < mn) {
+            if (PASS == 0 && threadIdx.x == 0) unit_cnt[u] = 0;
+            continue;
+        }
+        int wlo = mn >> 5, whi = mx >> 5;
+        if ((whi - wlo + 1) * 2 > words) wlo = 0, whi = words - 1;  // wide span: whole window, vector reads
+        for (int x = wlo + threadIdx.x; x <= whi; x += WG) bm[x] = 0u;
         __syncthreads();
         for (int p = p0 + threadIdx.x; p < p1; p += WG) {
             const int c = col[p] / tc - clo;
             if ((unsigned)c < (unsigned)win) atomicOr(&bm[c >> 5], 1u << (c & 31));
         }
         __syncthreads();
-        u32 wv[8];
-        bm_words(bm, wpt, wv);
-        int cnt = 0;
-        for (int x = 0; x < wpt; ++x) cnt += __popc(wv[x]);
-        if (PASS == 0) {
-            const int tot = block_sum(cnt, red);
-            if (threadIdx.x == 0) unit_cnt[u] = tot;
-        } else {
-            int tot;
-            int off = block_excl_scan(cnt, &tot, red) + unit_off[u];
-            for (int x = 0; x < wpt; ++x) {
-                const int wi = threadIdx.x * wpt + x;
-                u32 v = wv[x];
-                while (v) {
-                    tcol[off++] = clo + wi * 32 + __ffs(v) - 1;
-                    v &= v - 1;
-                }
-            }
-        }
+        bm_count_emit<PASS>(bm, words, wpt, wlo, whi, clo, red, unit_cnt, u, PASS == 1 ? unit_off[u] : 0, tcol);
         __syncthreads();
     }
 }
