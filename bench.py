@@ -43,6 +43,10 @@ def load_matrix(args):
         T.values_pos_mod10(A)
         m, n, rp, ci, vv = A.csr()
         return m, n, rp, ci, vv, os.path.basename(args.mtx), "real"
+    if args.matrix == "mawi":
+        m, n, rp, ci, vv = synth.mawi(scale=args.scale)
+        tag = "mawi-synthetic" + (f"x{args.scale:g}" if args.scale != 1.0 else "")
+        return m, n, rp, ci, vv, tag, "synthetic"
     m, n, rp, ci, vv = synth.GENERATORS[args.matrix]()
     return m, n, rp, ci, vv, args.matrix + "-synthetic", "synthetic"
 
@@ -127,7 +131,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--matrix", default="webbase", choices=["webbase", "cant", "mc2depi", "lj"])
+    ap.add_argument("--matrix", default="webbase", choices=["webbase", "cant", "mc2depi", "lj", "mawi"])
+    ap.add_argument("--scale", type=float, default=1.0, help="size factor for the mawi stand-in")
     ap.add_argument("--mtx", default=os.environ.get("TSG_MTX"))
     ap.add_argument("--aat", type=int, default=None)
     ap.add_argument("--tile", type=int, default=16)

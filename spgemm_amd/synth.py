@@ -16,6 +16,9 @@ mmio_allinone produces for SuiteSparse files, which are stored column-major
   cant      n = 62,451, symmetric banded FEM-like, ~64 nnz/row
   mc2depi   n = 525,825, unsymmetric 4-point stencil on a 725 x 725 grid + tail
   lj        n = 3,997,962, R-MAT (a=.57, b=c=.19), avg 17.3, symmetrised
+  mawi      n = 226,196,185 (x scale), symmetric star + noise: one hub adjacent
+            to 10^7 (x scale) random nodes, plus uniform random edges for an
+            average degree of ~2 (nnz ~472 M at scale 1; the real matrix has 480 M)
 """
 import numpy as np
 
@@ -154,4 +157,23 @@ def random_csr(m, n, density=None, nnz_per_row=None, seed=SEED, unsorted=False, 
     return m, n, rowptr, col, val
 
 
-GENERATORS = {"webbase": webbase, "cant": cant, "mc2depi": mc2depi, "lj": rmat}
+def mawi(scale=1.0, seed=SEED, hub_deg=10_000_000, noise_deg=2.0):
+    """Packet-trace graph stand-in: its A^2 is dominated by the hub (every hub
+    neighbour's row of C receives the hub's whole row), so the full product is
+    far beyond int32 nnz(C) -- bench.py runs the largest feasible row prefix."""
+    rng = np.random.default_rng(seed)
+    n = max(16, int(226_196_185 * scale))
+    hd = max(1, int(hub_deg * scale))
+    hub = int(rng.integers(n // 2, n))  # late, so row prefixes before it stay feasible
+    nb = rng.choice(n, size=hd, replace=False)
+    nb = nb[nb != hub]
+    m_noise = int(n * noise_deg / 2)
+    u = rng.integers(0, n, m_noise)
+    v = rng.integers(0, n, m_noise)
+    rows = np.concatenate([np.full(len(nb), hub, np.int64), nb, u, v])
+    cols = np.concatenate([nb, np.full(len(nb), hub, np.int64), v, u])
+    rowptr, col, val = _finish(n, n, rows, cols)
+    return n, n, rowptr, col, val
+
+
+GENERATORS = {"webbase": webbase, "cant": cant, "mc2depi": mc2depi, "lj": rmat, "mawi": mawi}

@@ -155,6 +155,18 @@ def test_aat_rectangular_and_empty():
     assert (m, n) == (40, 40) and rp.sum() == 0 and len(ci) == 0 and st["nnzC"] == 0
 
 
+def test_mawi_star_small_scale_vs_oracle():
+    """mawi stand-in at 3e-4 scale (68 K nodes, hub degree 3,000): the hub's
+    neighbours each receive the hub's whole row in C."""
+    m, n, rp, ci, vv = synth.mawi(scale=3e-4)
+    A = T.Matrix.from_csr(m, n, rp, ci, vv)
+    oA = O.OMat.from_csr(m, n, rp, ci, vv)
+    Cm, st = T.spgemm(A, T.Matrix.alias(A))
+    ref = O.gustavson(oA, O.OMat.alias(oA))
+    assert_csr_equal(Cm.csr(), ref.csr())
+    assert st["nnzC"] == ref.s.nnz
+
+
 @pytest.mark.parametrize("name", ["cant", "mc2depi", "webbase"])
 def test_full_size_synthetic_vs_oracle(name):
     """BASELINE configs at full size (synthetic stand-ins): pattern bit-exact,
