@@ -779,23 +779,25 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
                        A->n == B->n && tm == tn;
     bool s2elem = false, b_is_a = false;
     if (bsorted) {
+        // tile STRUCTURE of A and B from CSR; denser tiles add the row masks that
+        // step 2's tile-level ORs read (no sort-based csr2tile on this path)
         TSG_TRY(dev_tile_structure(cx, *A, tm, tn, tA, s));
         const char *md = getenv("TSG_STEP2_MODE");
         if (md && !strcmp(md, "elem")) s2elem = true;
         else if (md && !strcmp(md, "tile")) s2elem = false;
         else s2elem = (double)A->nnz < kStep2ElemMaxTileDensity * (double)tA.numtile;
-        if (s2elem) {
-            if (alias) {
-                tB = tA;
-                b_is_a = true;
-            } else {
-                TSG_TRY(dev_tile_structure(cx, *B, tn, tm, tB, s));
-            }
+        if (alias) {
+            tB = tA;
+            b_is_a = true;
         } else {
-            release_tiles(cx, tA);
+            TSG_TRY(dev_tile_structure(cx, *B, tn, tm, tB, s));
         }
-    }
-    if (!s2elem) {
+        if (!s2elem) {
+            TSG_TRY(dev_tile_masks(cx, *A, tA, &tA.mask, s));
+            if (b_is_a) tB.rm_mask = tA.mask;
+            else TSG_TRY(dev_tile_masks(cx, *B, tB, &tB.rm_mask, s));
+        }
+    } else {  // unsorted B rows: full csr2tile, tile-payload steps 2 and 3
         TSG_TRY(dev_csr2tile_row_major(cx, *A, tm, tn, tA, s));
         TSG_TRY(dev_csr2tile_col_major(cx, *B, tm, tn, tB, s));
     }

@@ -1064,6 +1064,37 @@ static void window_for(int tilen, int *win, int *nwin) {
     *nwin = (tilen + w - 1) / w;
 }
 
+// Row masks of a tiling straight from CSR (tile structure given): entry (R, c)
+// sets bit 15 - c%16 of word (R % tr) * (tc/16) + (c % tc)/16 of its tile, the
+// csr2tile mask layout (csr2tile.h:193-195).  mask must be zeroed.
+__global__ __launch_bounds__(WG) void k_tile_masks(const int *rowptr, const int *col, int m, int tr, int tc,
+                                                   const int *tile_ptr, const int *tcol, u16 *mask) {
+    const int mw = tc / 16;
+    u32 *m32 = reinterpret_cast<u32 *>(mask);
+    for (int R = blockIdx.x * WG + threadIdx.x; R < m; R += gridDim.x * WG) {
+        const int i = R / tr, r = R - i * tr;
+        const int t0 = tile_ptr[i], t1 = tile_ptr[i + 1];
+        for (int p = rowptr[R]; p < rowptr[R + 1]; ++p) {
+            const int c = col[p];
+            const int t = lower_bound_dev(tcol, t0, t1, c / tc);
+            const int lc = c % tc;
+            const long k = (long)t * tr * mw + r * mw + (lc >> 4);  // u16 index
+            atomicOr(&m32[k >> 1], (0x8000u >> (lc & 15)) << ((k & 1) * 16));
+        }
+    }
+}
+
+int dev_tile_masks(Context &cx, const tsg_dev_csr &M, tsg_dev_tiles &t, u16 **mask_out, hipStream_t s) {
+    const size_t words = ((size_t)t.numtile * t.tile_m * (t.tile_n / 16) + 2) & ~(size_t)1;
+    TSG_TRY(cx.get(mask_out, words));
+    TSG_HIP(hipMemsetAsync(*mask_out, 0, words * sizeof(u16), s));
+    if (M.m > 0)
+        k_tile_masks<<<grid_for(M.m, WG, 16384), WG, 0, s>>>(M.rowpointer, M.columnindex, M.m, t.tile_m, t.tile_n,
+                                                             t.tile_ptr, t.tile_columnidx, *mask_out);
+    TSG_HIP(hipGetLastError());
+    return TSG_OK;
+}
+
 int dev_tile_structure(Context &cx, const tsg_dev_csr &M, int tr, int tc, tsg_dev_tiles &out, hipStream_t s) {
     out = tsg_dev_tiles{};
     out.m = M.m; out.n = M.n; out.nnz = M.nnz;
@@ -1195,6 +1226,7 @@ struct ABView {
     const double *ValB;
     const int *split;     // per (unit, A tile): first B tile of the unit's column range
     const long long *sbase;  // per C tile row: offset of its units' split entries
+    const u16 *maskA;     // A tile masks (used when the A payload ColA/Annz is absent)
 };
 
 __global__ void k_units_per_row(const int *Cptr, int tilem, int *nunits) {
@@ -1365,8 +1397,29 @@ __device__ __forceinline__ void unit_items(const ABView &V, int ab, int na, int 
 
 template <int TM, int TN>
 __device__ __forceinline__ void or_product_masks(const ABView &V, int a, int b, u32 *tile) {
-    constexpr int MW = CM<TM>::MW;
+    constexpr int MW = CM<TM>::MW, AW = TN / 16;
     const u16 *mb = V.maskBrm + (size_t)b * TN * MW;
+    if (!V.ColA) {  // A given by its tile masks: every set bit (r, c) ORs B row c into C row r
+        const u16 *ma = V.maskA + (size_t)a * TM * AW;
+        for (int r = 0; r < TM; ++r)
+            for (int wa = 0; wa < AW; ++wa) {
+                u32 bits = ma[r * AW + wa];
+                while (bits) {
+                    const int hb = 31 - __clz(bits);
+                    const int c = wa * 16 + (15 - hb);
+                    bits &= ~(1u << hb);
+#pragma unroll
+                    for (int w = 0; w < MW; ++w) {
+                        const u32 mv = mb[c * MW + w];
+                        if (mv) {
+                            const int k = r * MW + w;
+                            atomicOr(&tile[k >> 1], mv << ((k & 1) * 16));
+                        }
+                    }
+                }
+            }
+        return;
+    }
     const int q1 = V.Annz[a + 1];
     for (int qa = V.Annz[a]; qa < q1; ++qa) {
         const int enc = V.ColA[qa];
@@ -1980,12 +2033,13 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     constexpr int TM = 16, TN = 16;
     if (A.tile_m != TM || A.tile_n != TN || B.tile_m != TN || B.tile_n != TM) return TSG_ERR_UNSUPPORTED;
     // element streaming needs the CSR operands (B rows column-sorted: caller's check)
-    const bool have_csr = Acsr && Bcsr && Acsr->m == A.m && Bcsr->m == B.m && Acsr->nnz > 0;
+    const bool have_csr = Acsr && Bcsr && Acsr->m == A.m && Bcsr->m == B.m;
     const bool s3elem = csr_out && have_csr && !(g_ablate & 16);
     const bool s2elem = step2_elem && have_csr;
     const bool tilepay = !(s2elem && s3elem);  // some step reads the tile payloads
     if (A.n != B.m) return TSG_ERR_INVALID;
-    if (tilepay && (!B.rm_mask || !B.rm_rowstart || !A.tile_csr_Col || !A.tile_nnz)) return TSG_ERR_INVALID;
+    if (!s2elem && (!B.rm_mask || !((A.tile_csr_Col && A.tile_nnz) || A.mask))) return TSG_ERR_INVALID;
+    if (!s3elem && (!B.rm_rowstart || !A.tile_csr_Col || !A.tile_nnz)) return TSG_ERR_INVALID;
     const int tilemA = A.tilem, tilenB = B.tilen;
     C = tsg_dev_tiles{};
     C.m = A.m; C.n = B.n; C.tile_m = TM; C.tile_n = TM;
@@ -2039,7 +2093,7 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     }
     const ABView V{A.tile_ptr, A.tile_columnidx, A.tile_nnz, A.tile_csr_Col, A.tile_csr_Value,
                    B.tile_ptr, B.tile_columnidx, B.rm_mask, B.rm_rowstart, B.tile_csr_Col, B.tile_csr_Value,
-                   split, sbase};
+                   split, sbase, A.mask};
     // element split points: every A entry's B CSR row cut at the unit boundaries (+ row end)
     ECsr E{};
     int *esplit = nullptr;
