@@ -1332,31 +1332,6 @@ __global__ void k_esplit_counts(const int *uoff, const int *rpA, int m, int tile
     if (blockIdx.x == 0 && threadIdx.x == 0) ebase[tilem] = 0;
 }
 
-template <int TM>
-__global__ __launch_bounds__(WG) void k_esplit(int m, const int *rpA, const int *ciA, const int *rpB, const int *ciB,
-                                               const int *uoff, const int *Cptr, const int *Ccol,
-                                               const long long *ebase, int *esplit) {
-    const int nnzA = rpA[m];
-    for (int p = blockIdx.x * WG + threadIdx.x; p < nnzA; p += gridDim.x * WG) {
-        int lo = 0, hi = m - 1;  // row of entry p (last R with rpA[R] <= p)
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (rpA[mid] <= p) lo = mid; else hi = mid - 1;
-        }
-        const int i = lo / TM;
-        const int e0 = rpA[i * TM], ei = rpA[min((i + 1) * TM, m)] - e0;
-        const int nu = uoff[i + 1] - uoff[i];
-        const int k = ciA[p];
-        int pos = rpB[k];
-        const int be = rpB[k + 1];
-        int *out = esplit + ebase[i] + (p - e0);
-        for (int q = 0; q < nu; ++q) {
-            if (q) pos = gallop_ge(ciB, pos, be, Ccol[Cptr[i] + q * CH] * TM);
-            out[(long)q * ei] = pos;
-        }
-        out[(long)nu * ei] = be;
-    }
-}
 
 // Products of A tiles [ab, ab+na) (row i, unit q of nu, A tiles from a0) that
 // fall in the unit's column range, from the precomputed split points:
@@ -1468,7 +1443,7 @@ __device__ __forceinline__ bool unit_masks(const ABView &V, int i, int q, int nu
 // Stream the element products of one unit straight from the CSR operands: for
 // every A entry p of C tile row i (row r of the tile row) and every B entry pb
 // of B row col(p) inside the unit's column range (split points precomputed by
-// k_esplit; narrowed to columns [clo, chi) when `narrow`), call f(r, slot, pb),
+// k_esplit_units; narrowed to columns [clo, chi) when `narrow`), call f(r, slot, pb),
 // slot = p's index in the current batch of WG A entries (s_va[slot] = A value
 // when s_va != nullptr).  Balanced over the workgroup by an LDS scan of the
 // segment lengths (consecutive products -> consecutive lanes: coalesced B reads).
@@ -1980,8 +1955,11 @@ __global__ __launch_bounds__(WG) void k_step3(const int4 *utab, const int4 *etab
     }
 }
 
-// TSG_ABLATE (diagnostics only: results are wrong when set) skips parts of
-// step 3 so that their cost can be measured: 1 masks, 4 values, 8 CSR writes.
+// TSG_ABLATE (diagnostics bitmask, read once per process):
+//    4  skip step 3's value pass        (results wrong)
+//    8  skip step 3's CSR writes        (results wrong)
+//   16  tile-payload value pass instead of element streaming (results correct)
+//   64  per-phase clock totals, with the -DTSG_PROF_BUILD library (make prof)
 static int g_ablate = -1;
 
 // Step 1 (C tile structure = tile-pattern product of A's and B's row-major tile
