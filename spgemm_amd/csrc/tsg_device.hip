@@ -1614,9 +1614,11 @@ __global__ __launch_bounds__(WG) void k_step2(const int4 *utab, const int4 *etab
             unit_masks<TM, TN>(V, i, q, nu, V.Aptr[i], V.Aptr[i + 1], s_cols, ns, s_mask, L, &tot);
         }
         PROF_MARK(9);
-        int rc[TM];
+        // row counts packed 4 x 16 bit (a unit's row count <= 256 * TM < 2^16)
+        constexpr int NP = TM / 4;
+        u64 pk[NP];
 #pragma unroll
-        for (int r = 0; r < TM; ++r) rc[r] = 0;
+        for (int g = 0; g < NP; ++g) pk[g] = 0;
         if (threadIdx.x < ns) {  // ns <= CH == WG
             static_assert((CM<TM>::TW32 % 4) == 0, "mask tile must be whole uint4");
             const int j = threadIdx.x;
@@ -1635,7 +1637,7 @@ __global__ __launch_bounds__(WG) void k_step2(const int4 *utab, const int4 *etab
                     const int k = r * MW + ww;
                     c += __popc((w[k >> 1] >> ((k & 1) * 16)) & 0xffffu);
                 }
-                rc[r] = c;
+                pk[r >> 2] += (u64)c << (16 * (r & 3));
                 nz += c;
             }
             nnzC[t0 + j] = nz;
@@ -1645,9 +1647,13 @@ __global__ __launch_bounds__(WG) void k_step2(const int4 *utab, const int4 *etab
             for (int k = 0; k < TW32 / 4; ++k) dst[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
         }
 #pragma unroll
-        for (int r = 0; r < TM; ++r) {
-            const int v = wave_sum(rc[r]);
-            if (lane_id() == 0 && v) atomicAdd(&s_rc[r], v);
+        for (int g = 0; g < NP; ++g) pk[g] = wave_sum(pk[g]);
+        if (lane_id() < TM) {  // lane r adds row r's count of this wave
+            u64 v = pk[0];
+#pragma unroll
+            for (int g = 1; g < NP; ++g) v = ((lane_id() >> 2) == g) ? pk[g] : v;
+            const int c = (int)((v >> (16 * (lane_id() & 3))) & 0xffffu);
+            if (c) atomicAdd(&s_rc[lane_id()], c);
         }
         __syncthreads();
         if (threadIdx.x < TM) unit_rc[(long)u * TM + threadIdx.x] = s_rc[threadIdx.x];
