@@ -1691,32 +1691,54 @@ __device__ __forceinline__ int kth_col16(u32 v, int k) {
 }
 
 
-template <int TM, int TN, bool WCSR, bool WTILE, bool ELEM>
-__global__ __launch_bounds__(WG) void k_step3(const int4 *utab, const int4 *etab, int nunits, int mrows, ABView V,
+// rank of column c among row r's set bits plus all bits of rows < r
+// (row-major in-tile position of (r, c); 16x16 tiles, MSB-first row words)
+__device__ __forceinline__ int tile_rank16(const u32 *tile, int r, int c) {
+    int rank = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const u32 v = tile[k];
+        if (2 * k + 1 < r) rank += __popc(v);
+        else if (2 * k < r) rank += __popc(v & 0xffffu);  // row 2k (low half) lies before r = 2k+1
+    }
+    const u32 row = (tile[r >> 1] >> ((r & 1) * 16)) & 0xffffu;
+    return rank + __popc(row >> (16 - c));  // bits of columns < c (column c = bit 15 - c)
+}
+
+// Step 3 with a TILE-MAJOR accumulator: a pass's nonzeros sit at
+// s_off[tile] - base + (row-major rank inside the tile), so the value pass needs
+// only the tile offsets (one block scan of tile nnz) and the tile mask.  The
+// CSR order across tiles is produced in the epilogue: every nonzero knows its
+// row r, and its rank among the pass's row-r nonzeros in tile order comes from
+// per-row ballots (16 per wave and 256 nonzeros) plus running per-row counters.
+// RST (denser tiles): a per-tile table of row-start ranks (u8) in LDS replaces
+// the eight popcounts of tile_rank16 on every product, at +4 KB of LDS.
+template <int TM, int TN, bool WCSR, bool WTILE, bool ELEM, bool RST = false>
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(6))) void k_step3(const int4 *utab, const int4 *etab, int nunits, int mrows, ABView V,
                                               ECsr E, const int *Ccol,
                                               const int *nnzoff, const u16 *maskC, const int *unit_rb,
                                               const int *rowptr, int *csr_col, double *csr_val, u16 *PtrC,
                                               u16 *ColC, double *ValC, int ablate) {
-    constexpr int MW = CM<TM>::MW, TW32 = CM<TM>::TW32, NV4 = TW32 / 4, NP = TM / 4;
+    static_assert(TM == 16, "tile-major step 3 is built for 16x16 C tiles");
+    constexpr int TW32 = CM<TM>::TW32, NV4 = TW32 / 4;
     static_assert(CH == WG, "one C tile per thread");
-    static_assert(TW32 % 4 == 0 && TM % 4 == 0, "mask tiles are whole uint4");
     __shared__ __align__(16) u32 s_mask[CH * TW32];
     __shared__ __align__(16) double acc[S3_NZCAP];
     __shared__ __align__(16) double s_va[WG];
-    constexpr int PS = CH + 2;            // s_pre row stride (u16): rows start on distinct banks
-    __shared__ u16 s_pre[PS * TM];        // [r][j]: row-r nonzeros of the unit's tiles [0, j)
     __shared__ int s_cols[CH];
-    __shared__ int s_off[CH + 1];         // [j]: nonzeros of the unit's tiles [0, j)
-    __shared__ int s_rp[TM + 1];          // A CSR row starts of the tile row (ELEM)
+    __shared__ int s_off[CH + 1];           // [j]: nonzeros of the unit's tiles [0, j)
+    __shared__ int s_rp[TM + 1];            // A CSR row starts of the tile row (ELEM)
     __shared__ unsigned char s_r[WG];
-    __shared__ int s_rowoff[TM + 1];      // per pass: CSR-order row offsets
-    __shared__ int s_rowbase[TM];         // per pass: rowoff[r] - pre[s_lo][r]
-    __shared__ int s_carry[TM];
+    __shared__ unsigned char s_key[S3_NZCAP];  // pass nonzero e: r << 4 | c
+    __shared__ u16 s_kt[S3_NZCAP];             // pass nonzero e: its tile
+    __shared__ unsigned char s_rs[RST ? CH * TM : 1];  // [tile][r]: in-tile rank of row r's first nonzero
+    __shared__ int s_wcnt[WAVES][TM];       // per-wave row counts of the current 256 nonzeros
+    __shared__ int s_run[TM];               // row-r nonzeros of this pass already placed
+    __shared__ int s_carry[TM];             // row-r nonzeros of this unit's earlier passes
     __shared__ int s_rowptr[TM];
-    __shared__ u64 s_red64[WAVES * NP];
     __shared__ int s_red[WAVES];
     __shared__ ProdLds L;
-    const int j = threadIdx.x;
+    const int j = threadIdx.x, lane = lane_id(), wv = wave_id();
 #ifdef TSG_PROF_BUILD
     u64 prof_t = (ablate & 64) ? __builtin_amdgcn_s_memtime() : 0;
 #endif
@@ -1760,58 +1782,28 @@ __global__ __launch_bounds__(WG) void k_step3(const int4 *utab, const int4 *etab
             reinterpret_cast<uint4 *>(s_mask + j * TW32)[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2],
                                                                          w[4 * k + 3]);
         s_cols[j] = col;
-        // ---- per-row counts (packed 4 x 16 bit) and tile totals, block-scanned over tiles
-        u64 pk[NP];
         int tt = 0;
+        if (RST) {
+            u32 rs4[TM / 4];
 #pragma unroll
-        for (int g = 0; g < NP; ++g) pk[g] = 0;
-#pragma unroll
-        for (int r = 0; r < TM; ++r) {
-            int c = 0;
-#pragma unroll
-            for (int ww = 0; ww < MW; ++ww) {
-                const int k = r * MW + ww;
-                c += __popc((w[k >> 1] >> ((k & 1) * 16)) & 0xffffu);
+            for (int r = 0; r < TM; ++r) {
+                if ((r & 3) == 0) rs4[r >> 2] = 0;
+                rs4[r >> 2] |= (u32)tt << (8 * (r & 3));
+                tt += __popc((w[r >> 1] >> ((r & 1) * 16)) & 0xffffu);
             }
-            pk[r >> 2] += (u64)c << (16 * (r & 3));
-            tt += c;
+#pragma unroll
+            for (int k = 0; k < TM / 16; ++k)
+                reinterpret_cast<uint4 *>(s_rs + j * TM)[k] = make_uint4(rs4[4 * k], rs4[4 * k + 1], rs4[4 * k + 2],
+                                                                         rs4[4 * k + 3]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < TW32; ++k) tt += __popc(w[k]);
         }
-        u64 ipk[NP];
-#pragma unroll
-        for (int g = 0; g < NP; ++g) ipk[g] = wave_incl_scan(pk[g]);
-        int itt = wave_incl_scan(tt);
-        if (lane_id() == 63) {
-#pragma unroll
-            for (int g = 0; g < NP; ++g) s_red64[wave_id() * NP + g] = ipk[g];
-            s_red[wave_id()] = itt;
-        }
-        __syncthreads();
-        PROF_MARK(0);
-        u64 tot64[NP];
-        int ttot = 0, toff = 0;
-#pragma unroll
-        for (int g = 0; g < NP; ++g) tot64[g] = 0;
-#pragma unroll
-        for (int wv = 0; wv < WAVES; ++wv) {
-            const bool before = wv < wave_id();
-#pragma unroll
-            for (int g = 0; g < NP; ++g) {
-                const u64 v = s_red64[wv * NP + g];
-                if (before) ipk[g] += v;
-                tot64[g] += v;
-            }
-            const int v = s_red[wv];
-            if (before) toff += v;
-            ttot += v;
-        }
-#pragma unroll
-        for (int r = 0; r < TM; ++r) {
-            const int g = r >> 2, sh = 16 * (r & 3);
-            s_pre[r * PS + j] = (u16)(((ipk[g] - pk[g]) >> sh) & 0xffffu);
-            if (j == WG - 1) s_pre[r * PS + CH] = (u16)((tot64[g] >> sh) & 0xffffu);
-        }
-        s_off[j] = toff + itt - tt;
+        int ttot;
+        const int toff = block_excl_scan(tt, &ttot, s_red);
+        s_off[j] = toff;
         if (j == WG - 1) s_off[CH] = ttot;
+        PROF_MARK(0);
         if (ttot == 0) {  // uniform: every tile of the unit is empty
             __syncthreads();
             continue;
@@ -1822,11 +1814,7 @@ __global__ __launch_bounds__(WG) void k_step3(const int4 *utab, const int4 *etab
 #pragma unroll
             for (int r = 0; r < TM; ++r) {
                 pp[r] = (u16)run;
-#pragma unroll
-                for (int ww = 0; ww < MW; ++ww) {
-                    const int k = r * MW + ww;
-                    run += __popc((w[k >> 1] >> ((k & 1) * 16)) & 0xffffu);
-                }
+                run += __popc((w[r >> 1] >> ((r & 1) * 16)) & 0xffffu);
             }
             uint4 *dst = reinterpret_cast<uint4 *>(PtrC + (size_t)(t0 + j) * TM);
 #pragma unroll
@@ -1845,24 +1833,28 @@ __global__ __launch_bounds__(WG) void k_step3(const int4 *utab, const int4 *etab
                 if (s_off[mid] - s_off[s_lo] <= S3_NZCAP) lo = mid; else hi = mid - 1;
             }
             const int s_hi = lo;
-            const int nz = s_off[s_hi] - s_off[s_lo];
+            const int base = s_off[s_lo];
+            const int nz = s_off[s_hi] - base;
             if (nz == 0) {  // uniform
                 s_lo = s_hi;
                 continue;
             }
-            int cnt_r = 0;
-            if (threadIdx.x < 64) {  // wave 0: per-row counts of the pass and their offsets
-                const int r = threadIdx.x;
-                const int p0 = r < TM ? (int)s_pre[r * PS + s_lo] : 0;
-                cnt_r = r < TM ? (int)s_pre[r * PS + s_hi] - p0 : 0;
-                const int inc = wave_incl_scan(cnt_r);
-                if (r < TM) {
-                    s_rowoff[r] = inc - cnt_r;
-                    s_rowbase[r] = inc - cnt_r - p0;
+            // expand the pass's nonzeros (tile-major, then row-major in the tile)
+            if (j >= s_lo && j < s_hi && tt > 0) {
+                int e = toff - base;
+#pragma unroll
+                for (int r = 0; r < TM; ++r) {
+                    u32 v = (w[r >> 1] >> ((r & 1) * 16)) & 0xffffu;
+                    while (v) {
+                        const int hb = 31 - __clz(v);  // MSB-first: lowest column first
+                        s_key[e] = (unsigned char)((r << 4) | (15 - hb));
+                        s_kt[e++] = (u16)j;
+                        v &= ~(1u << hb);
+                    }
                 }
-                if (r == TM - 1) s_rowoff[TM] = inc;
             }
             for (int e = threadIdx.x; e < nz; e += WG) acc[e] = 0.0;
+            if (threadIdx.x < TM) s_run[threadIdx.x] = 0;
             __syncthreads();
             PROF_MARK(2);
             // ---- V: values
@@ -1875,9 +1867,12 @@ __global__ __launch_bounds__(WG) void k_step3(const int4 *utab, const int4 *etab
                         const double vb = E.vB[pb];
                         const int sl = lower_bound_dev(s_cols, s_lo, s_hi, x / TM);
                         if (sl >= s_hi || s_cols[sl] != x / TM) return;  // another pass's tile
-                        atomicAdd(&acc[s_rowbase[r] + (int)s_pre[r * PS + sl] +
-                                       lds_rank<TM>(s_mask + sl * TW32, r, x % TM)],
-                                  s_va[slot] * vb);
+                        const int c = x % TM;
+                        const int rk = RST ? (int)s_rs[sl * TM + r] +
+                                                 __popc(((s_mask[sl * TW32 + (r >> 1)] >> ((r & 1) * 16)) & 0xffffu) >>
+                                                        (16 - c))
+                                           : tile_rank16(s_mask + sl * TW32, r, c);
+                        atomicAdd(&acc[s_off[sl] - base + rk], s_va[slot] * vb);
                     });
                 } else {
                     const int a0 = V.Aptr[i], a1 = V.Aptr[i + 1];
@@ -1888,6 +1883,7 @@ __global__ __launch_bounds__(WG) void k_step3(const int4 *utab, const int4 *etab
                             if (sl < s_lo || sl >= s_hi) return;
                             const int *br = V.rowsBrm + (size_t)b * (TN + 1);
                             const u32 *tile = s_mask + sl * TW32;
+                            const int tb = s_off[sl] - base;
                             const int q1 = V.Annz[a + 1];
                             for (int qa = V.Annz[a]; qa < q1; ++qa) {
                                 const int enc = V.ColA[qa];
@@ -1895,9 +1891,8 @@ __global__ __launch_bounds__(WG) void k_step3(const int4 *utab, const int4 *etab
                                 const int ks = br[c], ke = br[c + 1];
                                 if (ks >= ke) continue;
                                 const double va = V.ValA[qa];
-                                const int rb = s_rowbase[r] + (int)s_pre[r * PS + sl];
                                 for (int kb = ks; kb < ke; ++kb)
-                                    atomicAdd(&acc[rb + lds_rank<TM>(tile, r, V.ColB[kb])], va * V.ValB[kb]);
+                                    atomicAdd(&acc[tb + tile_rank16(tile, r, V.ColB[kb])], va * V.ValB[kb]);
                             }
                         });
                         __syncthreads();
@@ -1907,53 +1902,46 @@ __global__ __launch_bounds__(WG) void k_step3(const int4 *utab, const int4 *etab
             PROF_MARK(3);
             // ---- W: outputs of the pass
             if (WCSR && !(ablate & 8)) {
-                for (int e = threadIdx.x; e < nz; e += WG) {
-                    int r = 0;
+                for (int eb = 0; eb < nz; eb += WG) {
+                    const int e = eb + threadIdx.x;
+                    const bool in = e < nz;
+                    const int key = in ? (int)s_key[e] : 0;
+                    const int r = key >> 4;
+                    int lrank = 0;
 #pragma unroll
-                    for (int rr = 1; rr < TM; ++rr) r += (s_rowoff[rr] <= e) ? 1 : 0;
-                    const int kk = e - s_rowbase[r];  // rank of e inside row r of the unit
-                    int lo4 = s_lo, hi4 = s_hi - 1;   // tile holding it: last with pre <= kk
-                    while (lo4 < hi4) {
-                        const int mid = (lo4 + hi4 + 1) >> 1;
-                        if ((int)s_pre[r * PS + mid] <= kk) lo4 = mid; else hi4 = mid - 1;
+                    for (int rr = 0; rr < TM; ++rr) {  // rank among this wave's row-rr nonzeros
+                        const u64 m = __ballot(in && r == rr);
+                        if (r == rr) lrank = __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));
+                        if (lane == 0) s_wcnt[wv][rr] = __popcll(m);
                     }
-                    int b = kk - (int)s_pre[r * PS + lo4];
-                    int cl = 0;
-#pragma unroll
-                    for (int ww = 0; ww < MW; ++ww) {
-                        const u32 v = lds_row_word<TM>(s_mask + lo4 * TW32, r, ww);
-                        const int pc = __popc(v);
-                        if (b >= 0 && b < pc) cl = ww * 16 + kth_col16(v, b);
-                        b -= pc;
+                    __syncthreads();
+                    if (in) {
+                        int before = s_run[r];
+                        for (int w2 = 0; w2 < wv; ++w2) before += s_wcnt[w2][r];
+                        const int dst = s_rowptr[r] + s_carry[r] + before + lrank;
+                        csr_col[dst] = s_cols[s_kt[e]] * TM + (key & 15);
+                        csr_val[dst] = acc[e];
                     }
-                    const int dst = s_rowptr[r] + s_carry[r] + (e - s_rowoff[r]);
-                    csr_col[dst] = s_cols[lo4] * TM + cl;
-                    csr_val[dst] = acc[e];
+                    __syncthreads();
+                    if (threadIdx.x < TM) {
+                        int add = 0;
+                        for (int w2 = 0; w2 < WAVES; ++w2) add += s_wcnt[w2][threadIdx.x];
+                        s_run[threadIdx.x] += add;
+                    }
+                    __syncthreads();  // s_wcnt is rewritten by the next 256 nonzeros
                 }
             }
             if (WTILE) {
-                for (int jt = s_lo + threadIdx.x; jt < s_hi; jt += WG) {
-                    if (s_off[jt + 1] == s_off[jt]) continue;
-                    const u32 *tile = s_mask + jt * TW32;
-                    int out = nzbase + s_off[jt];
-#pragma unroll
-                    for (int r = 0; r < TM; ++r) {
-                        int k = s_rowbase[r] + (int)s_pre[r * PS + jt];
-#pragma unroll
-                        for (int ww = 0; ww < MW; ++ww) {
-                            u32 v = lds_row_word<TM>(tile, r, ww);
-                            while (v) {
-                                const int hb = 31 - __clz(v);
-                                ColC[out] = (u16)(ww * 16 + (15 - hb));
-                                ValC[out++] = acc[k++];
-                                v &= ~(1u << hb);
-                            }
-                        }
+                if (j >= s_lo && j < s_hi && tt > 0) {
+                    const int e0 = toff - base, out = nzbase + toff;
+                    for (int k = 0; k < tt; ++k) {
+                        ColC[out + k] = (u16)(s_key[e0 + k] & 15);
+                        ValC[out + k] = acc[e0 + k];
                     }
                 }
             }
             __syncthreads();
-            if (threadIdx.x < TM) s_carry[threadIdx.x] += cnt_r;
+            if (WCSR && threadIdx.x < TM) s_carry[threadIdx.x] += s_run[threadIdx.x];
             __syncthreads();
             PROF_MARK(4);
             s_lo = s_hi;
@@ -2145,7 +2133,11 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     if (ev) TSG_HIP(hipEventRecord(ev[4], s));
     if (csr_out) {
         if (nnzC > 0) {
-            if (s3elem)
+            if (s3elem && !s2elem)  // denser tiles: row-start table
+                k_step3<TM, TN, true, false, true, true><<<gu, WG, 0, s>>>(
+                    utab, etab, nunits, A.m, V, E, C.tile_columnidx, C.tile_nnz, C.mask, unit_rb,
+                    csr_out->rowpointer, csr_out->columnindex, csr_out->value, nullptr, nullptr, nullptr, g_ablate);
+            else if (s3elem)
                 k_step3<TM, TN, true, false, true><<<gu, WG, 0, s>>>(
                     utab, etab, nunits, A.m, V, E, C.tile_columnidx, C.tile_nnz, C.mask, unit_rb,
                     csr_out->rowpointer, csr_out->columnindex, csr_out->value, nullptr, nullptr, nullptr, g_ablate);
