@@ -1479,9 +1479,10 @@ __device__ __forceinline__ void elem_stream(const ECsr &E, int4 ue, const EPre &
         int bs = 0, len = 0;
         if (threadIdx.x < na) {
             const int p = e0 + eb + threadIdx.x;
-            int r = 0;
+            int r = 0;  // last row of the tile row starting at or before entry p
 #pragma unroll
-            for (int rr = 1; rr < TM; ++rr) r += (s_rp[rr] <= p) ? 1 : 0;
+            for (int st = TM / 2; st > 0; st >>= 1)
+                if (s_rp[r + st] <= p) r += st;
             s_r[threadIdx.x] = (unsigned char)r;
             int be;
             if (eb == 0) {
@@ -1714,7 +1715,7 @@ __device__ __forceinline__ int tile_rank16(const u32 *tile, int r, int c) {
 // RST (denser tiles): a per-tile table of row-start ranks (u8) in LDS replaces
 // the eight popcounts of tile_rank16 on every product, at +4 KB of LDS.
 template <int TM, int TN, bool WCSR, bool WTILE, bool ELEM, bool RST = false>
-__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(6))) void k_step3(const int4 *utab, const int4 *etab, int nunits, int mrows, ABView V,
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(RST ? 5 : 6))) void k_step3(const int4 *utab, const int4 *etab, int nunits, int mrows, ABView V,
                                               ECsr E, const int *Ccol,
                                               const int *nnzoff, const u16 *maskC, const int *unit_rb,
                                               const int *rowptr, int *csr_col, double *csr_val, u16 *PtrC,
