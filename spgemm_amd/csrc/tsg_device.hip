@@ -968,10 +968,13 @@ __device__ __forceinline__ void bm_count_emit(const u32 *bm, int words, int wpt,
     }
 }
 
+//   PASS 0 with bm_store: the unit's bitmask is also stored (full window, vector
+//   stores), and PASS 2 then emits from it instead of re-enumerating the tile
+//   products (PASS 1).
 template <int PASS>
 __global__ __launch_bounds__(WG) void k_step1(const int *Aptr, const int *Acol, const int *Bptr, const int *Bcol,
                                               int tilemA, int tilenB, int nwin, int win, int *unit_cnt,
-                                              const int *unit_off, int *Ccol, u64 *prod_total) {
+                                              const int *unit_off, int *Ccol, u64 *prod_total, u32 *bm_store) {
     __shared__ __align__(16) u32 bm[S1_MAXWORDS];
     __shared__ ProdLds L;
     __shared__ int red[WAVES];
@@ -987,19 +990,46 @@ __global__ __launch_bounds__(WG) void k_step1(const int *Aptr, const int *Acol, 
             continue;
         }
         const int clo = w * win, chi = min(clo + win, tilenB) - 1;
-        // the whole window (a span bound from the B tile rows' first/last columns
-        // costs webbase more than it saves banded matrices)
-        const int wlo = 0, whi = words - 1;
-        for (int q = wlo + threadIdx.x; q <= whi; q += WG) bm[q] = 0u;
-        __syncthreads();
-        long it = for_each_product(a0, a1, Acol, Bptr, Bcol, clo, chi, nwin > 1, L, [&](int a, int b) {
-            (void)a;
-            int c = Bcol[b] - clo;
-            atomicOr(&bm[c >> 5], 1u << (c & 31));
-        });
-        if (PASS == 0) my_items += (threadIdx.x == 0) ? it : 0;
-        bm_count_emit<PASS>(bm, words, wpt, wlo, whi, clo, red, unit_cnt, u, PASS == 1 ? unit_off[u] : 0, Ccol);
-        __syncthreads();
+        if constexpr (PASS == 2) {
+            const int o = unit_off[u], n = unit_off[u + 1] - o;
+            if (n == 0) continue;  // uniform
+            u32 wv[8];
+            bm_words(bm_store + (size_t)u * words, wpt, wv);
+            int cnt = 0;
+            for (int q = 0; q < wpt; ++q) cnt += __popc(wv[q]);
+            int tot;
+            int off = block_excl_scan(cnt, &tot, red) + o;
+            for (int q = 0; q < wpt; ++q) {
+                u32 x = wv[q];
+                while (x) {
+                    Ccol[off++] = clo + (threadIdx.x * wpt + q) * 32 + __ffs(x) - 1;
+                    x &= x - 1;
+                }
+            }
+            continue;
+        } else {
+            const int wlo = 0, whi = words - 1;
+            for (int q = wlo + threadIdx.x; q <= whi; q += WG) bm[q] = 0u;
+            __syncthreads();
+            long it = for_each_product(a0, a1, Acol, Bptr, Bcol, clo, chi, nwin > 1, L, [&](int a, int b) {
+                (void)a;
+                int c = Bcol[b] - clo;
+                atomicOr(&bm[c >> 5], 1u << (c & 31));
+            });
+            if (PASS == 0) my_items += (threadIdx.x == 0) ? it : 0;
+            if (PASS == 0 && bm_store) {
+                u32 wv[8];
+                bm_words(bm, wpt, wv);
+                u32 *dst = bm_store + (size_t)u * words + threadIdx.x * wpt;
+                for (int q = 0; q < wpt; q += 4) {
+                    if (wpt >= 4) reinterpret_cast<uint4 *>(dst)[q / 4] = make_uint4(wv[q], wv[q + 1], wv[q + 2], wv[q + 3]);
+                }
+                if (wpt < 4)
+                    for (int q = 0; q < wpt; ++q) dst[q] = wv[q];
+            }
+            bm_count_emit<PASS>(bm, words, wpt, wlo, whi, clo, red, unit_cnt, u, PASS == 1 ? unit_off[u] : 0, Ccol);
+            __syncthreads();
+        }
     }
     if (PASS == 0 && threadIdx.x == 0 && my_items) atomicAdd(prod_total, (u64)my_items);
 }
@@ -1975,9 +2005,21 @@ int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_d
     TSG_HIP(hipMemsetAsync(prod, 0, sizeof(u64), s));
     TSG_HIP(hipMemsetAsync(ucnt + nunits1, 0, sizeof(int), s));
     const int g1 = grid_for(nunits1, 1, 16384);
+    // keep each unit's bitmask (window/8 bytes) for the emit pass when that fits
+    // 4 GiB: one tile-product enumeration instead of two
+    // (and when the products per unit -- estimated from the mean B tile row --
+    // outweigh a reread of the window's words, i.e. not for banded matrices)
+    u32 *bmst = nullptr;
+    const size_t bm_bytes = (size_t)nunits1 * (win / 8);
+    const double est_products = (double)A.numtile * ((double)B.numtile / (double)(B.tilem > 0 ? B.tilem : 1));
+    const bool store = bm_bytes <= (4ull << 30) && est_products >= (double)nunits1 * (win / 32) / 8.0;
+    if (store && !(g_ablate & 256) && cx.get(&bmst, bm_bytes / 4) != TSG_OK) {
+        bmst = nullptr;
+        (void)hipGetLastError();
+    }
     if (tilemA > 0)
         k_step1<0><<<g1, WG, 0, s>>>(A.tile_ptr, A.tile_columnidx, B.tile_ptr, B.tile_columnidx, tilemA, tilenB,
-                                     nwin, win, ucnt, nullptr, nullptr, prod);
+                                     nwin, win, ucnt, nullptr, nullptr, prod, bmst);
     TSG_HIP(hipGetLastError());
     long long numblk64 = 0;
     TSG_TRY(scan_exclusive_i32_total(cx, ucnt, nunits1 + 1, s, &numblk64));  // overflow: > INT_MAX C tiles
@@ -1989,10 +2031,16 @@ int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_d
     C.numtile = numblkC;
     const size_t nb1 = (size_t)numblkC + 1;
     TSG_TRY(cx.get(&C.tile_columnidx, nb1));
-    if (tilemA > 0)
-        k_step1<1><<<g1, WG, 0, s>>>(A.tile_ptr, A.tile_columnidx, B.tile_ptr, B.tile_columnidx, tilemA, tilenB,
-                                     nwin, win, nullptr, ucnt, C.tile_columnidx, nullptr);
+    if (tilemA > 0) {
+        if (bmst)
+            k_step1<2><<<g1, WG, 0, s>>>(A.tile_ptr, A.tile_columnidx, B.tile_ptr, B.tile_columnidx, tilemA, tilenB,
+                                         nwin, win, nullptr, ucnt, C.tile_columnidx, nullptr, bmst);
+        else
+            k_step1<1><<<g1, WG, 0, s>>>(A.tile_ptr, A.tile_columnidx, B.tile_ptr, B.tile_columnidx, tilemA, tilenB,
+                                         nwin, win, nullptr, ucnt, C.tile_columnidx, nullptr, nullptr);
+    }
     TSG_HIP(hipGetLastError());
+    cx.put(bmst);
     cx.put(ucnt);
     cx.put(prod);
     *tile_products_out = tile_products;
