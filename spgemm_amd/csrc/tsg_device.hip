@@ -1671,7 +1671,7 @@ __global__ __launch_bounds__(WG) void k_step2(const int4 *utab, const int4 *etab
                 pk[r >> 2] += (u64)c << (16 * (r & 3));
                 nz += c;
             }
-            nnzC[t0 + j] = nz;
+            if (nnzC) nnzC[t0 + j] = nz;  // tile nnz (host tile API; the CSR path needs only row counts)
             // C row masks (all-zero for empty tiles); step 3 reads them back
             uint4 *dst = reinterpret_cast<uint4 *>(maskC + (size_t)(t0 + j) * CM<TM>::TW);
 #pragma unroll
@@ -2080,12 +2080,12 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     TSG_TRY(cx.get(&urow, (size_t)maxu));
     TSG_TRY(cx.get(&utab, (size_t)maxu));
     TSG_TRY(cx.get(&unit_rc, (size_t)maxu * TM));
-    TSG_TRY(cx.get(&C.tile_nnz, nb1));
+    if (!csr_out) TSG_TRY(cx.get(&C.tile_nnz, nb1));  // CSR path: row counts only, no tile nnz scan
     TSG_TRY(cx.get(&C.mask, nb1 * CM<TM>::TW));
     k_units_per_row<<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(C.tile_ptr, tilemA, uoff);
     TSG_TRY(scan_exclusive_i32(cx, uoff, (long)tilemA + 1, s));
     k_unit_rows<<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(uoff, C.tile_ptr, tilemA, urow, utab);
-    k_set_i32<<<1, 1, 0, s>>>(C.tile_nnz + numblkC, 0);
+    if (C.tile_nnz) k_set_i32<<<1, 1, 0, s>>>(C.tile_nnz + numblkC, 0);
     TSG_HIP(hipGetLastError());
     int nunits = 0;
     TSG_TRY(read_i32(cx, uoff + tilemA, &nunits, s));
@@ -2153,7 +2153,7 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     }
     TSG_HIP(hipGetLastError());
     long long nnz64 = 0;
-    TSG_TRY(scan_exclusive_i32_total(cx, C.tile_nnz, (long)numblkC + 1, s, &nnz64));  // nnz(C) must fit int32
+    if (!csr_out) TSG_TRY(scan_exclusive_i32_total(cx, C.tile_nnz, (long)numblkC + 1, s, &nnz64));  // fits int32
     if (csr_out) {
         csr_out->m = A.m;
         csr_out->n = B.n;
@@ -2164,7 +2164,7 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
             k_unit_rowbase<TM><<<grid_for((long)tilemA * TM, WG, 8192), WG, 0, s>>>(uoff, tilemA, A.m, unit_rc, unit_rb,
                                                                                   csr_out->rowpointer);
         TSG_HIP(hipGetLastError());
-        TSG_TRY(scan_exclusive_i32(cx, csr_out->rowpointer, (long)A.m + 1, s));
+        TSG_TRY(scan_exclusive_i32_total(cx, csr_out->rowpointer, (long)A.m + 1, s, &nnz64));  // nnz(C) fits int32
     }
     const int nnzC = (int)nnz64;
     C.nnz = nnzC;
