@@ -1175,8 +1175,9 @@ __global__ void k_unit_etab(const int4 *utab, int nunits, const int *rpA, int m,
 // starts its segment at the first B row position reaching the unit's first
 // tile column; the last unit also writes the row ends.
 template <int TM>
-__global__ __launch_bounds__(WG) void k_esplit_units(const int4 *utab, const int4 *etab, int nunits, const int *ciA,
-                                                     const int *rpB, const int *ciB, const int *Ccol, int *esplit) {
+__global__ __launch_bounds__(WG) void k_esplit_units(const int4 *utab, const int4 *etab, int nunits,
+                                                     const int2 *ebnd, const int *ciB, const int *Ccol,
+                                                     int *esplit) {
     const int lane = lane_id();
     for (int u = (blockIdx.x * WG + threadIdx.x) >> 6; u < nunits; u += gridDim.x * WAVES) {
         const int4 ut = utab[u], ue = etab[u];
@@ -1185,11 +1186,18 @@ __global__ __launch_bounds__(WG) void k_esplit_units(const int4 *utab, const int
         int *sp = esplit + (((long long)(unsigned)ue.z) | ((long long)ue.w << 32));
         const int key = Ccol[t0] * TM;
         for (int x = lane; x < ei; x += 64) {
-            const int k = ciA[e0 + x];
-            const int b0 = rpB[k], b1 = rpB[k + 1];
-            sp[x] = q == 0 ? b0 : lower_bound_dev(ciB, b0, b1, key);
-            if (q == nu - 1) sp[ei + x] = b1;
+            const int2 b = ebnd[e0 + x];  // the entry's B row [b0, b1), one coalesced load
+            sp[x] = q == 0 ? b.x : lower_bound_dev(ciB, b.x, b.y, key);
+            if (q == nu - 1) sp[ei + x] = b.y;
         }
+    }
+}
+
+// per A entry: its B row's position range
+__global__ __launch_bounds__(WG) void k_entry_bounds(const int *ciA, long nnzA, const int *rpB, int2 *ebnd) {
+    for (long p = (long)blockIdx.x * WG + threadIdx.x; p < nnzA; p += (long)gridDim.x * WG) {
+        const int k = ciA[p];
+        ebnd[p] = make_int2(rpB[k], rpB[k + 1]);
     }
 }
 
@@ -2120,6 +2128,7 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     int *esplit = nullptr;
     long long *ebase = nullptr;
     int4 *etab = nullptr;
+    int2 *ebnd = nullptr;
     if (s2elem || s3elem) {
         TSG_TRY(cx.get(&ebase, (size_t)tilemA + 1));
         k_esplit_counts<TM><<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(uoff, Acsr->rowpointer, A.m, tilemA, ebase);
@@ -2133,9 +2142,13 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
         if (nunits > 0) {
             k_unit_etab<TM><<<grid_for(nunits, WG, 8192), WG, 0, s>>>(utab, nunits, Acsr->rowpointer, A.m, ebase,
                                                                       etab);
-            k_esplit_units<TM><<<grid_for(nunits, WAVES, 16384), WG, 0, s>>>(
-                utab, etab, nunits, Acsr->columnindex, Bcsr->rowpointer, Bcsr->columnindex, C.tile_columnidx,
-                esplit);
+            TSG_TRY(cx.get(&ebnd, (size_t)Acsr->nnz + 1));
+            if (Acsr->nnz > 0)
+                k_entry_bounds<<<grid_for(Acsr->nnz, WG, 16384), WG, 0, s>>>(Acsr->columnindex, Acsr->nnz,
+                                                                            Bcsr->rowpointer, ebnd);
+            k_esplit_units<TM><<<grid_for(nunits, WAVES, 16384), WG, 0, s>>>(utab, etab, nunits, ebnd,
+                                                                             Bcsr->columnindex, C.tile_columnidx,
+                                                                             esplit);
         }
         TSG_HIP(hipGetLastError());
     }
@@ -2219,6 +2232,7 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     cx.put(esplit);
     cx.put(ebase);
     cx.put(etab);
+    cx.put(ebnd);
     cx.put(uoff);
     cx.put(urow);
     cx.put(utab);
