@@ -111,6 +111,6 @@ int read_i32(Context &cx, const int *d, int *h, hipStream_t s);
 int read_i64(Context &cx, const long long *d, long long *h, hipStream_t s);
 
 bool tile_size_supported(int tm, int tn);  // the SpGEMM steps (16x16)
-bool tile_side_supported(int t);         // csr2tile / tile2csr sides: 16, 32, 64
+bool tile_side_supported(int t);         // csr2tile / tile2csr sides: 16, 32, 48, 64
 
 }  // namespace tsg
