@@ -1578,7 +1578,8 @@ __device__ unsigned long long g_prof[16];  // [0,8) step 3, [8,16) step 2
 
 template <int TM, int TN, bool ELEM>
 __global__ __launch_bounds__(WG) void k_step2(const int4 *utab, const int4 *etab, int nunits, ABView V, ECsr E,
-                                              const int *Ccol, int *nnzC, int *unit_rc, u16 *maskC, int ablate) {
+                                              const int *Ccol, int *nnzC, int *unit_rc, u16 *maskC, u16 *codeC,
+                                              int ablate) {
 #ifdef TSG_PROF_BUILD
     u64 prof_t = (ablate & 64) ? __builtin_amdgcn_s_memtime() : 0;
 #endif
@@ -1588,6 +1589,7 @@ __global__ __launch_bounds__(WG) void k_step2(const int4 *utab, const int4 *etab
     __shared__ int s_rc[TM];
     __shared__ int s_rp[TM + 1];
     __shared__ unsigned char s_r[WG];
+    __shared__ int s_wm[WAVES];
     __shared__ ProdLds L;
     // Software pipeline over this workgroup's units (stride G): the unit tables
     // run two units ahead and the unit's first loads (C tile columns, split
@@ -1658,16 +1660,16 @@ __global__ __launch_bounds__(WG) void k_step2(const int4 *utab, const int4 *etab
         u64 pk[NP];
 #pragma unroll
         for (int g = 0; g < NP; ++g) pk[g] = 0;
-        if (threadIdx.x < ns) {  // ns <= CH == WG
-            static_assert((CM<TM>::TW32 % 4) == 0, "mask tile must be whole uint4");
-            const int j = threadIdx.x;
-            u32 w[TW32];  // the tile's words via vector LDS reads
+        static_assert((CM<TM>::TW32 % 4) == 0, "mask tile must be whole uint4");
+        u32 w[TW32];  // tile j's words via vector LDS reads
+        int nz = 0;
+        const int j = threadIdx.x;
+        if (j < ns) {  // ns <= CH == WG
 #pragma unroll
             for (int k = 0; k < TW32 / 4; ++k) {
                 const uint4 v = reinterpret_cast<const uint4 *>(s_mask + j * TW32)[k];
                 w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
             }
-            int nz = 0;
 #pragma unroll
             for (int r = 0; r < TM; ++r) {
                 int c = 0;
@@ -1680,10 +1682,12 @@ __global__ __launch_bounds__(WG) void k_step2(const int4 *utab, const int4 *etab
                 nz += c;
             }
             if (nnzC) nnzC[t0 + j] = nz;  // tile nnz (host tile API; the CSR path needs only row counts)
-            // C row masks (all-zero for empty tiles); step 3 reads them back
-            uint4 *dst = reinterpret_cast<uint4 *>(maskC + (size_t)(t0 + j) * CM<TM>::TW);
+            if (!codeC) {  // C row masks in tile order (all-zero for empty tiles): the tile API's C.mask
+                uint4 *dst = reinterpret_cast<uint4 *>(maskC + (size_t)(t0 + j) * CM<TM>::TW);
 #pragma unroll
-            for (int k = 0; k < TW32 / 4; ++k) dst[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+                for (int k = 0; k < TW32 / 4; ++k)
+                    dst[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+            }
         }
 #pragma unroll
         for (int g = 0; g < NP; ++g) pk[g] = wave_sum(pk[g]);
@@ -1694,7 +1698,32 @@ __global__ __launch_bounds__(WG) void k_step2(const int4 *utab, const int4 *etab
             const int c = (int)((v >> (16 * (lane_id() & 3))) & 0xffffu);
             if (c) atomicAdd(&s_rc[lane_id()], c);
         }
+        u64 bm = 0;
+        if (codeC) {
+            bm = __ballot(nz > 1);
+            if (lane_id() == 0) s_wm[wave_id()] = __popcll(bm);
+        }
         __syncthreads();
+        if (codeC && j < ns) {  // compact form for step 3 (16x16 tiles)
+            u32 code = 0;
+            if (nz == 1) {  // one nonzero: its in-tile position r << 4 | c
+#pragma unroll
+                for (int k = 0; k < TW32; ++k)
+                    if (w[k]) {
+                        const int hb = 31 - __clz(w[k]);
+                        code = 0x8000u | (u32)((2 * k + (hb >> 4)) << 4) | (u32)(15 - (hb & 15));
+                    }
+            } else if (nz > 1) {  // full mask, compacted to the front of the unit's mask range
+                int idx = __builtin_amdgcn_mbcnt_hi((u32)(bm >> 32), __builtin_amdgcn_mbcnt_lo((u32)bm, 0u));
+                for (int w2 = 0; w2 < wave_id(); ++w2) idx += s_wm[w2];
+                code = (u32)idx + 1;
+                uint4 *dst = reinterpret_cast<uint4 *>(maskC + (size_t)(t0 + idx) * CM<TM>::TW);
+#pragma unroll
+                for (int k = 0; k < TW32 / 4; ++k)
+                    dst[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+            }
+            codeC[t0 + j] = (u16)code;
+        }
         if (threadIdx.x < TM) unit_rc[(long)u * TM + threadIdx.x] = s_rc[threadIdx.x];
         __syncthreads();
         PROF_MARK(10);
@@ -1755,7 +1784,8 @@ __device__ __forceinline__ int tile_rank16(const u32 *tile, int r, int c) {
 template <int TM, int TN, bool WCSR, bool WTILE, bool ELEM, bool RST = false>
 __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(RST ? 5 : 6))) void k_step3(const int4 *utab, const int4 *etab, int nunits, int mrows, ABView V,
                                               ECsr E, const int *Ccol,
-                                              const int *nnzoff, const u16 *maskC, const int *unit_rb,
+                                              const int *nnzoff, const u16 *maskC, const u16 *codeC,
+                                              const int *unit_rb,
                                               const int *rowptr, int *csr_col, double *csr_val, u16 *PtrC,
                                               u16 *ColC, double *ValC, int ablate) {
     static_assert(TM == 16, "tile-major step 3 is built for 16x16 C tiles");
@@ -1782,13 +1812,16 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(RST ? 5 : 6)
     u64 prof_t = (ablate & 64) ? __builtin_amdgcn_s_memtime() : 0;
 #endif
     int4 ut_n = make_int4(0, 0, 0, 0), ue_n = make_int4(0, 0, 0, 0);
+    u32 code_n = 0;  // WCSR: this thread's tile code of the next unit (loaded one unit ahead)
     if ((int)blockIdx.x < nunits) {
         ut_n = utab[blockIdx.x];
         if (ELEM) ue_n = etab[blockIdx.x];
+        if (WCSR && j < (ut_n.w & 511)) code_n = codeC[ut_n.y + j];
     }
     for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
         PROF_MARK(7);
         const int4 ut = ut_n, ue = ue_n;
+        const u32 code = code_n;
         if (u + (int)gridDim.x < nunits) {  // next unit's table entries, in flight during this one
             ut_n = utab[u + gridDim.x];
             if (ELEM) ue_n = etab[u + gridDim.x];
@@ -1798,19 +1831,34 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(RST ? 5 : 6)
         if (ELEM && !(ablate & 4)) pre = epre_load(E, ue, true);
         // ---- load: C masks (written by step 2) + columns; thread j owns tile j
         u32 w[TW32];
+#pragma unroll
+        for (int k = 0; k < TW32; ++k) w[k] = 0u;
         int col = 0;
         if (j < ns) {
-            const uint4 *src = reinterpret_cast<const uint4 *>(maskC + (size_t)(t0 + j) * CM<TM>::TW);
+            if (WCSR) {  // compact form (k_step2): 0 empty, 0x8000|pos one nonzero, idx+1 full mask
+                if (code & 0x8000u) {
+                    const int r = (code >> 4) & 15, c = code & 15;
 #pragma unroll
-            for (int k = 0; k < NV4; ++k) {
-                const uint4 v = src[k];
-                w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+                    for (int k = 0; k < TW32; ++k) w[k] = (k == (r >> 1)) ? (0x8000u >> c) << ((r & 1) * 16) : 0u;
+                } else if (code) {
+                    const uint4 *src = reinterpret_cast<const uint4 *>(maskC + (size_t)(t0 + code - 1) * CM<TM>::TW);
+#pragma unroll
+                    for (int k = 0; k < NV4; ++k) {
+                        const uint4 v = src[k];
+                        w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+                    }
+                }
+            } else {
+                const uint4 *src = reinterpret_cast<const uint4 *>(maskC + (size_t)(t0 + j) * CM<TM>::TW);
+#pragma unroll
+                for (int k = 0; k < NV4; ++k) {
+                    const uint4 v = src[k];
+                    w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+                }
             }
             col = Ccol[t0 + j];
-        } else {
-#pragma unroll
-            for (int k = 0; k < TW32; ++k) w[k] = 0u;
         }
+        if (WCSR && u + (int)gridDim.x < nunits) code_n = j < (ut_n.w & 511) ? (u32)codeC[ut_n.y + j] : 0u;
         if (threadIdx.x < TM) {
             s_carry[threadIdx.x] = WCSR ? unit_rb[(long)u * TM + threadIdx.x] : 0;
             if (WCSR) s_rowptr[threadIdx.x] = rowptr[min(i * TM + (int)threadIdx.x, mrows)];
@@ -2090,6 +2138,10 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     TSG_TRY(cx.get(&unit_rc, (size_t)maxu * TM));
     if (!csr_out) TSG_TRY(cx.get(&C.tile_nnz, nb1));  // CSR path: row counts only, no tile nnz scan
     TSG_TRY(cx.get(&C.mask, nb1 * CM<TM>::TW));
+    // CSR path: step 2 hands step 3 a u16 code per C tile and full masks only for
+    // tiles with > 1 nonzero (most webbase-like C tiles hold one nonzero)
+    u16 *codeC = nullptr;
+    if (csr_out) TSG_TRY(cx.get(&codeC, nb1));
     k_units_per_row<<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(C.tile_ptr, tilemA, uoff);
     TSG_TRY(scan_exclusive_i32(cx, uoff, (long)tilemA + 1, s));
     k_unit_rows<<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(uoff, C.tile_ptr, tilemA, urow, utab);
@@ -2159,10 +2211,10 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     if (numblkC > 0) {
         if (s2elem)
             k_step2<TM, TN, true><<<gu, WG, 0, s>>>(utab, etab, nunits, V, E, C.tile_columnidx, C.tile_nnz, unit_rc,
-                                                    C.mask, g_ablate);
+                                                    C.mask, codeC, g_ablate);
         else
             k_step2<TM, TN, false><<<gu, WG, 0, s>>>(utab, etab, nunits, V, E, C.tile_columnidx, C.tile_nnz, unit_rc,
-                                                     C.mask, g_ablate);
+                                                     C.mask, codeC, g_ablate);
     }
     TSG_HIP(hipGetLastError());
     long long nnz64 = 0;
@@ -2197,21 +2249,21 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
         if (nnzC > 0) {
             if (s3elem && !s2elem)  // denser tiles: row-start table
                 k_step3<TM, TN, true, false, true, true><<<gu, WG, 0, s>>>(
-                    utab, etab, nunits, A.m, V, E, C.tile_columnidx, C.tile_nnz, C.mask, unit_rb,
+                    utab, etab, nunits, A.m, V, E, C.tile_columnidx, C.tile_nnz, C.mask, codeC, unit_rb,
                     csr_out->rowpointer, csr_out->columnindex, csr_out->value, nullptr, nullptr, nullptr, g_ablate);
             else if (s3elem)
                 k_step3<TM, TN, true, false, true><<<gu, WG, 0, s>>>(
-                    utab, etab, nunits, A.m, V, E, C.tile_columnidx, C.tile_nnz, C.mask, unit_rb,
+                    utab, etab, nunits, A.m, V, E, C.tile_columnidx, C.tile_nnz, C.mask, codeC, unit_rb,
                     csr_out->rowpointer, csr_out->columnindex, csr_out->value, nullptr, nullptr, nullptr, g_ablate);
             else
                 k_step3<TM, TN, true, false, false><<<gu, WG, 0, s>>>(
-                    utab, etab, nunits, A.m, V, E, C.tile_columnidx, C.tile_nnz, C.mask, unit_rb,
+                    utab, etab, nunits, A.m, V, E, C.tile_columnidx, C.tile_nnz, C.mask, codeC, unit_rb,
                     csr_out->rowpointer, csr_out->columnindex, csr_out->value, nullptr, nullptr, nullptr, g_ablate);
         }
     } else {
         if (nnzC > 0)
             k_step3<TM, TN, false, true, false><<<gu, WG, 0, s>>>(
-                utab, etab, nunits, A.m, V, E, C.tile_columnidx, C.tile_nnz, C.mask, nullptr, nullptr,
+                utab, etab, nunits, A.m, V, E, C.tile_columnidx, C.tile_nnz, C.mask, nullptr, nullptr, nullptr,
                 nullptr, nullptr, C.tile_csr_Ptr, C.tile_csr_Col, C.tile_csr_Value, g_ablate);
     }
     TSG_HIP(hipGetLastError());
@@ -2232,6 +2284,7 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     cx.put(esplit);
     cx.put(ebase);
     cx.put(etab);
+    cx.put(codeC);
     cx.put(ebnd);
     cx.put(uoff);
     cx.put(urow);
