@@ -1811,64 +1811,88 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(RST ? 5 : 6)
 #ifdef TSG_PROF_BUILD
     u64 prof_t = (ablate & 64) ? __builtin_amdgcn_s_memtime() : 0;
 #endif
-    int4 ut_n = make_int4(0, 0, 0, 0), ue_n = make_int4(0, 0, 0, 0);
-    u32 code_n = 0;  // WCSR: this thread's tile code of the next unit (loaded one unit ahead)
-    if ((int)blockIdx.x < nunits) {
-        ut_n = utab[blockIdx.x];
-        if (ELEM) ue_n = etab[blockIdx.x];
-        if (WCSR && j < (ut_n.w & 511)) code_n = codeC[ut_n.y + j];
-    }
-    for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
-        PROF_MARK(7);
-        const int4 ut = ut_n, ue = ue_n;
-        const u32 code = code_n;
-        if (u + (int)gridDim.x < nunits) {  // next unit's table entries, in flight during this one
-            ut_n = utab[u + gridDim.x];
-            if (ELEM) ue_n = etab[u + gridDim.x];
-        }
-        const int i = ut.x, t0 = ut.y, nu = ut.z, q = ut.w >> 9, ns = ut.w & 511;
-        EPre pre{0, 0, 0.0};
-        if (ELEM && !(ablate & 4)) pre = epre_load(E, ue, true);
-        // ---- load: C masks (written by step 2) + columns; thread j owns tile j
-        u32 w[TW32];
+    // Software pipeline over this workgroup's units (stride G): the unit tables
+    // run two units ahead, the tile codes one unit ahead, and the unit's inputs
+    // (C masks + columns, row bases, first element batch) are issued for the
+    // next unit once this unit's value pass is done, so their HBM round trip
+    // overlaps this unit's CSR writes.
+    const int G = gridDim.x;
+    u32 nw[TW32];
+    int ncol = 0, nrb = 0, nrw = 0, nrp = 0;
+    EPre npre{0, 0, 0.0};
+    auto issue = [&](int un, int4 utx, int4 uex, u32 cd) {
+        const int t0x = utx.y, nsx = utx.w & 511, ix = utx.x;
 #pragma unroll
-        for (int k = 0; k < TW32; ++k) w[k] = 0u;
-        int col = 0;
-        if (j < ns) {
+        for (int k = 0; k < TW32; ++k) nw[k] = 0u;
+        ncol = 0;
+        if (j < nsx) {
             if (WCSR) {  // compact form (k_step2): 0 empty, 0x8000|pos one nonzero, idx+1 full mask
-                if (code & 0x8000u) {
-                    const int r = (code >> 4) & 15, c = code & 15;
+                if (cd & 0x8000u) {
+                    const int r = (cd >> 4) & 15, c = cd & 15;
 #pragma unroll
-                    for (int k = 0; k < TW32; ++k) w[k] = (k == (r >> 1)) ? (0x8000u >> c) << ((r & 1) * 16) : 0u;
-                } else if (code) {
-                    const uint4 *src = reinterpret_cast<const uint4 *>(maskC + (size_t)(t0 + code - 1) * CM<TM>::TW);
+                    for (int k = 0; k < TW32; ++k) nw[k] = (k == (r >> 1)) ? (0x8000u >> c) << ((r & 1) * 16) : 0u;
+                } else if (cd) {
+                    const uint4 *src = reinterpret_cast<const uint4 *>(maskC + (size_t)(t0x + cd - 1) * CM<TM>::TW);
 #pragma unroll
                     for (int k = 0; k < NV4; ++k) {
                         const uint4 v = src[k];
-                        w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+                        nw[4 * k] = v.x; nw[4 * k + 1] = v.y; nw[4 * k + 2] = v.z; nw[4 * k + 3] = v.w;
                     }
                 }
             } else {
-                const uint4 *src = reinterpret_cast<const uint4 *>(maskC + (size_t)(t0 + j) * CM<TM>::TW);
+                const uint4 *src = reinterpret_cast<const uint4 *>(maskC + (size_t)(t0x + j) * CM<TM>::TW);
 #pragma unroll
                 for (int k = 0; k < NV4; ++k) {
                     const uint4 v = src[k];
-                    w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+                    nw[4 * k] = v.x; nw[4 * k + 1] = v.y; nw[4 * k + 2] = v.z; nw[4 * k + 3] = v.w;
                 }
             }
-            col = Ccol[t0 + j];
+            ncol = Ccol[t0x + j];
         }
-        if (WCSR && u + (int)gridDim.x < nunits) code_n = j < (ut_n.w & 511) ? (u32)codeC[ut_n.y + j] : 0u;
+        if (WCSR && j < TM) {
+            nrb = unit_rb[(long)un * TM + j];
+            nrw = rowptr[min(ix * TM + j, mrows)];
+        }
+        if (ELEM && j <= TM) nrp = E.rpA[min(ix * TM + j, E.m)];
+        if (ELEM && !(ablate & 4)) npre = epre_load(E, uex, true);
+    };
+    int4 ut_c = make_int4(0, 0, 0, 0), ue_c = ut_c, ut_n = ut_c, ue_n = ut_c;
+    u32 code_n = 0;
+    if ((int)blockIdx.x < nunits) {
+        ut_c = utab[blockIdx.x];
+        if (ELEM) ue_c = etab[blockIdx.x];
+        if (WCSR && j < (ut_c.w & 511)) code_n = codeC[ut_c.y + j];
+        issue(blockIdx.x, ut_c, ue_c, code_n);
+    }
+    if ((int)blockIdx.x + G < nunits) {
+        ut_n = utab[blockIdx.x + G];
+        if (ELEM) ue_n = etab[blockIdx.x + G];
+    }
+    for (int u = blockIdx.x; u < nunits; u += G) {
+        PROF_MARK(7);
+        const int4 ut = ut_c, ue = ue_c;
+        ut_c = ut_n;
+        ue_c = ue_n;
+        if (u + 2 * G < nunits) {
+            ut_n = utab[u + 2 * G];
+            if (ELEM) ue_n = etab[u + 2 * G];
+        }
+        const bool more = u + G < nunits;
+        const int i = ut.x, t0 = ut.y, nu = ut.z, q = ut.w >> 9, ns = ut.w & 511;
+        const EPre pre = npre;
+        u32 w[TW32];
+#pragma unroll
+        for (int k = 0; k < TW32; ++k) w[k] = nw[k];
         if (threadIdx.x < TM) {
-            s_carry[threadIdx.x] = WCSR ? unit_rb[(long)u * TM + threadIdx.x] : 0;
-            if (WCSR) s_rowptr[threadIdx.x] = rowptr[min(i * TM + (int)threadIdx.x, mrows)];
+            s_carry[threadIdx.x] = WCSR ? nrb : 0;
+            if (WCSR) s_rowptr[threadIdx.x] = nrw;
         }
-        if (ELEM && threadIdx.x <= TM) s_rp[threadIdx.x] = E.rpA[min(i * TM + (int)threadIdx.x, E.m)];
+        if (ELEM && threadIdx.x <= TM) s_rp[threadIdx.x] = nrp;
 #pragma unroll
         for (int k = 0; k < NV4; ++k)
             reinterpret_cast<uint4 *>(s_mask + j * TW32)[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2],
                                                                          w[4 * k + 3]);
-        s_cols[j] = col;
+        s_cols[j] = ncol;
         int tt = 0;
         if (RST) {
             u32 rs4[TM / 4];
@@ -1890,8 +1914,10 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(RST ? 5 : 6)
         const int toff = block_excl_scan(tt, &ttot, s_red);
         s_off[j] = toff;
         if (j == WG - 1) s_off[CH] = ttot;
+        if (WCSR && more) code_n = j < (ut_c.w & 511) ? (u32)codeC[ut_c.y + j] : 0u;
         PROF_MARK(0);
         if (ttot == 0) {  // uniform: every tile of the unit is empty
+            if (more) issue(u + G, ut_c, ue_c, code_n);
             __syncthreads();
             continue;
         }
@@ -1913,25 +1939,75 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(RST ? 5 : 6)
         const int nzbase = WTILE ? nnzoff[t0] : 0;
         __syncthreads();
         PROF_MARK(1);
-        for (int s_lo = 0; s_lo < ns;) {
+        int s_lo = 0, s_hi = 0, base = 0, nz = 0;  // the current pass: tiles [s_lo, s_hi)
+        // ---- W: outputs of a pass
+        auto write_pass = [&]() {
+            if (WCSR && !(ablate & 8)) {
+                for (int eb = 0; eb < nz; eb += WG) {
+                    const int e = eb + threadIdx.x;
+                    const bool in = e < nz;
+                    const int key = in ? (int)s_key[e] : 0;
+                    const int r = key >> 4;
+                    int lrank = 0;
+#pragma unroll
+                    for (int rr = 0; rr < TM; ++rr) {  // rank among this wave's row-rr nonzeros
+                        const u64 m = __ballot(in && r == rr);
+                        if (r == rr) lrank = __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));
+                        if (lane == 0) s_wcnt[wv][rr] = __popcll(m);
+                    }
+                    __syncthreads();
+                    if (in) {
+                        int before = s_run[r];
+                        for (int w2 = 0; w2 < wv; ++w2) before += s_wcnt[w2][r];
+                        const int dst = s_rowptr[r] + s_carry[r] + before + lrank;
+                        csr_col[dst] = s_cols[s_kt[e]] * TM + (key & 15);
+                        csr_val[dst] = acc[e];
+                    }
+                    __syncthreads();
+                    if (threadIdx.x < TM) {
+                        int add = 0;
+                        for (int w2 = 0; w2 < WAVES; ++w2) add += s_wcnt[w2][threadIdx.x];
+                        s_run[threadIdx.x] += add;
+                    }
+                    __syncthreads();  // s_wcnt is rewritten by the next 256 nonzeros
+                }
+            }
+            if (WTILE) {
+                if (j >= s_lo && j < s_hi && tt > 0) {
+                    const int e0 = toff - base, out = nzbase + toff;
+                    for (int k = 0; k < tt; ++k) {
+                        ColC[out + k] = (u16)(s_key[e0 + k] & 15);
+                        ValC[out + k] = acc[e0 + k];
+                    }
+                }
+            }
+            __syncthreads();
+            if (WCSR && threadIdx.x < TM) s_carry[threadIdx.x] += s_run[threadIdx.x];
+            __syncthreads();
+            PROF_MARK(4);
+        };
+        for (;;) {
             int lo = s_lo + 1, hi = ns;  // largest s_hi with nnz(tiles s_lo..s_hi-1) <= NZCAP
             while (lo < hi) {
                 const int mid = (lo + hi + 1) >> 1;
                 if (s_off[mid] - s_off[s_lo] <= S3_NZCAP) lo = mid; else hi = mid - 1;
             }
-            const int s_hi = lo;
-            const int base = s_off[s_lo];
-            const int nz = s_off[s_hi] - base;
-            if (nz == 0) {  // uniform
-                s_lo = s_hi;
-                continue;
-            }
+            s_hi = lo;
+            base = s_off[s_lo];
+            nz = s_off[s_hi] - base;
+            if (nz == 0) break;  // uniform; only the last pass can be empty (it then runs to ns)
             // expand the pass's nonzeros (tile-major, then row-major in the tile)
             if (j >= s_lo && j < s_hi && tt > 0) {
                 int e = toff - base;
+                u32 wl[TW32];  // tile j's words, back from LDS
+#pragma unroll
+                for (int k = 0; k < NV4; ++k) {
+                    const uint4 v = reinterpret_cast<const uint4 *>(s_mask + j * TW32)[k];
+                    wl[4 * k] = v.x; wl[4 * k + 1] = v.y; wl[4 * k + 2] = v.z; wl[4 * k + 3] = v.w;
+                }
 #pragma unroll
                 for (int r = 0; r < TM; ++r) {
-                    u32 v = (w[r >> 1] >> ((r & 1) * 16)) & 0xffffu;
+                    u32 v = (wl[r >> 1] >> ((r & 1) * 16)) & 0xffffu;
                     while (v) {
                         const int hb = 31 - __clz(v);  // MSB-first: lowest column first
                         s_key[e] = (unsigned char)((r << 4) | (15 - hb));
@@ -1987,52 +2063,12 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(RST ? 5 : 6)
                 }
             }
             PROF_MARK(3);
-            // ---- W: outputs of the pass
-            if (WCSR && !(ablate & 8)) {
-                for (int eb = 0; eb < nz; eb += WG) {
-                    const int e = eb + threadIdx.x;
-                    const bool in = e < nz;
-                    const int key = in ? (int)s_key[e] : 0;
-                    const int r = key >> 4;
-                    int lrank = 0;
-#pragma unroll
-                    for (int rr = 0; rr < TM; ++rr) {  // rank among this wave's row-rr nonzeros
-                        const u64 m = __ballot(in && r == rr);
-                        if (r == rr) lrank = __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));
-                        if (lane == 0) s_wcnt[wv][rr] = __popcll(m);
-                    }
-                    __syncthreads();
-                    if (in) {
-                        int before = s_run[r];
-                        for (int w2 = 0; w2 < wv; ++w2) before += s_wcnt[w2][r];
-                        const int dst = s_rowptr[r] + s_carry[r] + before + lrank;
-                        csr_col[dst] = s_cols[s_kt[e]] * TM + (key & 15);
-                        csr_val[dst] = acc[e];
-                    }
-                    __syncthreads();
-                    if (threadIdx.x < TM) {
-                        int add = 0;
-                        for (int w2 = 0; w2 < WAVES; ++w2) add += s_wcnt[w2][threadIdx.x];
-                        s_run[threadIdx.x] += add;
-                    }
-                    __syncthreads();  // s_wcnt is rewritten by the next 256 nonzeros
-                }
-            }
-            if (WTILE) {
-                if (j >= s_lo && j < s_hi && tt > 0) {
-                    const int e0 = toff - base, out = nzbase + toff;
-                    for (int k = 0; k < tt; ++k) {
-                        ColC[out + k] = (u16)(s_key[e0 + k] & 15);
-                        ValC[out + k] = acc[e0 + k];
-                    }
-                }
-            }
-            __syncthreads();
-            if (WCSR && threadIdx.x < TM) s_carry[threadIdx.x] += s_run[threadIdx.x];
-            __syncthreads();
-            PROF_MARK(4);
+            if (s_hi == ns) break;  // the last pass writes after the next unit's loads are issued
+            write_pass();
             s_lo = s_hi;
         }
+        if (more) issue(u + G, ut_c, ue_c, code_n);  // in flight during the last pass's writes
+        if (nz > 0) write_pass();
     }
 }
 
