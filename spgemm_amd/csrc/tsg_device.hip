@@ -1492,6 +1492,19 @@ struct EPre {
     double va;
 };
 
+// Unit-table prefetch: a row (int4) fetched one int per lane (lanes 0..3), so it
+// stays a divergent vector load whose wait sits at the row's first use
+// (tab_row).  A uniform int4 load is compiled to a vector load followed at once
+// by readfirstlane -- a full HBM round trip at the prefetch point.
+__device__ __forceinline__ int tab_fetch(const int4 *tab, int u) {
+    const int l = lane_id();
+    return l < 4 ? reinterpret_cast<const int *>(tab + u)[l] : 0;
+}
+__device__ __forceinline__ int4 tab_row(int v) {
+    return make_int4(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 1),
+                     __builtin_amdgcn_readlane(v, 2), __builtin_amdgcn_readlane(v, 3));
+}
+
 __device__ __forceinline__ const int *etab_split(const ECsr &E, int4 ue) {
     return E.esplit + (((long long)(unsigned)ue.z) | ((long long)ue.w << 32));
 }
@@ -1577,7 +1590,7 @@ __device__ unsigned long long g_prof[16];  // [0,8) step 3, [8,16) step 2
 #endif
 
 template <int TM, int TN, bool ELEM>
-__global__ __launch_bounds__(WG) void k_step2(const int4 *utab, const int4 *etab, int nunits, ABView V, ECsr E,
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(6))) void k_step2(const int4 *utab, const int4 *etab, int nunits, ABView V, ECsr E,
                                               const int *Ccol, int *nnzC, int *unit_rc, u16 *maskC, u16 *codeC,
                                               int ablate) {
 #ifdef TSG_PROF_BUILD
@@ -1610,7 +1623,9 @@ __global__ __launch_bounds__(WG) void k_step2(const int4 *utab, const int4 *etab
         }
         return d;
     };
+    constexpr bool LT = true;  // lane-fetched unit tables (tab_fetch)
     int4 ut_a = make_int4(0, 0, 0, 0), ue_a = ut_a, ut_b = ut_a, ue_b = ut_a;
+    int tv_b = 0, ev_b = 0;  // tables of the unit two ahead (lanes 0..3, tab_fetch)
     UData d_a{0, 0, {0, 0, 0.0}};
     if ((int)blockIdx.x < nunits) {
         ut_a = utab[blockIdx.x];
@@ -1618,18 +1633,28 @@ __global__ __launch_bounds__(WG) void k_step2(const int4 *utab, const int4 *etab
         d_a = load_data(ut_a, ue_a);
     }
     if ((int)blockIdx.x + G < nunits) {
-        ut_b = utab[blockIdx.x + G];
-        if (ELEM) ue_b = etab[blockIdx.x + G];
+        if (LT) {
+            tv_b = tab_fetch(utab, blockIdx.x + G);
+            if (ELEM) ev_b = tab_fetch(etab, blockIdx.x + G);
+        } else {
+            ut_b = utab[blockIdx.x + G];
+            if (ELEM) ue_b = etab[blockIdx.x + G];
+        }
     }
     for (int u = blockIdx.x; u < nunits; u += G) {
         const int4 ut = ut_a, ue = ue_a;
         const UData d = d_a;
-        if (u + G < nunits) d_a = load_data(ut_b, ue_b);
-        ut_a = ut_b;
-        ue_a = ue_b;
+        ut_a = LT ? tab_row(tv_b) : ut_b;
+        if (ELEM) ue_a = LT ? tab_row(ev_b) : ue_b;
+        if (u + G < nunits) d_a = load_data(ut_a, ue_a);
         if (u + 2 * G < nunits) {
-            ut_b = utab[u + 2 * G];
-            if (ELEM) ue_b = etab[u + 2 * G];
+            if (LT) {
+                tv_b = tab_fetch(utab, u + 2 * G);
+                if (ELEM) ev_b = tab_fetch(etab, u + 2 * G);
+            } else {
+                ut_b = utab[u + 2 * G];
+                if (ELEM) ue_b = etab[u + 2 * G];
+            }
         }
         const int i = ut.x, t0 = ut.y, nu = ut.z, q = ut.w >> 9, ns = ut.w & 511;
         const EPre pre = d.pre;
@@ -1856,7 +1881,9 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(RST ? 5 : 6)
         if (ELEM && j <= TM) nrp = E.rpA[min(ix * TM + j, E.m)];
         if (ELEM && !(ablate & 4)) npre = epre_load(E, uex, true);
     };
+    constexpr bool LT = !RST;  // lane-fetched tables (measured: a loss for the few, long RST units)
     int4 ut_c = make_int4(0, 0, 0, 0), ue_c = ut_c, ut_n = ut_c, ue_n = ut_c;
+    int tv_n = 0, ev_n = 0;  // tables of the unit two ahead (lanes 0..3, tab_fetch)
     u32 code_n = 0;
     if ((int)blockIdx.x < nunits) {
         ut_c = utab[blockIdx.x];
@@ -1865,17 +1892,27 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(RST ? 5 : 6)
         issue(blockIdx.x, ut_c, ue_c, code_n);
     }
     if ((int)blockIdx.x + G < nunits) {
-        ut_n = utab[blockIdx.x + G];
-        if (ELEM) ue_n = etab[blockIdx.x + G];
+        if (LT) {
+            tv_n = tab_fetch(utab, blockIdx.x + G);
+            if (ELEM) ev_n = tab_fetch(etab, blockIdx.x + G);
+        } else {
+            ut_n = utab[blockIdx.x + G];
+            if (ELEM) ue_n = etab[blockIdx.x + G];
+        }
     }
     for (int u = blockIdx.x; u < nunits; u += G) {
         PROF_MARK(7);
         const int4 ut = ut_c, ue = ue_c;
-        ut_c = ut_n;
-        ue_c = ue_n;
+        ut_c = LT ? tab_row(tv_n) : ut_n;
+        if (ELEM) ue_c = LT ? tab_row(ev_n) : ue_n;
         if (u + 2 * G < nunits) {
-            ut_n = utab[u + 2 * G];
-            if (ELEM) ue_n = etab[u + 2 * G];
+            if (LT) {
+                tv_n = tab_fetch(utab, u + 2 * G);
+                if (ELEM) ev_n = tab_fetch(etab, u + 2 * G);
+            } else {
+                ut_n = utab[u + 2 * G];
+                if (ELEM) ue_n = etab[u + 2 * G];
+            }
         }
         const bool more = u + G < nunits;
         const int i = ut.x, t0 = ut.y, nu = ut.z, q = ut.w >> 9, ns = ut.w & 511;
