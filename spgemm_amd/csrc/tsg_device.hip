@@ -70,9 +70,24 @@ template <class T> __device__ __forceinline__ T wave_sum(T x) {
     return x;
 }
 
+// 32-bit inclusive wave scan on DPP lane moves (no LDS round trips): row_shr
+// 1/2/4/8 scans each 16-lane row, row_bcast:15 / :31 carry the row totals.
+// Needs the whole wave active.
+__device__ __forceinline__ int wave_incl_scan_dpp(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+    return v;
+}
+
 // exclusive scan across the 256-thread workgroup; red needs WAVES entries
 template <class T> __device__ __forceinline__ T block_excl_scan(T x, T *total, T *red) {
-    T inc = wave_incl_scan(x);
+    T inc;
+    if constexpr (sizeof(T) == 4) inc = (T)wave_incl_scan_dpp((int)x);
+    else inc = wave_incl_scan(x);
     if (lane_id() == 63) red[wave_id()] = inc;
     __syncthreads();
     T off = 0, tot = 0;
@@ -1714,13 +1729,18 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(6))) void k_
                     dst[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
             }
         }
+        // wave totals per 32-bit half (no carries cross the 16-bit fields):
+        // row r's count is field r & 1 of half r >> 1
+        u32 hs[2 * NP];
 #pragma unroll
-        for (int g = 0; g < NP; ++g) pk[g] = wave_sum(pk[g]);
+        for (int h = 0; h < 2 * NP; ++h)
+            hs[h] = (u32)__builtin_amdgcn_readlane(
+                wave_incl_scan_dpp((int)(u32)(pk[h >> 1] >> (32 * (h & 1)))), 63);
         if (lane_id() < TM) {  // lane r adds row r's count of this wave
-            u64 v = pk[0];
+            u32 v = hs[0];
 #pragma unroll
-            for (int g = 1; g < NP; ++g) v = ((lane_id() >> 2) == g) ? pk[g] : v;
-            const int c = (int)((v >> (16 * (lane_id() & 3))) & 0xffffu);
+            for (int h = 1; h < 2 * NP; ++h) v = ((lane_id() >> 1) == h) ? hs[h] : v;
+            const int c = (int)((v >> (16 * (lane_id() & 1))) & 0xffffu);
             if (c) atomicAdd(&s_rc[lane_id()], c);
         }
         u64 bm = 0;
