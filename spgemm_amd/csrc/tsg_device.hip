@@ -19,6 +19,7 @@
 // per chunk with a load-balanced expansion across the 256-thread workgroup.
 #include "tsg_internal.h"
 
+#include <climits>
 #include <cstdio>
 #include <cstdlib>
 #include <type_traits>
@@ -44,50 +45,65 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// 32-bit inclusive wave scans on DPP lane moves (no LDS permute round trips):
+// row_shr 1/2/4/8 scan each 16-lane row, row_bcast:15 / :31 carry the row
+// totals into rows 1, 3 and 2, 3.  id = the operator's identity (what lanes
+// without a source read).  The whole wave must be active.
+template <int CTRL, int RM> __device__ __forceinline__ int dpp_mov(int id, int v) {
+    return __builtin_amdgcn_update_dpp(id, v, CTRL, RM, 0xf, false);
+}
+template <class Op> __device__ __forceinline__ int wave_incl_dpp(int v, int id, Op op) {
+    v = op(v, dpp_mov<0x111, 0xf>(id, v));  // row_shr:1
+    v = op(v, dpp_mov<0x112, 0xf>(id, v));  // row_shr:2
+    v = op(v, dpp_mov<0x114, 0xf>(id, v));  // row_shr:4
+    v = op(v, dpp_mov<0x118, 0xf>(id, v));  // row_shr:8
+    v = op(v, dpp_mov<0x142, 0xa>(id, v));  // row_bcast:15
+    v = op(v, dpp_mov<0x143, 0xc>(id, v));  // row_bcast:31
+    return v;
+}
+struct OpAdd {
+    __device__ int operator()(int a, int b) const { return a + b; }
+};
+struct OpMin {
+    __device__ int operator()(int a, int b) const { return min(a, b); }
+};
+struct OpMax {
+    __device__ int operator()(int a, int b) const { return max(a, b); }
+};
+__device__ __forceinline__ int wave_incl_scan_dpp(int v) { return wave_incl_dpp(v, 0, OpAdd{}); }
+
 template <class T> __device__ __forceinline__ T wave_incl_scan(T x) {
-    const int l = lane_id();
+    if constexpr (sizeof(T) == 4) {
+        return (T)wave_incl_scan_dpp((int)x);
+    } else {
+        const int l = lane_id();
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        T y = __shfl_up(x, d, 64);
-        if (l >= d) x += y;
+        for (int d = 1; d < 64; d <<= 1) {
+            T y = __shfl_up(x, d, 64);
+            if (l >= d) x += y;
+        }
+        return x;
     }
-    return x;
 }
 
-__device__ __forceinline__ int wave_incl_max(int x) {
-    const int l = lane_id();
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        int y = __shfl_up(x, d, 64);
-        if (l >= d) x = max(x, y);
-    }
-    return x;
-}
+__device__ __forceinline__ int wave_incl_max(int x) { return wave_incl_dpp(x, INT_MIN, OpMax{}); }
+
+// the value of lane 63 (a scan's total), as a wave-uniform value
+__device__ __forceinline__ int wave_last(int x) { return __builtin_amdgcn_readlane(x, 63); }
 
 template <class T> __device__ __forceinline__ T wave_sum(T x) {
+    if constexpr (sizeof(T) == 4) {
+        return (T)wave_last(wave_incl_scan_dpp((int)x));
+    } else {
 #pragma unroll
-    for (int d = 32; d > 0; d >>= 1) x += __shfl_xor(x, d, 64);
-    return x;
-}
-
-// 32-bit inclusive wave scan on DPP lane moves (no LDS round trips): row_shr
-// 1/2/4/8 scans each 16-lane row, row_bcast:15 / :31 carry the row totals.
-// Needs the whole wave active.
-__device__ __forceinline__ int wave_incl_scan_dpp(int v) {
-    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);  // row_shr:1
-    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);  // row_shr:2
-    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);  // row_shr:4
-    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);  // row_shr:8
-    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
-    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
-    return v;
+        for (int d = 32; d > 0; d >>= 1) x += __shfl_xor(x, d, 64);
+        return x;
+    }
 }
 
 // exclusive scan across the 256-thread workgroup; red needs WAVES entries
 template <class T> __device__ __forceinline__ T block_excl_scan(T x, T *total, T *red) {
-    T inc;
-    if constexpr (sizeof(T) == 4) inc = (T)wave_incl_scan_dpp((int)x);
-    else inc = wave_incl_scan(x);
+    const T inc = wave_incl_scan(x);
     if (lane_id() == 63) red[wave_id()] = inc;
     __syncthreads();
     T off = 0, tot = 0;
@@ -104,11 +120,8 @@ template <class T> __device__ __forceinline__ T block_excl_scan(T x, T *total, T
 
 // workgroup min and max of x (red: 2*WAVES ints)
 __device__ __forceinline__ void block_minmax(int &mn, int &mx, int *red) {
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) {
-        mn = min(mn, __shfl_xor(mn, d, 64));
-        mx = max(mx, __shfl_xor(mx, d, 64));
-    }
+    mn = wave_last(wave_incl_dpp(mn, INT_MAX, OpMin{}));
+    mx = wave_last(wave_incl_dpp(mx, INT_MIN, OpMax{}));
     if (lane_id() == 0) {
         red[wave_id()] = mn;
         red[WAVES + wave_id()] = mx;
@@ -296,7 +309,7 @@ __global__ __launch_bounds__(WG) void k_sort_classify(const int *seg, int nseg, 
             const int leader = __ffsll((long long)msk) - 1;
             int pos0 = 0;
             if (lane == leader) pos0 = atomicAdd(&counts[t], __popcll(msk));
-            pos0 = __shfl(pos0, leader, 64);
+            pos0 = __builtin_amdgcn_readlane(pos0, leader);
             if (tier == t) lists[(long)t * nseg + pos0 + __popcll(msk & below)] = (int)i;
         }
     }
@@ -647,8 +660,8 @@ __global__ __launch_bounds__(WG) void k_c2t_fill(const u64 *keys, const int *seg
             const bool gs = in && (nt || key_lr(kp) != lr);
             int u = carry_u + wave_incl_scan(nt ? 1 : 0);
             int f = max(wave_incl_max(nt ? p : -1), carry_first);
-            carry_u = __shfl(u, 63, 64);
-            carry_first = __shfl(f, 63, 64);
+            carry_u = wave_last(u);
+            carry_first = wave_last(f);
             if (!in) continue;
             const int trm = tbase + u;
             if (MODE == FILL_B_STRUCT) {
@@ -2574,7 +2587,7 @@ __global__ __launch_bounds__(WG) void k_t2c_fill(const int *Cptr, const int *Cco
                 int c = nx - st;
                 int inc = wave_incl_scan(c);
                 int dst0 = carry[r] + inc - c;
-                carry[r] += __shfl(inc, 63, 64);
+                carry[r] += wave_last(inc);
                 if (r < rowlen && c > 0) {
                     const int R = i * TM + r;
                     int d = rowptr[R] + dst0;
