@@ -250,6 +250,9 @@ def main():
     # SURVEY §8d algorithmic bytes (src/external/cusparse/main.cu:205-208), this rank's share
     b_alg = 4.0 * (mblk + 1) + 12.0 * len(ciblk) + 4.0 * (mb + 1) + 12.0 * len(cib) + 4.0 * (mblk + 1) + 12.0 * c.nnz
     achieved_pipe = b_alg / (dev_ms * 1e-3) / 1e9
+    # context only (never the graded figure): + one fp64 value and one u16 local column
+    # per intermediate product of this rank (SURVEY §8d B_stream)
+    b_stream = b_alg + 10.0 * nnzcub_rows(rpblk, ciblk, rpb, 0, mblk)
     # dominant kernel: step 3 (reads the CSR operands, writes the CSR result = B_alg's
     # terms), timed with HIP events around its launch on the call's stream
     k3_ms = med["t_step3_kernel_ms"]
@@ -280,7 +283,9 @@ def main():
                          "algorithmic_bytes": int(b_alg), "kernel_ms": round(k3_ms, 4),
                          "pipeline": {"achieved": round(achieved_pipe, 2),
                                       "frac": round(achieved_pipe / HBM_PEAK_GBS, 5),
-                                      "device_ms": round(dev_ms, 4)}},
+                                      "device_ms": round(dev_ms, 4)},
+                         "stream_bytes": int(b_stream),
+                         "stream_achieved": round(b_stream / (k3_ms * 1e-3) / 1e9, 2)},
             "stage_ms": {k: round(med[k], 4) for k in ("t_csr2tile_ms", "t_step1_ms", "t_step2_ms",
                                                         "t_step3_ms", "t_step3_kernel_ms", "t_tile2csr_ms", "t_malloc_ms",
                                                         "t_kern_ms", "t_e2e_ms")},

@@ -999,10 +999,16 @@ __device__ __forceinline__ void bm_count_emit(const u32 *bm, int words, int wpt,
 //   PASS 0 with bm_store: the unit's bitmask is also stored (full window, vector
 //   stores), and PASS 2 then emits from it instead of re-enumerating the tile
 //   products (PASS 1).
-template <int PASS>
+// EL (CSR path, sparse tiles): the unit walks the ELEMENT products of CSR A's
+// rows [16i, 16i+16) and CSR B's rows (Aptr = A row pointer, mA its row count,
+// Bcol = B's element columns, bit = column / 16), so C gets only the tiles
+// holding a nonzero -- for web-like matrices fewer products than the
+// tile-pattern product, and no empty C tiles for steps 2 and 3.
+template <int PASS, bool EL = false>
 __global__ __launch_bounds__(WG) void k_step1(const int *Aptr, const int *Acol, const int *Bptr, const int *Bcol,
                                               int tilemA, int tilenB, int nwin, int win, int *unit_cnt,
-                                              const int *unit_off, int *Ccol, u64 *prod_total, u32 *bm_store) {
+                                              const int *unit_off, int *Ccol, u64 *prod_total, u32 *bm_store,
+                                              int mA = 0) {
     __shared__ __align__(16) u32 bm[S1_MAXWORDS];
     __shared__ ProdLds L;
     __shared__ int red[WAVES];
@@ -1012,7 +1018,7 @@ __global__ __launch_bounds__(WG) void k_step1(const int *Aptr, const int *Acol, 
     long my_items = 0;
     for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
         const int i = u / nwin, w = u - i * nwin;
-        const int a0 = Aptr[i], a1 = Aptr[i + 1];
+        const int a0 = EL ? Aptr[min(i * 16, mA)] : Aptr[i], a1 = EL ? Aptr[min(i * 16 + 16, mA)] : Aptr[i + 1];
         if (a0 == a1) {
             if (PASS == 0 && threadIdx.x == 0) unit_cnt[u] = 0;
             continue;
@@ -1039,9 +1045,10 @@ __global__ __launch_bounds__(WG) void k_step1(const int *Aptr, const int *Acol, 
             const int wlo = 0, whi = words - 1;
             for (int q = wlo + threadIdx.x; q <= whi; q += WG) bm[q] = 0u;
             __syncthreads();
-            long it = for_each_product(a0, a1, Acol, Bptr, Bcol, clo, chi, nwin > 1, L, [&](int a, int b) {
+            long it = for_each_product(a0, a1, Acol, Bptr, Bcol, EL ? clo * 16 : clo, EL ? chi * 16 + 15 : chi,
+                                       nwin > 1, L, [&](int a, int b) {
                 (void)a;
-                int c = Bcol[b] - clo;
+                int c = (EL ? Bcol[b] >> 4 : Bcol[b]) - clo;
                 atomicOr(&bm[c >> 5], 1u << (c & 31));
             });
             if (PASS == 0) my_items += (threadIdx.x == 0) ? it : 0;
@@ -2151,9 +2158,12 @@ static int g_ablate = -1;
 
 // Step 1 (C tile structure = tile-pattern product of A's and B's row-major tile
 // structures; includes tiles whose element product is empty, as the reference).
-// Works for any tile sizes: only tile_ptr / tile_columnidx are read.
+// Works for any tile sizes: only tile_ptr / tile_columnidx are read.  With CSR
+// operands Ael/Bel (16x16): the element-level structure instead (non-empty C
+// tiles only; the CSR path, whose C tiles are internal).
 int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_dev_tiles &C,
-              long long *tile_products_out, hipStream_t s) {
+              long long *tile_products_out, hipStream_t s, const tsg_dev_csr *Ael, const tsg_dev_csr *Bel) {
+    const bool el = Ael && Bel;  // element-level structure (16x16 tiles, CSR operands)
     const int tilemA = A.tilem, tilenB = B.tilen;
     int win, nwin;
     window_for(tilenB, &win, &nwin);
@@ -2173,15 +2183,22 @@ int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_d
     // outweigh a reread of the window's words, i.e. not for banded matrices)
     u32 *bmst = nullptr;
     const size_t bm_bytes = (size_t)nunits1 * (win / 8);
-    const double est_products = (double)A.numtile * ((double)B.numtile / (double)(B.tilem > 0 ? B.tilem : 1));
+    const double est_products =
+        el ? (double)Ael->nnz * ((double)Bel->nnz / (double)(Bel->m > 0 ? Bel->m : 1))
+           : (double)A.numtile * ((double)B.numtile / (double)(B.tilem > 0 ? B.tilem : 1));
     const bool store = bm_bytes <= (4ull << 30) && est_products >= (double)nunits1 * (win / 32) / 8.0;
     if (store && !(g_ablate & 256) && cx.get(&bmst, bm_bytes / 4) != TSG_OK) {
         bmst = nullptr;
         (void)hipGetLastError();
     }
-    if (tilemA > 0)
-        k_step1<0><<<g1, WG, 0, s>>>(A.tile_ptr, A.tile_columnidx, B.tile_ptr, B.tile_columnidx, tilemA, tilenB,
-                                     nwin, win, ucnt, nullptr, nullptr, prod, bmst);
+    if (tilemA > 0) {
+        if (el)
+            k_step1<0, true><<<g1, WG, 0, s>>>(Ael->rowpointer, Ael->columnindex, Bel->rowpointer, Bel->columnindex,
+                                               tilemA, tilenB, nwin, win, ucnt, nullptr, nullptr, prod, bmst, Ael->m);
+        else
+            k_step1<0><<<g1, WG, 0, s>>>(A.tile_ptr, A.tile_columnidx, B.tile_ptr, B.tile_columnidx, tilemA, tilenB,
+                                         nwin, win, ucnt, nullptr, nullptr, prod, bmst);
+    }
     TSG_HIP(hipGetLastError());
     long long numblk64 = 0;
     TSG_TRY(scan_exclusive_i32_total(cx, ucnt, nunits1 + 1, s, &numblk64));  // overflow: > INT_MAX C tiles
@@ -2197,6 +2214,10 @@ int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_d
         if (bmst)
             k_step1<2><<<g1, WG, 0, s>>>(A.tile_ptr, A.tile_columnidx, B.tile_ptr, B.tile_columnidx, tilemA, tilenB,
                                          nwin, win, nullptr, ucnt, C.tile_columnidx, nullptr, bmst);
+        else if (el)
+            k_step1<1, true><<<g1, WG, 0, s>>>(Ael->rowpointer, Ael->columnindex, Bel->rowpointer, Bel->columnindex,
+                                               tilemA, tilenB, nwin, win, nullptr, ucnt, C.tile_columnidx, nullptr,
+                                               nullptr, Ael->m);
         else
             k_step1<1><<<g1, WG, 0, s>>>(A.tile_ptr, A.tile_columnidx, B.tile_ptr, B.tile_columnidx, tilemA, tilenB,
                                          nwin, win, nullptr, ucnt, C.tile_columnidx, nullptr, nullptr);
@@ -2229,8 +2250,10 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     C.tilem = tilemA; C.tilen = tilenB;
     if (ev) TSG_HIP(hipEventRecord(ev[0], s));
     // ---- step 1 ----
+    // CSR path with element streaming: C's structure at element level (no empty tiles)
+    const bool s1elem = csr_out && s2elem && s3elem;
     long long tile_products = 0;
-    TSG_TRY(dev_step1(cx, A, B, C, &tile_products, s));
+    TSG_TRY(dev_step1(cx, A, B, C, &tile_products, s, s1elem ? Acsr : nullptr, s1elem ? Bcsr : nullptr));
     const int numblkC = C.numtile;
     const size_t nb1 = (size_t)numblkC + 1;
     if (ev) TSG_HIP(hipEventRecord(ev[1], s));

@@ -95,7 +95,8 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
                    bool step2_elem = false);
 // step 1 alone: C tile structure (tile_ptr, tile_columnidx, numtile) of any tile size
 int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_dev_tiles &C,
-              long long *tile_products, hipStream_t s);
+              long long *tile_products, hipStream_t s, const tsg_dev_csr *Ael = nullptr,
+              const tsg_dev_csr *Bel = nullptr);
 // C payload for a step-1 structure C (tile_m set) from the non-empty tiles Cne of C's CSR
 int dev_retile_c(Context &cx, const tsg_dev_tiles &Cne, tsg_dev_tiles &C, hipStream_t s);
 // tile_ptr + tile_columnidx of a CSR's tiling (tr x tc tiles), no payload
