@@ -781,16 +781,18 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
     if (bsorted) {
         // tile STRUCTURE of A and B from CSR; denser tiles add the row masks that
         // step 2's tile-level ORs read (no sort-based csr2tile on this path)
-        TSG_TRY(dev_tile_structure(cx, *A, tm, tn, tA, s));
+        // element streaming throughout (sparse tiles) builds C's structure from the
+        // CSR operands: then A's and B's tile counts are all that is needed
         const char *md = getenv("TSG_STEP2_MODE");
-        if (md && !strcmp(md, "elem")) s2elem = true;
-        else if (md && !strcmp(md, "tile")) s2elem = false;
-        else s2elem = (double)A->nnz < kStep2ElemMaxTileDensity * (double)tA.numtile;
+        const int forced = !md ? -1 : !strcmp(md, "elem") ? 1 : !strcmp(md, "tile") ? 0 : -1;
+        const double skip = forced == 1 ? 1e300 : forced == 0 ? 0.0 : kStep2ElemMaxTileDensity;
+        TSG_TRY(dev_tile_structure(cx, *A, tm, tn, tA, s, skip));
+        s2elem = forced >= 0 ? forced == 1 : (double)A->nnz < kStep2ElemMaxTileDensity * (double)tA.numtile;
         if (alias) {
             tB = tA;
             b_is_a = true;
         } else {
-            TSG_TRY(dev_tile_structure(cx, *B, tn, tm, tB, s));
+            TSG_TRY(dev_tile_structure(cx, *B, tn, tm, tB, s, s2elem ? 1e300 : 0.0));
         }
         if (!s2elem) {
             TSG_TRY(dev_tile_masks(cx, *A, tA, &tA.mask, s));

@@ -1160,7 +1160,8 @@ int dev_tile_masks(Context &cx, const tsg_dev_csr &M, tsg_dev_tiles &t, u16 **ma
     return TSG_OK;
 }
 
-int dev_tile_structure(Context &cx, const tsg_dev_csr &M, int tr, int tc, tsg_dev_tiles &out, hipStream_t s) {
+int dev_tile_structure(Context &cx, const tsg_dev_csr &M, int tr, int tc, tsg_dev_tiles &out, hipStream_t s,
+                       double skip_emit_density) {
     out = tsg_dev_tiles{};
     out.m = M.m; out.n = M.n; out.nnz = M.nnz;
     out.tile_m = tr; out.tile_n = tc;
@@ -1182,6 +1183,10 @@ int dev_tile_structure(Context &cx, const tsg_dev_csr &M, int tr, int tc, tsg_de
     TSG_TRY(scan_exclusive_i32(cx, ucnt, nunits + 1, s));
     k_rows_from_units<<<grid_for(out.tilem + 1, WG, 4096), WG, 0, s>>>(ucnt, out.tilem, nwin, out.tile_ptr);
     TSG_TRY(read_i32(cx, out.tile_ptr + out.tilem, &out.numtile, s));
+    if ((double)M.nnz < skip_emit_density * (double)out.numtile) {  // caller needs the counts only
+        cx.put(ucnt);
+        return TSG_OK;
+    }
     TSG_TRY(cx.get(&out.tile_columnidx, (size_t)out.numtile + 1));
     if (out.tilem > 0)
         k_tstruct<1><<<g, WG, 0, s>>>(M.rowpointer, M.columnindex, M.m, tr, tc, out.tilem, out.tilen, nwin, win,
@@ -2252,6 +2257,8 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     // ---- step 1 ----
     // CSR path with element streaming: C's structure at element level (no empty tiles)
     const bool s1elem = csr_out && s2elem && s3elem;
+    if (!s1elem && (!A.tile_columnidx || !B.tile_columnidx) && A.numtile > 0 && B.numtile > 0)
+        return TSG_ERR_INVALID;  // tile-level step 1 needs both tile structures
     long long tile_products = 0;
     TSG_TRY(dev_step1(cx, A, B, C, &tile_products, s, s1elem ? Acsr : nullptr, s1elem ? Bcsr : nullptr));
     const int numblkC = C.numtile;

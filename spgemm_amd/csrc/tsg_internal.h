@@ -99,8 +99,10 @@ int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_d
               const tsg_dev_csr *Bel = nullptr);
 // C payload for a step-1 structure C (tile_m set) from the non-empty tiles Cne of C's CSR
 int dev_retile_c(Context &cx, const tsg_dev_tiles &Cne, tsg_dev_tiles &C, hipStream_t s);
-// tile_ptr + tile_columnidx of a CSR's tiling (tr x tc tiles), no payload
-int dev_tile_structure(Context &cx, const tsg_dev_csr &M, int tr, int tc, tsg_dev_tiles &out, hipStream_t s);
+// tile_ptr + tile_columnidx of a CSR's tiling (tr x tc tiles), no payload;
+// tile_columnidx is left null when M.nnz < skip_emit_density * numtile
+int dev_tile_structure(Context &cx, const tsg_dev_csr &M, int tr, int tc, tsg_dev_tiles &out, hipStream_t s,
+                       double skip_emit_density = 0);
 // row masks of a tiling (structure in t) straight from CSR, into a new zeroed array
 int dev_tile_masks(Context &cx, const tsg_dev_csr &M, tsg_dev_tiles &t, uint16_t **mask_out, hipStream_t s);
 // whether every CSR row is column-sorted (synchronous)
