@@ -7,9 +7,16 @@ step 3 + GPU tile2csr (SURVEY.md §8d t_e2e).  Inputs are resident in HBM
 (src/tilespgemm-cuda.h:2808).
 
   python bench.py                       # N=1, webbase-1M synthetic stand-in
-  python bench.py --gpus N ...          # under torch.distributed.run: A split by
-                                        # tile-row blocks of equal work, B
-                                        # replicated, C gathered to rank 0 (RCCL)
+  python bench.py --gpus N ...          # under torch.distributed.run, weak scaling
+                                        # (default): rank r computes row block r of
+                                        # [A; A; ...; A] * B (one full A per rank, B
+                                        # replicated, C stays distributed: no
+                                        # data-path collective)
+  python bench.py --gpus N --scaling strong
+                                        # the fixed product A*B: A split by tile-row
+                                        # blocks of equal work, B replicated, C row
+                                        # blocks gathered to rank 0 over RCCL
+                                        # (inside the timed region)
 Rank 0 prints ONE JSON line.
 """
 import argparse
@@ -146,6 +153,10 @@ def main():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N>1 (nccl = RCCL over xGMI; gloo = host-staged "
                          "rehearsal of the multi-rank path, e.g. several ranks on one GPU)")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="N>1: weak = every rank owns one A-sized row block of the stacked "
+                         "product (fixed work per GPU, no collective on the data path); strong = "
+                         "A's tile rows partitioned by work + RCCL gather of C to rank 0")
     args = ap.parse_args()
 
     import torch
@@ -188,8 +199,10 @@ def main():
     if rows is not None and rows < m:
         m, rp, ci, vv = rows, rp[:rows + 1].copy(), ci[:rp[rows]].copy(), vv[:rp[rows]].copy()
         name = f"{name} rows[0,{rows}) of {full_m}"
-    nnzcub_total = nnzcub_rows(rp, ci, rpb, 0, m)
-    if world > 1:
+    nnzcub_rank = nnzcub_rows(rp, ci, rpb, 0, m)
+    weak = world > 1 and args.scaling == "weak"
+    nnzcub_total = nnzcub_rank * world if weak else nnzcub_rank
+    if world > 1 and not weak:
         work = tdist.tile_row_work(rp, ci, rpb, m, tm)
         parts = tdist.partition_tile_rows(work, world)
         t0r, t1r = parts[rank]
@@ -197,7 +210,7 @@ def main():
     else:
         mblk, rpblk, ciblk, vvblk = m, rp, ci, vv
     dA = DeviceCSR.from_host(mblk, n, rpblk, ciblk, vvblk)
-    dB = dA if (not aat and world == 1 and m == full_m) else DeviceCSR.from_host(mb, nb, rpb, cib, vvb)
+    dB = dA if (not aat and (world == 1 or weak) and m == full_m) else DeviceCSR.from_host(mb, nb, rpb, cib, vvb)
     ctx = Context(dev_id)
     torch.cuda.synchronize()
 
@@ -207,7 +220,7 @@ def main():
     def one_step():
         ctx.reset()
         c, st = ctx.spgemm(dA, dB, tm, tm)  # returns with C complete on the device
-        if world > 1:
+        if world > 1 and not weak:
             g0 = time.perf_counter()
             cblk = ctx.view_torch(c)  # zero-copy views of the context-owned C block
             if host_coll:
@@ -260,6 +273,17 @@ def main():
     workload = (f"{name} C=A{'*A^T' if aat else '^2'} fp64, {tm}x{tm} tiles, "
                 "csr2tile+steps1-3+tile2csr (device CSR in -> device CSR out)")
     traffic, traffic_src = pmc_traffic("k_step3", workload)
+    chk = None
+    if args.check and (world == 1 or weak):
+        g_rp, g_ci, g_vv = ctx.to_host(c)[2:]
+        chk = [float(len(g_ci)), float(g_rp.astype(np.int64).sum()), float(g_ci.astype(np.int64).sum()),
+               float(g_vv.sum())]
+        if weak:  # every rank's block of the stacked product is the same C
+            t = torch.tensor(chk, dtype=torch.float64, device=red_dev)
+            lo, hi = t.clone(), t.clone()
+            dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+            dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+            assert torch.equal(lo, hi), "weak scaling: rank C blocks differ"
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -270,12 +294,14 @@ def main():
         out = {
             "metric": METRIC, "value": round(gflops, 3), "unit": "GFLOPS", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True, "scaling": "strong" if world > 1 else "weak",
+            "higher_is_better": True, "scaling": args.scaling,
             "vs_baseline": None, "dtype": "f64", "data": data_kind,
             "config": {"workload": workload,
-                       "m": m, "nnzA": int(len(ci)), "nnzCub": nnzcub_total, "nnzC": nnzC,
+                       "m": m * world if weak else m, "m_per_rank": m if weak else None,
+                       "nnzA": int(len(ci)) * (world if weak else 1), "nnzCub": nnzcub_total, "nnzC": nnzC,
                        "numtileA": int(med["numtileA"]), "numblkC": int(med["numblkC"]),
-                       "parallelism": f"row-block{world}" if world > 1 else "single"},
+                       "parallelism": (f"stacked-row-block{world} (B replicated, C distributed)" if weak else
+                                       f"row-block{world} + RCCL gather" if world > 1 else "single")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "traffic_source": traffic_src,
@@ -295,11 +321,12 @@ def main():
             "cpu_baseline": cpu,
         }
         if args.check:
-            if world > 1:
-                g_rp, g_ci, g_vv = (x.cpu().numpy() for x in gathered[0])
+            if chk is not None:
+                out["check"] = {"nnz": int(chk[0]), "rowptr_sum": int(chk[1]), "col_sum": int(chk[2]),
+                                "val_sum": chk[3]}
             else:
-                g_rp, g_ci, g_vv = ctx.to_host(c)[2:]
-            out["check"] = {"nnz": int(len(g_ci)), "rowptr_sum": int(g_rp.astype(np.int64).sum()),
+                g_rp, g_ci, g_vv = (x.cpu().numpy() for x in gathered[0])
+                out["check"] = {"nnz": int(len(g_ci)), "rowptr_sum": int(g_rp.astype(np.int64).sum()),
                             "col_sum": int(g_ci.astype(np.int64).sum()), "val_sum": float(g_vv.sum())}
         print(json.dumps(out), flush=True)
     ctx.close()

@@ -896,18 +896,27 @@ struct ProdLds {
     int red[WAVES];
 };
 
+// ebnd (optional): per A entry its B row's [start, end), one load instead of
+// the colA -> bptr chain
 template <class F>
 __device__ __forceinline__ long for_each_product(int a0, int a1, const int *colA, const int *bptr,
                                                  const int *bcol, int clo, int chi, bool narrow,
-                                                 ProdLds &L, F &&f) {
+                                                 ProdLds &L, F &&f, const int2 *ebnd = nullptr) {
     long items = 0;
     for (int ab = a0; ab < a1; ab += WG) {
         const int a = ab + threadIdx.x;
         int bs = 0, len = 0;
         if (a < a1) {
-            int k = colA[a];
-            bs = bptr[k];
-            int be = bptr[k + 1];
+            int be;
+            if (ebnd) {
+                const int2 e = ebnd[a];
+                bs = e.x;
+                be = e.y;
+            } else {
+                int k = colA[a];
+                bs = bptr[k];
+                be = bptr[k + 1];
+            }
             if (narrow) {
                 bs = lower_bound_dev(bcol, bs, be, clo);
                 be = lower_bound_dev(bcol, bs, be, chi + 1);
@@ -986,6 +995,7 @@ __device__ __forceinline__ void bm_count_emit(const u32 *bm, int words, int wpt,
     } else {
         int tot;
         int off = block_excl_scan(cnt, &tot, red) + off0;
+        if (unit_cnt && threadIdx.x == 0) unit_cnt[u] = tot;  // emit into a unit buffer
         for (int q = 0; q < nw; ++q) {
             u32 x = wv[q];
             while (x) {
@@ -1004,11 +1014,16 @@ __device__ __forceinline__ void bm_count_emit(const u32 *bm, int words, int wpt,
 // Bcol = B's element columns, bit = column / 16), so C gets only the tiles
 // holding a nonzero -- for web-like matrices fewer products than the
 // tile-pattern product, and no empty C tiles for steps 2 and 3.
+//   PASS 0 with ubuf (EL): count AND emit the unit's sorted columns into its
+//   slot ubuf[ubuf_off[u]..] (capacity = min(products, window)); k_step1_gather
+//   then compacts the slots into tile_columnidx -- one element-product
+//   enumeration instead of two.
 template <int PASS, bool EL = false>
 __global__ __launch_bounds__(WG) void k_step1(const int *Aptr, const int *Acol, const int *Bptr, const int *Bcol,
                                               int tilemA, int tilenB, int nwin, int win, int *unit_cnt,
                                               const int *unit_off, int *Ccol, u64 *prod_total, u32 *bm_store,
-                                              int mA = 0) {
+                                              int mA = 0, const int2 *ebnd = nullptr, int *ubuf = nullptr,
+                                              const long long *ubuf_off = nullptr) {
     __shared__ __align__(16) u32 bm[S1_MAXWORDS];
     __shared__ ProdLds L;
     __shared__ int red[WAVES];
@@ -1050,7 +1065,7 @@ __global__ __launch_bounds__(WG) void k_step1(const int *Aptr, const int *Acol, 
                 (void)a;
                 int c = (EL ? Bcol[b] >> 4 : Bcol[b]) - clo;
                 atomicOr(&bm[c >> 5], 1u << (c & 31));
-            });
+            }, EL ? ebnd : nullptr);
             if (PASS == 0) my_items += (threadIdx.x == 0) ? it : 0;
             if (PASS == 0 && bm_store) {
                 u32 wv[8];
@@ -1062,11 +1077,44 @@ __global__ __launch_bounds__(WG) void k_step1(const int *Aptr, const int *Acol, 
                 if (wpt < 4)
                     for (int q = 0; q < wpt; ++q) dst[q] = wv[q];
             }
-            bm_count_emit<PASS>(bm, words, wpt, wlo, whi, clo, red, unit_cnt, u, PASS == 1 ? unit_off[u] : 0, Ccol);
+            if (PASS == 0 && ubuf)
+                bm_count_emit<1>(bm, words, wpt, wlo, whi, clo, red, unit_cnt, u, 0, ubuf + ubuf_off[u]);
+            else
+                bm_count_emit<PASS>(bm, words, wpt, wlo, whi, clo, red, PASS == 1 ? nullptr : unit_cnt, u,
+                                    PASS == 1 ? unit_off[u] : 0, Ccol);
             __syncthreads();
         }
     }
     if (PASS == 0 && threadIdx.x == 0 && my_items) atomicAdd(prod_total, (u64)my_items);
+}
+
+// EL step 1 unit-buffer capacities: wave per A tile row, its element products
+// P (sum of its entries' B row lengths); every window of the row gets
+// min(P, window width) slots.
+__global__ __launch_bounds__(WG) void k_step1_cap(const int *Aptr, int mA, const int2 *ebnd, int tilemA, int nwin,
+                                                  int win, int tilenB, long long *cap) {
+    const int lane = threadIdx.x & 63;
+    for (long i = ((long)blockIdx.x * WG + threadIdx.x) >> 6; i < tilemA; i += ((long)gridDim.x * WG) >> 6) {
+        const int a0 = Aptr[min((int)i * 16, mA)], a1 = Aptr[min((int)i * 16 + 16, mA)];
+        long long p = 0;
+        for (int a = a0 + lane; a < a1; a += 64) {
+            const int2 e = ebnd[a];
+            p += e.y - e.x;
+        }
+        p = wave_sum(p);
+        for (int w = lane; w < nwin; w += 64)
+            cap[i * nwin + w] = min(p, (long long)min(win, tilenB - w * win));
+    }
+}
+
+// compact the EL step-1 unit buffers into tile_columnidx (workgroup per unit)
+__global__ __launch_bounds__(WG) void k_step1_gather(const int *ubuf, const long long *ubuf_off, const int *unit_off,
+                                                     long nunits, int *Ccol) {
+    for (long u = blockIdx.x; u < nunits; u += gridDim.x) {
+        const int o = unit_off[u], n = unit_off[u + 1] - o;
+        const int *src = ubuf + ubuf_off[u];
+        for (int q = threadIdx.x; q < n; q += WG) Ccol[o + q] = src[q];
+    }
 }
 
 __global__ void k_rows_from_units(const int *unit_off, int tilem, int nwin, int *Cptr) {
@@ -2167,7 +2215,8 @@ static int g_ablate = -1;
 // operands Ael/Bel (16x16): the element-level structure instead (non-empty C
 // tiles only; the CSR path, whose C tiles are internal).
 int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_dev_tiles &C,
-              long long *tile_products_out, hipStream_t s, const tsg_dev_csr *Ael, const tsg_dev_csr *Bel) {
+              long long *tile_products_out, hipStream_t s, const tsg_dev_csr *Ael, const tsg_dev_csr *Bel,
+              const int2 *ebnd) {
     const bool el = Ael && Bel;  // element-level structure (16x16 tiles, CSR operands)
     const int tilemA = A.tilem, tilenB = B.tilen;
     int win, nwin;
@@ -2186,20 +2235,45 @@ int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_d
     // 4 GiB: one tile-product enumeration instead of two
     // (and when the products per unit -- estimated from the mean B tile row --
     // outweigh a reread of the window's words, i.e. not for banded matrices)
+    // EL with per-entry B bounds: pass 0 also emits each unit's sorted columns into
+    // a unit buffer (capacity min(products, window)) when the buffers total at most
+    // 2 x the element products + 2^26 slots; a gather compacts them after the scan
+    int *ubuf = nullptr;
+    long long *ubuf_off = nullptr;
+    if (el && ebnd && tilemA > 0 && !(g_ablate & 512)) {
+        TSG_TRY(cx.get(&ubuf_off, (size_t)nunits1 + 1));
+        TSG_HIP(hipMemsetAsync(ubuf_off + nunits1, 0, sizeof(long long), s));
+        k_step1_cap<<<grid_for((long)tilemA * 64, WG, 8192), WG, 0, s>>>(Ael->rowpointer, Ael->m, ebnd, tilemA, nwin,
+                                                                         win, tilenB, ubuf_off);
+        TSG_HIP(hipGetLastError());
+        TSG_TRY(scan_exclusive_i64(cx, ubuf_off, nunits1 + 1, s));
+        long long slots = 0;
+        TSG_TRY(read_i64(cx, ubuf_off + nunits1, &slots, s));
+        const double est = (double)Ael->nnz * ((double)Bel->nnz / (double)(Bel->m > 0 ? Bel->m : 1));
+        if ((double)slots <= 2.0 * est + (double)(1 << 26) && slots < (1LL << 31) &&
+            cx.get(&ubuf, (size_t)slots + 1) == TSG_OK) {
+        } else {
+            (void)hipGetLastError();
+            ubuf = nullptr;
+            cx.put(ubuf_off);
+            ubuf_off = nullptr;
+        }
+    }
     u32 *bmst = nullptr;
     const size_t bm_bytes = (size_t)nunits1 * (win / 8);
     const double est_products =
         el ? (double)Ael->nnz * ((double)Bel->nnz / (double)(Bel->m > 0 ? Bel->m : 1))
            : (double)A.numtile * ((double)B.numtile / (double)(B.tilem > 0 ? B.tilem : 1));
     const bool store = bm_bytes <= (4ull << 30) && est_products >= (double)nunits1 * (win / 32) / 8.0;
-    if (store && !(g_ablate & 256) && cx.get(&bmst, bm_bytes / 4) != TSG_OK) {
+    if (store && !ubuf && !(g_ablate & 256) && cx.get(&bmst, bm_bytes / 4) != TSG_OK) {
         bmst = nullptr;
         (void)hipGetLastError();
     }
     if (tilemA > 0) {
         if (el)
             k_step1<0, true><<<g1, WG, 0, s>>>(Ael->rowpointer, Ael->columnindex, Bel->rowpointer, Bel->columnindex,
-                                               tilemA, tilenB, nwin, win, ucnt, nullptr, nullptr, prod, bmst, Ael->m);
+                                               tilemA, tilenB, nwin, win, ucnt, nullptr, nullptr, prod, bmst, Ael->m,
+                                               ebnd, ubuf, ubuf_off);
         else
             k_step1<0><<<g1, WG, 0, s>>>(A.tile_ptr, A.tile_columnidx, B.tile_ptr, B.tile_columnidx, tilemA, tilenB,
                                          nwin, win, ucnt, nullptr, nullptr, prod, bmst);
@@ -2216,7 +2290,9 @@ int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_d
     const size_t nb1 = (size_t)numblkC + 1;
     TSG_TRY(cx.get(&C.tile_columnidx, nb1));
     if (tilemA > 0) {
-        if (bmst)
+        if (ubuf)
+            k_step1_gather<<<g1, WG, 0, s>>>(ubuf, ubuf_off, ucnt, nunits1, C.tile_columnidx);
+        else if (bmst)
             k_step1<2><<<g1, WG, 0, s>>>(A.tile_ptr, A.tile_columnidx, B.tile_ptr, B.tile_columnidx, tilemA, tilenB,
                                          nwin, win, nullptr, ucnt, C.tile_columnidx, nullptr, bmst);
         else if (el)
@@ -2229,6 +2305,8 @@ int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_d
     }
     TSG_HIP(hipGetLastError());
     cx.put(bmst);
+    cx.put(ubuf);
+    cx.put(ubuf_off);
     cx.put(ucnt);
     cx.put(prod);
     *tile_products_out = tile_products;
@@ -2260,7 +2338,16 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     if (!s1elem && (!A.tile_columnidx || !B.tile_columnidx) && A.numtile > 0 && B.numtile > 0)
         return TSG_ERR_INVALID;  // tile-level step 1 needs both tile structures
     long long tile_products = 0;
-    TSG_TRY(dev_step1(cx, A, B, C, &tile_products, s, s1elem ? Acsr : nullptr, s1elem ? Bcsr : nullptr));
+    // per A entry: its B row's position range (step 1's element walk, the split points)
+    int2 *ebnd = nullptr;
+    if ((s2elem || s3elem) && Acsr->nnz > 0) {
+        TSG_TRY(cx.get(&ebnd, (size_t)Acsr->nnz + 1));
+        k_entry_bounds<<<grid_for(Acsr->nnz, WG, 16384), WG, 0, s>>>(Acsr->columnindex, Acsr->nnz,
+                                                                    Bcsr->rowpointer, ebnd);
+        TSG_HIP(hipGetLastError());
+    }
+    TSG_TRY(dev_step1(cx, A, B, C, &tile_products, s, s1elem ? Acsr : nullptr, s1elem ? Bcsr : nullptr,
+                      s1elem ? ebnd : nullptr));
     const int numblkC = C.numtile;
     const size_t nb1 = (size_t)numblkC + 1;
     if (ev) TSG_HIP(hipEventRecord(ev[1], s));
@@ -2316,7 +2403,6 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     int *esplit = nullptr;
     long long *ebase = nullptr;
     int4 *etab = nullptr;
-    int2 *ebnd = nullptr;
     if (s2elem || s3elem) {
         TSG_TRY(cx.get(&ebase, (size_t)tilemA + 1));
         k_esplit_counts<TM><<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(uoff, Acsr->rowpointer, A.m, tilemA, ebase);
@@ -2330,10 +2416,6 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
         if (nunits > 0) {
             k_unit_etab<TM><<<grid_for(nunits, WG, 8192), WG, 0, s>>>(utab, nunits, Acsr->rowpointer, A.m, ebase,
                                                                       etab);
-            TSG_TRY(cx.get(&ebnd, (size_t)Acsr->nnz + 1));
-            if (Acsr->nnz > 0)
-                k_entry_bounds<<<grid_for(Acsr->nnz, WG, 16384), WG, 0, s>>>(Acsr->columnindex, Acsr->nnz,
-                                                                            Bcsr->rowpointer, ebnd);
             k_esplit_units<TM><<<grid_for(nunits, WAVES, 16384), WG, 0, s>>>(utab, etab, nunits, ebnd,
                                                                              Bcsr->columnindex, C.tile_columnidx,
                                                                              esplit);
