@@ -1328,7 +1328,16 @@ int dev_rows_sorted(Context &cx, const tsg_dev_csr &M, bool *sorted, hipStream_t
 // the row-major views (rm_mask, rm_rowstart) that csr2tile builds.
 // ---------------------------------------------------------------------------
 constexpr int CH = 256;          // C tiles per unit
-constexpr int S3_NZCAP = 1024;   // fp64 accumulator slots per numeric pass
+#ifndef TSG_S3CAP
+#define TSG_S3CAP 1024
+#endif
+#ifndef TSG_S3WPE
+#define TSG_S3WPE 6
+#endif
+#ifndef TSG_S2WPE
+#define TSG_S2WPE 6
+#endif
+constexpr int S3_NZCAP = TSG_S3CAP;  // fp64 accumulator slots per numeric pass
 
 template <int TM> struct CM {
     static constexpr int MW = TM / 16;           // u16 mask words per C row
@@ -1678,7 +1687,7 @@ __device__ unsigned long long g_prof[16];  // [0,8) step 3, [8,16) step 2
 #endif
 
 template <int TM, int TN, bool ELEM>
-__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(6))) void k_step2(const int4 *utab, const int4 *etab, int nunits, ABView V, ECsr E,
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(TSG_S2WPE))) void k_step2(const int4 *utab, const int4 *etab, int nunits, ABView V, ECsr E,
                                               const int *Ccol, int *nnzC, int *unit_rc, u16 *maskC, u16 *codeC,
                                               int ablate) {
 #ifdef TSG_PROF_BUILD
@@ -1900,7 +1909,7 @@ __device__ __forceinline__ int tile_rank16(const u32 *tile, int r, int c) {
 // RST (denser tiles): a per-tile table of row-start ranks (u8) in LDS replaces
 // the eight popcounts of tile_rank16 on every product, at +4 KB of LDS.
 template <int TM, int TN, bool WCSR, bool WTILE, bool ELEM, bool RST = false>
-__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(RST ? 5 : 6))) void k_step3(const int4 *utab, const int4 *etab, int nunits, int mrows, ABView V,
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(RST ? 5 : TSG_S3WPE))) void k_step3(const int4 *utab, const int4 *etab, int nunits, int mrows, ABView V,
                                               ECsr E, const int *Ccol,
                                               const int *nnzoff, const u16 *maskC, const u16 *codeC,
                                               const int *unit_rb,
