@@ -26,6 +26,13 @@
 
 namespace tsg {
 
+// TSG_ABLATE diagnostics bitmask (documented above dev_step1), read once
+static int g_ablate = -1;
+static int ablate_bits() {
+    if (g_ablate < 0) g_ablate = getenv("TSG_ABLATE") ? atoi(getenv("TSG_ABLATE")) : 0;
+    return g_ablate;
+}
+
 typedef unsigned long long u64;
 typedef unsigned int u32;
 typedef unsigned short u16;
@@ -1125,10 +1132,11 @@ __global__ void k_rows_from_units(const int *unit_off, int tilem, int nwin, int 
 // row) straight from CSR, the structural half of csr2tile (csr2tile.h:6-120):
 // unit = (tile row i, window of `win` tile columns), LDS bitmask of the tile
 // columns hit by the tile row's entries.  PASS 0 counts, PASS 1 emits.
+//   flagged_only (PASS 0): only the units k_tcount16 marked -1
 template <int PASS>
 __global__ __launch_bounds__(WG) void k_tstruct(const int *rowptr, const int *col, int m, int tr, int tc, int tilem,
                                                 int tilen, int nwin, int win, int *unit_cnt, const int *unit_off,
-                                                int *tcol) {
+                                                int *tcol, int flagged_only = 0) {
     __shared__ __align__(16) u32 bm[S1_MAXWORDS];
     __shared__ int red[WAVES];
     __shared__ int red2[2 * WAVES];
@@ -1136,6 +1144,7 @@ __global__ __launch_bounds__(WG) void k_tstruct(const int *rowptr, const int *co
     const int words = win >> 5;
     const int wpt = words / WG;
     for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
+        if (PASS == 0 && flagged_only && unit_cnt[u] >= 0) continue;  // uniform
         const int i = u / nwin, w = u - i * nwin;
         const int p0 = rowptr[i * tr], p1 = rowptr[min((i + 1) * tr, m)];
         if (p0 == p1) {
@@ -1167,6 +1176,47 @@ __global__ __launch_bounds__(WG) void k_tstruct(const int *rowptr, const int *co
         __syncthreads();
         bm_count_emit<PASS>(bm, words, wpt, wlo, whi, clo, red, unit_cnt, u, PASS == 1 ? unit_off[u] : 0, tcol);
         __syncthreads();
+    }
+}
+
+// Tile counts of 16x16 tile rows (one window), wave per tile row: the tile
+// row's E <= 256 tile columns go into a wave-private LDS hash set (512 slots,
+// linear probing, atomicCAS tells new from duplicate), so a tile row costs
+// ~E/64 hash rounds and no workgroup syncs.  Larger tile rows get -1 and go to
+// k_tstruct's bitmap.
+constexpr int TC_SLOTS = 512;
+__global__ __launch_bounds__(WG) void k_tcount16(const int *rowptr, const int *col, int m, int tilem, int *unit_cnt) {
+    __shared__ __align__(16) u32 ht_all[WAVES * TC_SLOTS];
+    u32 *ht = ht_all + wave_id() * TC_SLOTS;
+    const int lane = lane_id();
+    for (long i = ((long)blockIdx.x * WG + threadIdx.x) >> 6; i < tilem; i += ((long)gridDim.x * WG) >> 6) {
+        const int p0 = rowptr[i * 16], p1 = rowptr[min((int)i * 16 + 16, m)];
+        const int E = p1 - p0;
+        if (E > TC_SLOTS / 2) {
+            if (lane == 0) unit_cnt[i] = -1;
+            continue;
+        }
+#pragma unroll
+        for (int q = 0; q < TC_SLOTS / 256; ++q)
+            reinterpret_cast<uint4 *>(ht)[q * 64 + lane] = make_uint4(~0u, ~0u, ~0u, ~0u);
+        wave_lds_sync();
+        int cnt = 0;
+        for (int c = 0; c < E; c += 64) {
+            bool fresh = false;
+            if (c + lane < E) {
+                const u32 tc = (u32)col[p0 + c + lane] >> 4;
+                u32 h = (tc * 0x9E3779B1u) >> 23;  // 9 bits: TC_SLOTS = 512
+                for (int pr = 0; pr < TC_SLOTS; ++pr) {
+                    const u32 old = atomicCAS(&ht[h], ~0u, tc);
+                    if (old == ~0u) { fresh = true; break; }
+                    if (old == tc) break;
+                    h = (h + 1) & (TC_SLOTS - 1);
+                }
+            }
+            cnt += __popcll(__ballot(fresh));
+        }
+        wave_lds_sync();
+        if (lane == 0) unit_cnt[i] = cnt;
     }
 }
 
@@ -1224,9 +1274,18 @@ int dev_tile_structure(Context &cx, const tsg_dev_csr &M, int tr, int tc, tsg_de
     TSG_TRY(cx.get(&out.tile_ptr, (size_t)out.tilem + 1));
     TSG_HIP(hipMemsetAsync(ucnt + nunits, 0, sizeof(int), s));
     const int g = grid_for(nunits, 1, 16384);
-    if (out.tilem > 0)
-        k_tstruct<0><<<g, WG, 0, s>>>(M.rowpointer, M.columnindex, M.m, tr, tc, out.tilem, out.tilen, nwin, win,
-                                      ucnt, nullptr, nullptr);
+    if (out.tilem > 0) {
+        const bool wave16 = tr == 16 && tc == 16 && nwin == 1 && !(ablate_bits() & 2048);
+        if (wave16) {  // wave per tile row; the (rare) tile rows over 1024 entries then take the bitmap
+            k_tcount16<<<grid_for((long)out.tilem * 64, WG, 16384), WG, 0, s>>>(M.rowpointer, M.columnindex, M.m,
+                                                                               out.tilem, ucnt);
+            k_tstruct<0><<<g, WG, 0, s>>>(M.rowpointer, M.columnindex, M.m, tr, tc, out.tilem, out.tilen, nwin, win,
+                                          ucnt, nullptr, nullptr, 1);
+        } else {
+            k_tstruct<0><<<g, WG, 0, s>>>(M.rowpointer, M.columnindex, M.m, tr, tc, out.tilem, out.tilen, nwin, win,
+                                          ucnt, nullptr, nullptr);
+        }
+    }
     TSG_HIP(hipGetLastError());
     TSG_TRY(scan_exclusive_i32(cx, ucnt, nunits + 1, s));
     k_rows_from_units<<<grid_for(out.tilem + 1, WG, 4096), WG, 0, s>>>(ucnt, out.tilem, nwin, out.tile_ptr);
@@ -1289,28 +1348,37 @@ __global__ __launch_bounds__(WG) void k_entry_bounds(const int *ciA, long nnzA, 
     }
 }
 
-__global__ __launch_bounds__(WG) void k_rows_unsorted2(const int *rp, const int *ci, int m, int *flag) {
-    const int nnz = rp[m];
-    for (int p = blockIdx.x * WG + threadIdx.x + 1; p < nnz; p += gridDim.x * WG) {
-        if (ci[p] >= ci[p - 1]) continue;
-        int lo = 0, hi = m;  // is p a row start?  (first R with rp[R] >= p)
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (rp[mid] < p) lo = mid + 1; else hi = mid;
-        }
-        if (rp[lo] != p) *flag = 1;
+// row starts as a bitmap over entry positions (bit p set: some non-empty row starts at p)
+__global__ __launch_bounds__(WG) void k_row_start_bits(const int *rp, int m, u32 *bits) {
+    for (int r = blockIdx.x * WG + threadIdx.x; r < m; r += gridDim.x * WG) {
+        const int p = rp[r];
+        if (p < rp[r + 1]) atomicOr(&bits[p >> 5], 1u << (p & 31));
     }
+}
+// a descent ci[p] < ci[p-1] that is not at a row start: rows are not column-sorted
+__global__ __launch_bounds__(WG) void k_rows_unsorted3(const int *rp, const int *ci, int m, const u32 *bits,
+                                                       int *flag) {
+    const int nnz = rp[m];
+    for (int p = blockIdx.x * WG + threadIdx.x + 1; p < nnz; p += gridDim.x * WG)
+        if (ci[p] < ci[p - 1] && !((bits[p >> 5] >> (p & 31)) & 1u)) *flag = 1;
 }
 
 int dev_rows_sorted(Context &cx, const tsg_dev_csr &M, bool *sorted, hipStream_t s) {
     int *flag = nullptr;
     TSG_TRY(cx.get(&flag, 1));
     TSG_HIP(hipMemsetAsync(flag, 0, sizeof(int), s));
-    if (M.m > 0 && M.nnz > 1)
-        k_rows_unsorted2<<<grid_for(M.nnz, WG, 16384), WG, 0, s>>>(M.rowpointer, M.columnindex, M.m, flag);
+    u32 *bits = nullptr;
+    if (M.m > 0 && M.nnz > 1) {
+        const size_t nw = ((size_t)M.nnz + 31) / 32;
+        TSG_TRY(cx.get(&bits, nw));
+        TSG_HIP(hipMemsetAsync(bits, 0, nw * sizeof(u32), s));
+        k_row_start_bits<<<grid_for(M.m, WG, 16384), WG, 0, s>>>(M.rowpointer, M.m, bits);
+        k_rows_unsorted3<<<grid_for(M.nnz, WG, 16384), WG, 0, s>>>(M.rowpointer, M.columnindex, M.m, bits, flag);
+    }
     TSG_HIP(hipGetLastError());
     int f = 0;
     TSG_TRY(read_i32(cx, flag, &f, s));
+    cx.put(bits);
     cx.put(flag);
     *sorted = (f == 0);
     return TSG_OK;
@@ -2216,7 +2284,8 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(RST ? 5 : TS
 //    8  skip step 3's CSR writes        (results wrong)
 //   16  tile-payload value pass instead of element streaming (results correct)
 //   64  per-phase clock totals, with the -DTSG_PROF_BUILD library (make prof)
-static int g_ablate = -1;
+//  256  step 1: no stored bitmasks       512  step 1: no unit-buffer emit (second product pass)
+// 2048  tile counts: bitmap kernel only (no wave-per-tile-row count)
 
 // Step 1 (C tile structure = tile-pattern product of A's and B's row-major tile
 // structures; includes tiles whose element product is empty, as the reference).
@@ -2249,7 +2318,7 @@ int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_d
     // 2 x the element products + 2^26 slots; a gather compacts them after the scan
     int *ubuf = nullptr;
     long long *ubuf_off = nullptr;
-    if (el && ebnd && tilemA > 0 && !(g_ablate & 512)) {
+    if (el && ebnd && tilemA > 0 && !(ablate_bits() & 512)) {
         TSG_TRY(cx.get(&ubuf_off, (size_t)nunits1 + 1));
         TSG_HIP(hipMemsetAsync(ubuf_off + nunits1, 0, sizeof(long long), s));
         k_step1_cap<<<grid_for((long)tilemA * 64, WG, 8192), WG, 0, s>>>(Ael->rowpointer, Ael->m, ebnd, tilemA, nwin,
@@ -2274,7 +2343,7 @@ int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_d
         el ? (double)Ael->nnz * ((double)Bel->nnz / (double)(Bel->m > 0 ? Bel->m : 1))
            : (double)A.numtile * ((double)B.numtile / (double)(B.tilem > 0 ? B.tilem : 1));
     const bool store = bm_bytes <= (4ull << 30) && est_products >= (double)nunits1 * (win / 32) / 8.0;
-    if (store && !ubuf && !(g_ablate & 256) && cx.get(&bmst, bm_bytes / 4) != TSG_OK) {
+    if (store && !ubuf && !(ablate_bits() & 256) && cx.get(&bmst, bm_bytes / 4) != TSG_OK) {
         bmst = nullptr;
         (void)hipGetLastError();
     }
@@ -2325,7 +2394,7 @@ int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_d
 int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_dev_tiles &C,
                    tsg_stats *st, hipStream_t s, hipEvent_t *ev, tsg_dev_csr *csr_out, const tsg_dev_csr *Acsr,
                    const tsg_dev_csr *Bcsr, bool step2_elem) {
-    if (g_ablate < 0) g_ablate = getenv("TSG_ABLATE") ? atoi(getenv("TSG_ABLATE")) : 0;
+    ablate_bits();
     constexpr int TM = 16, TN = 16;
     if (A.tile_m != TM || A.tile_n != TN || B.tile_m != TN || B.tile_n != TM) return TSG_ERR_UNSUPPORTED;
     // element streaming needs the CSR operands (B rows column-sorted: caller's check)
