@@ -165,6 +165,53 @@ __device__ __forceinline__ int lower_bound_dev(const T *a, int lo, int hi, T key
     return lo;
 }
 
+#ifndef TSG_BL_LB
+#define TSG_BL_LB 1
+#endif
+#ifndef TSG_BL_OWN
+#define TSG_BL_OWN 0  // measured: the while-loop search is faster here
+#endif
+#ifndef TSG_BL_RANK
+#define TSG_BL_RANK 1
+#endif
+// Branchless searches for WAVE-UNIFORM bounds: the trip count depends only on
+// the (uniform) range length, so the loop has no exec-mask bookkeeping and the
+// body is compare + select around one LDS read.
+// first index in [lo,hi) with a[idx] >= key
+__device__ __forceinline__ int lower_bound_u(const int *a, int lo, int hi, int key) {
+#if TSG_BL_LB
+    int len = hi - lo, base = lo;
+    if (len <= 0) return lo;
+    while (len > 1) {
+        const int half = len >> 1;
+        base = (a[base + half - 1] < key) ? base + half : base;
+        len -= half;
+    }
+    return base + (a[base] < key ? 1 : 0);
+#else
+    return lower_bound_dev(a, lo, hi, key);
+#endif
+}
+// largest l in [0, n) with off[l] <= it (off non-decreasing, off[0] <= it);
+// reads stay below the next power of two of n
+__device__ __forceinline__ int owner_search(const int *off, int n, int it) {
+#if TSG_BL_OWN
+    int lo = 0;
+    for (int st = n > 1 ? 1 << (31 - __clz(n - 1)) : 0; st > 0; st >>= 1) {
+        const int c = lo + st;
+        lo = (c < n && off[c] <= it) ? c : lo;
+    }
+    return lo;
+#else
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (off[mid] <= it) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+#endif
+}
+
 static inline int grid_for(long work, int per_block, int cap) {
     long g = (work + per_block - 1) / per_block;
     if (g < 1) g = 1;
@@ -937,11 +984,7 @@ __device__ __forceinline__ long for_each_product(int a0, int a1, const int *colA
         __syncthreads();
         const int nA = min(WG, a1 - ab);
         for (int q = threadIdx.x; q < tot; q += WG) {
-            int lo = 0, hi = nA - 1;
-            while (lo < hi) {
-                int mid = (lo + hi + 1) >> 1;
-                if (L.off[mid] <= q) lo = mid; else hi = mid - 1;
-            }
+            const int lo = owner_search(L.off, nA, q);
             f(ab + lo, L.bs[lo] + (q - L.off[lo]));
         }
         items += tot;
@@ -1563,13 +1606,9 @@ template <class F>
 __device__ __forceinline__ void unit_items(const ABView &V, int ab, int na, int tot, const int *s_cols, int ns,
                                            ProdLds &L, F &&f) {
     for (int q = threadIdx.x; q < tot; q += WG) {
-        int lo = 0, hi = na - 1;
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (L.off[mid] <= q) lo = mid; else hi = mid - 1;
-        }
+        const int lo = owner_search(L.off, na, q);
         const int b = L.bs[lo] + (q - L.off[lo]);
-        f(ab + lo, b, lower_bound_dev(s_cols, 0, ns, V.Bcol[b]));
+        f(ab + lo, b, lower_bound_u(s_cols, 0, ns, V.Bcol[b]));
     }
 }
 
@@ -1723,11 +1762,7 @@ __device__ __forceinline__ void elem_stream(const ECsr &E, int4 ue, const EPre &
         L.off[threadIdx.x] = off;
         __syncthreads();
         for (int it = threadIdx.x; it < tot; it += WG) {
-            int lo = 0, hi = na - 1;
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (L.off[mid] <= it) lo = mid; else hi = mid - 1;
-            }
+            const int lo = owner_search(L.off, na, it);
             f((int)s_r[lo], lo, L.bs[lo] + (it - L.off[lo]));
         }
         __syncthreads();
@@ -1836,7 +1871,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(TSG_S2WPE)))
         if (ELEM) {
             elem_stream<TM>(E, ue, pre, s_rp, false, 0, 0, s_r, nullptr, L, [&](int r, int, int pb) {
                 const int x = E.ciB[pb];
-                const int sl = lower_bound_dev(s_cols, 0, ns, x / TM);  // step 1 covers every product
+                const int sl = lower_bound_u(s_cols, 0, ns, x / TM);  // step 1 covers every product
                 const int c = x % TM, k = r * MW + (c >> 4);
                 atomicOr(&s_mask[sl * TW32 + (k >> 1)], (0x8000u >> (c & 15)) << ((k & 1) * 16));
             });
@@ -1957,6 +1992,24 @@ __device__ __forceinline__ int kth_col16(u32 v, int k) {
 // rank of column c among row r's set bits plus all bits of rows < r
 // (row-major in-tile position of (r, c); 16x16 tiles, MSB-first row words)
 __device__ __forceinline__ int tile_rank16(const u32 *tile, int r, int c) {
+#if TSG_BL_RANK
+    // two vector LDS reads, masked popcounts (no per-word branches)
+    const uint4 a = reinterpret_cast<const uint4 *>(tile)[0], b = reinterpret_cast<const uint4 *>(tile)[1];
+    const u32 wv[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    const int kr = r >> 1;
+    int rank = 0;
+    u32 row = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        rank += __popc(wv[k] & (k < kr ? ~0u : 0u));
+        row = (k == kr) ? wv[k] : row;
+    }
+    if (r & 1) {
+        rank += __popc(row & 0xffffu);
+        row >>= 16;
+    }
+    return rank + __popc((row & 0xffffu) >> (16 - c));  // bits of columns < c (column c = bit 15 - c)
+#else
     int rank = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -1966,6 +2019,7 @@ __device__ __forceinline__ int tile_rank16(const u32 *tile, int r, int c) {
     }
     const u32 row = (tile[r >> 1] >> ((r & 1) * 16)) & 0xffffu;
     return rank + __popc(row >> (16 - c));  // bits of columns < c (column c = bit 15 - c)
+#endif
 }
 
 // Step 3 with a TILE-MAJOR accumulator: a pass's nonzeros sit at
@@ -2235,7 +2289,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(RST ? 5 : TS
                     elem_stream<TM>(E, ue, pre, s_rp, narrow, clo, chi, s_r, s_va, L, [&](int r, int slot, int pb) {
                         const int x = E.ciB[pb];
                         const double vb = E.vB[pb];
-                        const int sl = lower_bound_dev(s_cols, s_lo, s_hi, x / TM);
+                        const int sl = lower_bound_u(s_cols, s_lo, s_hi, x / TM);
                         if (sl >= s_hi || s_cols[sl] != x / TM) return;  // another pass's tile
                         const int c = x % TM;
                         const int rk = RST ? (int)s_rs[sl * TM + r] +
