@@ -171,6 +171,9 @@ __device__ __forceinline__ int lower_bound_dev(const T *a, int lo, int hi, T key
 #ifndef TSG_BL_OWN
 #define TSG_BL_OWN 0  // measured: the while-loop search is faster here
 #endif
+#ifndef TSG_BL_BALLOT
+#define TSG_BL_BALLOT 0  // measured: the branchy ballot loop is faster
+#endif
 #ifndef TSG_BL_RANK
 #define TSG_BL_RANK 1
 #endif
@@ -1871,8 +1874,8 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(TSG_S2WPE)))
         if (ELEM) {
             elem_stream<TM>(E, ue, pre, s_rp, false, 0, 0, s_r, nullptr, L, [&](int r, int, int pb) {
                 const int x = E.ciB[pb];
-                const int sl = lower_bound_u(s_cols, 0, ns, x / TM);  // step 1 covers every product
-                const int c = x % TM, k = r * MW + (c >> 4);
+                const int sl = lower_bound_u(s_cols, 0, ns, (int)((u32)x / TM));  // step 1 covers every product
+                const int c = (int)((u32)x % TM), k = r * MW + (c >> 4);
                 atomicOr(&s_mask[sl * TW32 + (k >> 1)], (0x8000u >> (c & 15)) << ((k & 1) * 16));
             });
         } else {
@@ -2208,11 +2211,29 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(RST ? 5 : TS
                     const int e = eb + threadIdx.x;
                     const bool in = e < nz;
                     const int key = in ? (int)s_key[e] : 0;
-                    const int r = key >> 4;
+                    const int r = in ? key >> 4 : TM;  // idle lanes match no row
+#if TSG_BL_BALLOT
+                    // branchless: rank from mbcnt by select, the wave's row counts
+                    // gathered in lanes 0..15 and stored with one LDS write
+                    int lrank = 0, cntv = 0;
+#pragma unroll
+                    for (int rr = 0; rr < TM; ++rr) {  // rank among this wave's row-rr nonzeros
+                        const u64 m = __ballot(r == rr);
+                        const int mr = __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));
+                        lrank = (r == rr) ? mr : lrank;
+                        cntv = (lane == rr) ? (int)__popcll(m) : cntv;
+                    }
+                    if (lane < TM) s_wcnt[wv][lane] = cntv;
+                    __syncthreads();
+                    if (in) {
+                        int before = s_run[r];
+#pragma unroll
+                        for (int w2 = 0; w2 < WAVES - 1; ++w2) before += (w2 < wv) ? s_wcnt[w2][r] : 0;
+#else
                     int lrank = 0;
 #pragma unroll
                     for (int rr = 0; rr < TM; ++rr) {  // rank among this wave's row-rr nonzeros
-                        const u64 m = __ballot(in && r == rr);
+                        const u64 m = __ballot(r == rr);
                         if (r == rr) lrank = __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));
                         if (lane == 0) s_wcnt[wv][rr] = __popcll(m);
                     }
@@ -2220,6 +2241,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(RST ? 5 : TS
                     if (in) {
                         int before = s_run[r];
                         for (int w2 = 0; w2 < wv; ++w2) before += s_wcnt[w2][r];
+#endif
                         const int dst = s_rowptr[r] + s_carry[r] + before + lrank;
                         csr_col[dst] = s_cols[s_kt[e]] * TM + (key & 15);
                         csr_val[dst] = acc[e];
@@ -2289,9 +2311,9 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(RST ? 5 : TS
                     elem_stream<TM>(E, ue, pre, s_rp, narrow, clo, chi, s_r, s_va, L, [&](int r, int slot, int pb) {
                         const int x = E.ciB[pb];
                         const double vb = E.vB[pb];
-                        const int sl = lower_bound_u(s_cols, s_lo, s_hi, x / TM);
-                        if (sl >= s_hi || s_cols[sl] != x / TM) return;  // another pass's tile
-                        const int c = x % TM;
+                        const int xt = (int)((u32)x / TM), c = (int)((u32)x % TM);  // x >= 0
+                        const int sl = lower_bound_u(s_cols, s_lo, s_hi, xt);
+                        if (sl >= s_hi || s_cols[sl] != xt) return;  // another pass's tile
                         const int rk = RST ? (int)s_rs[sl * TM + r] +
                                                  __popc(((s_mask[sl * TW32 + (r >> 1)] >> ((r & 1) * 16)) & 0xffffu) >>
                                                         (16 - c))
