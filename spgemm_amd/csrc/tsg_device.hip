@@ -2271,6 +2271,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(RST ? 5 : TS
         };
         for (;;) {
             int lo = s_lo + 1, hi = ns;  // largest s_hi with nnz(tiles s_lo..s_hi-1) <= NZCAP
+            if (s_off[ns] - s_off[s_lo] <= S3_NZCAP) lo = ns;  // the rest fits one pass (the common case)
             while (lo < hi) {
                 const int mid = (lo + hi + 1) >> 1;
                 if (s_off[mid] - s_off[s_lo] <= S3_NZCAP) lo = mid; else hi = mid - 1;
