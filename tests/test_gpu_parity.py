@@ -185,6 +185,14 @@ def test_full_size_synthetic_vs_oracle(name):
     ref = O.gustavson(oA, oB)
     assert_csr_equal(Cm.csr(), ref.csr())
     assert st["nnzC"] == ref.s.nnz
+    # the pipeline's A/B tile counts (wave hash sets + bitmap fallback for tile
+    # rows over 256 entries) equal the oracle csr2tile's numtile
+    tA = O.OMat.from_csr(m, n, rp, ci, vv)
+    O.csr2tile_row_major(tA, 16, 16)
+    assert st["numtileA"] == tA.s.numtile
+    tB = O.transpose(tA) if name == "mc2depi" else O.OMat.from_csr(m, n, rp, ci, vv)
+    O.csr2tile_col_major(tB, 16, 16)
+    assert st["numtileB"] == tB.s.numtile
 
 
 def test_device_api_matches_host_api():
