@@ -165,6 +165,9 @@ __device__ __forceinline__ int lower_bound_dev(const T *a, int lo, int hi, T key
     return lo;
 }
 
+#ifndef TSG_WS1
+#define TSG_WS1 1
+#endif
 #ifndef TSG_BL_LB
 #define TSG_BL_LB 1
 #endif
@@ -996,6 +999,65 @@ __device__ __forceinline__ long for_each_product(int a0, int a1, const int *colA
     return items;
 }
 
+// Wave-sweep product enumeration (no per-product owner search): entries of the
+// batch (thread t = entry ab + t) with a segment of <= WS_SHORT products walk
+// it themselves; longer segments are compacted into an LDS list and swept by
+// whole waves (lane l takes products bs + l, bs + l + 64, ...: coalesced B
+// reads, wave-uniform entry).  f(a, b) for every product; returns this
+// thread's share of the product count.
+constexpr int WS_SHORT = 8;
+struct WsLds {
+    int2 seg[WG];   // long segments [bs, be)
+    int ent[WG];    // their A entries
+    int cnt[WAVES];
+};
+template <class F>
+__device__ __forceinline__ long for_each_product_ws(int a0, int a1, const int2 *ebnd, const int *bcol, int clo,
+                                                    int chi, bool narrow, WsLds &W, F &&f) {
+    long items = 0;
+    const int lane = lane_id(), wv = wave_id();
+    for (int ab = a0; ab < a1; ab += WG) {
+        const int a = ab + threadIdx.x;
+        int bs = 0, be = 0;
+        if (a < a1) {
+            const int2 e = ebnd[a];
+            bs = e.x;
+            be = e.y;
+            if (narrow) {
+                bs = lower_bound_dev(bcol, bs, be, clo);
+                be = lower_bound_dev(bcol, bs, be, chi + 1);
+            }
+        }
+        items += be - bs;
+        const bool lng = be - bs > WS_SHORT;
+        if (!lng)
+            for (int b = bs; b < be; ++b) f(a, b);
+        const u64 m = __ballot(lng);
+        if (lane == 0) W.cnt[wv] = __popcll(m);
+        __syncthreads();
+        int base = 0, total = 0;
+#pragma unroll
+        for (int w2 = 0; w2 < WAVES; ++w2) {
+            const int v = W.cnt[w2];
+            base += (w2 < wv) ? v : 0;
+            total += v;
+        }
+        if (lng) {
+            const int pos = base + __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));
+            W.seg[pos] = make_int2(bs, be);
+            W.ent[pos] = a;
+        }
+        __syncthreads();
+        for (int k = wv; k < total; k += WAVES) {  // wave-uniform
+            const int2 sg = W.seg[k];
+            const int ea = W.ent[k];
+            for (int b = sg.x + lane; b < sg.y; b += 64) f(ea, b);
+        }
+        __syncthreads();  // the list is rewritten by the next batch
+    }
+    return items;
+}
+
 // ---------------------------------------------------------------------------
 // step 1: C tile structure.  Unit = (A tile row i, window w of `win` B tile
 // columns); an LDS bitmask collects the reachable tile columns.
@@ -1079,11 +1141,13 @@ __global__ __launch_bounds__(WG) void k_step1(const int *Aptr, const int *Acol, 
                                               const long long *ubuf_off = nullptr) {
     __shared__ __align__(16) u32 bm[S1_MAXWORDS];
     __shared__ ProdLds L;
+    __shared__ WsLds W;
     __shared__ int red[WAVES];
     const int nunits = tilemA * nwin;
     const int words = win >> 5;
     const int wpt = words / WG;  // words per thread (win is a multiple of 8192)
-    long my_items = 0;
+    long my_items = 0;    // block totals (thread 0)
+    long my_items_t = 0;  // per-thread shares (wave sweep)
     for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
         const int i = u / nwin, w = u - i * nwin;
         const int a0 = EL ? Aptr[min(i * 16, mA)] : Aptr[i], a1 = EL ? Aptr[min(i * 16 + 16, mA)] : Aptr[i + 1];
@@ -1113,13 +1177,18 @@ __global__ __launch_bounds__(WG) void k_step1(const int *Aptr, const int *Acol, 
             const int wlo = 0, whi = words - 1;
             for (int q = wlo + threadIdx.x; q <= whi; q += WG) bm[q] = 0u;
             __syncthreads();
-            long it = for_each_product(a0, a1, Acol, Bptr, Bcol, EL ? clo * 16 : clo, EL ? chi * 16 + 15 : chi,
-                                       nwin > 1, L, [&](int a, int b) {
+            auto mark = [&](int a, int b) {
                 (void)a;
                 int c = (EL ? Bcol[b] >> 4 : Bcol[b]) - clo;
                 atomicOr(&bm[c >> 5], 1u << (c & 31));
-            }, EL ? ebnd : nullptr);
-            if (PASS == 0) my_items += (threadIdx.x == 0) ? it : 0;
+            };
+            if (EL && TSG_WS1) {
+                my_items_t += for_each_product_ws(a0, a1, ebnd, Bcol, clo * 16, chi * 16 + 15, nwin > 1, W, mark);
+            } else {
+                long it = for_each_product(a0, a1, Acol, Bptr, Bcol, EL ? clo * 16 : clo, EL ? chi * 16 + 15 : chi,
+                                           nwin > 1, L, mark, EL ? ebnd : nullptr);
+                if (PASS == 0) my_items += (threadIdx.x == 0) ? it : 0;
+            }
             if (PASS == 0 && bm_store) {
                 u32 wv[8];
                 bm_words(bm, wpt, wv);
@@ -1137,6 +1206,10 @@ __global__ __launch_bounds__(WG) void k_step1(const int *Aptr, const int *Acol, 
                                     PASS == 1 ? unit_off[u] : 0, Ccol);
             __syncthreads();
         }
+    }
+    if (PASS == 0 && EL && TSG_WS1) {
+        my_items_t = wave_sum((long long)my_items_t);
+        if (lane_id() == 0 && my_items_t) atomicAdd(prod_total, (u64)my_items_t);
     }
     if (PASS == 0 && threadIdx.x == 0 && my_items) atomicAdd(prod_total, (u64)my_items);
 }
