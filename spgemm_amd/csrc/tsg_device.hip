@@ -165,27 +165,11 @@ __device__ __forceinline__ int lower_bound_dev(const T *a, int lo, int hi, T key
     return lo;
 }
 
-#ifndef TSG_WS1
-#define TSG_WS1 1
-#endif
-#ifndef TSG_BL_LB
-#define TSG_BL_LB 1
-#endif
-#ifndef TSG_BL_OWN
-#define TSG_BL_OWN 0  // measured: the while-loop search is faster here
-#endif
-#ifndef TSG_BL_BALLOT
-#define TSG_BL_BALLOT 0  // measured: the branchy ballot loop is faster
-#endif
-#ifndef TSG_BL_RANK
-#define TSG_BL_RANK 1
-#endif
-// Branchless searches for WAVE-UNIFORM bounds: the trip count depends only on
-// the (uniform) range length, so the loop has no exec-mask bookkeeping and the
-// body is compare + select around one LDS read.
+// Branchless lower bound for WAVE-UNIFORM bounds: the trip count depends only
+// on the (uniform) range length, so the loop has no exec-mask bookkeeping and
+// the body is compare + select around one LDS read.
 // first index in [lo,hi) with a[idx] >= key
 __device__ __forceinline__ int lower_bound_u(const int *a, int lo, int hi, int key) {
-#if TSG_BL_LB
     int len = hi - lo, base = lo;
     if (len <= 0) return lo;
     while (len > 1) {
@@ -194,28 +178,16 @@ __device__ __forceinline__ int lower_bound_u(const int *a, int lo, int hi, int k
         len -= half;
     }
     return base + (a[base] < key ? 1 : 0);
-#else
-    return lower_bound_dev(a, lo, hi, key);
-#endif
 }
-// largest l in [0, n) with off[l] <= it (off non-decreasing, off[0] <= it);
-// reads stay below the next power of two of n
+// largest l in [0, n) with off[l] <= it (off non-decreasing, off[0] <= it).
+// A branchless fixed-step variant measured slower here.
 __device__ __forceinline__ int owner_search(const int *off, int n, int it) {
-#if TSG_BL_OWN
-    int lo = 0;
-    for (int st = n > 1 ? 1 << (31 - __clz(n - 1)) : 0; st > 0; st >>= 1) {
-        const int c = lo + st;
-        lo = (c < n && off[c] <= it) ? c : lo;
-    }
-    return lo;
-#else
     int lo = 0, hi = n - 1;
     while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
         if (off[mid] <= it) lo = mid; else hi = mid - 1;
     }
     return lo;
-#endif
 }
 
 static inline int grid_for(long work, int per_block, int cap) {
@@ -1182,7 +1154,7 @@ __global__ __launch_bounds__(WG) void k_step1(const int *Aptr, const int *Acol, 
                 int c = (EL ? Bcol[b] >> 4 : Bcol[b]) - clo;
                 atomicOr(&bm[c >> 5], 1u << (c & 31));
             };
-            if (EL && TSG_WS1) {
+            if (EL) {
                 my_items_t += for_each_product_ws(a0, a1, ebnd, Bcol, clo * 16, chi * 16 + 15, nwin > 1, W, mark);
             } else {
                 long it = for_each_product(a0, a1, Acol, Bptr, Bcol, EL ? clo * 16 : clo, EL ? chi * 16 + 15 : chi,
@@ -1207,7 +1179,7 @@ __global__ __launch_bounds__(WG) void k_step1(const int *Aptr, const int *Acol, 
             __syncthreads();
         }
     }
-    if (PASS == 0 && EL && TSG_WS1) {
+    if (PASS == 0 && EL) {
         my_items_t = wave_sum((long long)my_items_t);
         if (lane_id() == 0 && my_items_t) atomicAdd(prod_total, (u64)my_items_t);
     }
@@ -2068,7 +2040,6 @@ __device__ __forceinline__ int kth_col16(u32 v, int k) {
 // rank of column c among row r's set bits plus all bits of rows < r
 // (row-major in-tile position of (r, c); 16x16 tiles, MSB-first row words)
 __device__ __forceinline__ int tile_rank16(const u32 *tile, int r, int c) {
-#if TSG_BL_RANK
     // two vector LDS reads, masked popcounts (no per-word branches)
     const uint4 a = reinterpret_cast<const uint4 *>(tile)[0], b = reinterpret_cast<const uint4 *>(tile)[1];
     const u32 wv[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
@@ -2085,17 +2056,6 @@ __device__ __forceinline__ int tile_rank16(const u32 *tile, int r, int c) {
         row >>= 16;
     }
     return rank + __popc((row & 0xffffu) >> (16 - c));  // bits of columns < c (column c = bit 15 - c)
-#else
-    int rank = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const u32 v = tile[k];
-        if (2 * k + 1 < r) rank += __popc(v);
-        else if (2 * k < r) rank += __popc(v & 0xffffu);  // row 2k (low half) lies before r = 2k+1
-    }
-    const u32 row = (tile[r >> 1] >> ((r & 1) * 16)) & 0xffffu;
-    return rank + __popc(row >> (16 - c));  // bits of columns < c (column c = bit 15 - c)
-#endif
 }
 
 // Step 3 with a TILE-MAJOR accumulator: a pass's nonzeros sit at
@@ -2285,24 +2245,6 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(RST ? 5 : TS
                     const bool in = e < nz;
                     const int key = in ? (int)s_key[e] : 0;
                     const int r = in ? key >> 4 : TM;  // idle lanes match no row
-#if TSG_BL_BALLOT
-                    // branchless: rank from mbcnt by select, the wave's row counts
-                    // gathered in lanes 0..15 and stored with one LDS write
-                    int lrank = 0, cntv = 0;
-#pragma unroll
-                    for (int rr = 0; rr < TM; ++rr) {  // rank among this wave's row-rr nonzeros
-                        const u64 m = __ballot(r == rr);
-                        const int mr = __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));
-                        lrank = (r == rr) ? mr : lrank;
-                        cntv = (lane == rr) ? (int)__popcll(m) : cntv;
-                    }
-                    if (lane < TM) s_wcnt[wv][lane] = cntv;
-                    __syncthreads();
-                    if (in) {
-                        int before = s_run[r];
-#pragma unroll
-                        for (int w2 = 0; w2 < WAVES - 1; ++w2) before += (w2 < wv) ? s_wcnt[w2][r] : 0;
-#else
                     int lrank = 0;
 #pragma unroll
                     for (int rr = 0; rr < TM; ++rr) {  // rank among this wave's row-rr nonzeros
@@ -2314,7 +2256,6 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(RST ? 5 : TS
                     if (in) {
                         int before = s_run[r];
                         for (int w2 = 0; w2 < wv; ++w2) before += s_wcnt[w2][r];
-#endif
                         const int dst = s_rowptr[r] + s_carry[r] + before + lrank;
                         csr_col[dst] = s_cols[s_kt[e]] * TM + (key & 15);
                         csr_val[dst] = acc[e];
