@@ -2246,11 +2246,26 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(RST ? 5 : TS
                     const int key = in ? (int)s_key[e] : 0;
                     const int r = in ? key >> 4 : TM;  // idle lanes match no row
                     int lrank = 0;
+                    // rank among this wave's row-r nonzeros by four DPP wave scans of
+                    // one-hot row counts (four rows x 8-bit fields per u32; a wave
+                    // holds <= 64 of a row): no per-row ballot / exec-mask loop
+                    {
+                        const int g = r >> 2, sh = 8 * (r & 3);
+                        u32 tot[4];
+                        int pre = 0;
 #pragma unroll
-                    for (int rr = 0; rr < TM; ++rr) {  // rank among this wave's row-rr nonzeros
-                        const u64 m = __ballot(r == rr);
-                        if (r == rr) lrank = __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));
-                        if (lane == 0) s_wcnt[wv][rr] = __popcll(m);
+                        for (int k = 0; k < 4; ++k) {
+                            const u32 oh = (g == k) ? (1u << sh) : 0u;
+                            const u32 inc = (u32)wave_incl_scan_dpp((int)oh);
+                            tot[k] = (u32)__builtin_amdgcn_readlane((int)inc, 63);
+                            pre = (g == k) ? (int)(((inc - oh) >> sh) & 0xffu) : pre;
+                        }
+                        lrank = pre;
+                        if (lane < TM) {
+                            const u32 t = (lane >> 2) == 0 ? tot[0] : (lane >> 2) == 1 ? tot[1]
+                                        : (lane >> 2) == 2 ? tot[2] : tot[3];
+                            s_wcnt[wv][lane] = (int)((t >> (8 * (lane & 3))) & 0xffu);
+                        }
                     }
                     __syncthreads();
                     if (in) {
