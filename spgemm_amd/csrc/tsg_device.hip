@@ -1530,13 +1530,18 @@ __global__ void k_units_per_row(const int *Cptr, int tilem, int *nunits) {
 }
 
 // unit -> C tile row (urow) and the unit table {i, t0, nu, q << 9 | ns} of step 3
-__global__ void k_unit_rows(const int *uoff, const int *Cptr, int tilem, int *urow, int4 *utab) {
+// tbase (optional): the tile row's first C tile in another index space (the
+// step-1 unit buffers, whose columns then need no compaction); t0 is then
+// counted from tbase[i] instead of Cptr[i]
+__global__ void k_unit_rows(const int *uoff, const int *Cptr, int tilem, int *urow, int4 *utab,
+                            const long long *tbase) {
     for (int i = blockIdx.x * WG + threadIdx.x; i < tilem; i += gridDim.x * WG) {
         const int u0 = uoff[i], nu = uoff[i + 1] - u0, c0 = Cptr[i], c1 = Cptr[i + 1];
+        const int b0 = tbase ? (int)tbase[i] : c0;
         for (int q = 0; q < nu; ++q) {
             urow[u0 + q] = i;
             const int t0 = c0 + q * CH;
-            utab[u0 + q] = make_int4(i, t0, nu, (q << 9) | min(CH, c1 - t0));
+            utab[u0 + q] = make_int4(i, b0 + q * CH, nu, (q << 9) | min(CH, c1 - t0));
         }
     }
 }
@@ -2392,6 +2397,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(RST ? 5 : TS
 //   64  per-phase clock totals, with the -DTSG_PROF_BUILD library (make prof)
 //  256  step 1: no stored bitmasks       512  step 1: no unit-buffer emit (second product pass)
 // 2048  tile counts: bitmap kernel only (no wave-per-tile-row count)
+// 8192  CSR path: compact step 1's unit buffers into tile_columnidx (k_step1_gather)
 
 // Step 1 (C tile structure = tile-pattern product of A's and B's row-major tile
 // structures; includes tiles whose element product is empty, as the reference).
@@ -2400,7 +2406,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(RST ? 5 : TS
 // tiles only; the CSR path, whose C tiles are internal).
 int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_dev_tiles &C,
               long long *tile_products_out, hipStream_t s, const tsg_dev_csr *Ael, const tsg_dev_csr *Bel,
-              const int2 *ebnd) {
+              const int2 *ebnd, long long **tbase_out, long long *tslots_out) {
     const bool el = Ael && Bel;  // element-level structure (16x16 tiles, CSR operands)
     const int tilemA = A.tilem, tilenB = B.tilen;
     int win, nwin;
@@ -2424,6 +2430,7 @@ int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_d
     // 2 x the element products + 2^26 slots; a gather compacts them after the scan
     int *ubuf = nullptr;
     long long *ubuf_off = nullptr;
+    long long slots = 0;
     if (el && ebnd && tilemA > 0 && !(ablate_bits() & 512)) {
         TSG_TRY(cx.get(&ubuf_off, (size_t)nunits1 + 1));
         TSG_HIP(hipMemsetAsync(ubuf_off + nunits1, 0, sizeof(long long), s));
@@ -2431,7 +2438,6 @@ int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_d
                                                                          win, tilenB, ubuf_off);
         TSG_HIP(hipGetLastError());
         TSG_TRY(scan_exclusive_i64(cx, ubuf_off, nunits1 + 1, s));
-        long long slots = 0;
         TSG_TRY(read_i64(cx, ubuf_off + nunits1, &slots, s));
         const double est = (double)Ael->nnz * ((double)Bel->nnz / (double)(Bel->m > 0 ? Bel->m : 1));
         if ((double)slots <= 2.0 * est + (double)(1 << 26) && slots < (1LL << 31) &&
@@ -2472,6 +2478,21 @@ int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_d
     long long tile_products = cx.pinned64[0];
     C.numtile = numblkC;
     const size_t nb1 = (size_t)numblkC + 1;
+    if (tbase_out) *tbase_out = nullptr;
+    // (only while the buffers are at most 2x the compacted tiles: step 2's mask
+    // array is sized by the index space)
+    if (ubuf && nwin == 1 && tbase_out && slots <= 2 * numblk64 + (1 << 20)) {
+        // the caller indexes C tiles in unit-buffer space (tile row i's columns
+        // start at ubuf_off[i]): no compaction; C.tile_columnidx is the buffer
+        C.tile_columnidx = ubuf;
+        *tbase_out = ubuf_off;
+        *tslots_out = slots;
+        cx.put(bmst);
+        cx.put(ucnt);
+        cx.put(prod);
+        *tile_products_out = tile_products;
+        return TSG_OK;
+    }
     TSG_TRY(cx.get(&C.tile_columnidx, nb1));
     if (tilemA > 0) {
         if (ubuf)
@@ -2530,10 +2551,15 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
                                                                     Bcsr->rowpointer, ebnd);
         TSG_HIP(hipGetLastError());
     }
+    // CSR path: C tiles indexed in step 1's unit-buffer space when it allows (no
+    // column compaction; C's tile arrays are internal there)
+    long long *tbase = nullptr;
+    long long tslots = 0;  // size of the C tile index space: numblkC, or the unit-buffer slots
     TSG_TRY(dev_step1(cx, A, B, C, &tile_products, s, s1elem ? Acsr : nullptr, s1elem ? Bcsr : nullptr,
-                      s1elem ? ebnd : nullptr));
+                      s1elem ? ebnd : nullptr, (s1elem && !(g_ablate & 8192)) ? &tbase : nullptr, &tslots));
     const int numblkC = C.numtile;
     const size_t nb1 = (size_t)numblkC + 1;
+    if (!tbase) tslots = numblkC;
     if (ev) TSG_HIP(hipEventRecord(ev[1], s));
     // ---- step 2 ----
     int *uoff = nullptr, *urow = nullptr, *unit_rc = nullptr, *unit_rb = nullptr;
@@ -2544,14 +2570,14 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     TSG_TRY(cx.get(&utab, (size_t)maxu));
     TSG_TRY(cx.get(&unit_rc, (size_t)maxu * TM));
     if (!csr_out) TSG_TRY(cx.get(&C.tile_nnz, nb1));  // CSR path: row counts only, no tile nnz scan
-    TSG_TRY(cx.get(&C.mask, nb1 * CM<TM>::TW));
+    TSG_TRY(cx.get(&C.mask, ((size_t)tslots + 1) * CM<TM>::TW));
     // CSR path: step 2 hands step 3 a u16 code per C tile and full masks only for
     // tiles with > 1 nonzero (most webbase-like C tiles hold one nonzero)
     u16 *codeC = nullptr;
-    if (csr_out) TSG_TRY(cx.get(&codeC, nb1));
+    if (csr_out) TSG_TRY(cx.get(&codeC, (size_t)tslots + 1));
     k_units_per_row<<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(C.tile_ptr, tilemA, uoff);
     TSG_TRY(scan_exclusive_i32(cx, uoff, (long)tilemA + 1, s));
-    k_unit_rows<<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(uoff, C.tile_ptr, tilemA, urow, utab);
+    k_unit_rows<<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(uoff, C.tile_ptr, tilemA, urow, utab, tbase);
     if (C.tile_nnz) k_set_i32<<<1, 1, 0, s>>>(C.tile_nnz + numblkC, 0);
     TSG_HIP(hipGetLastError());
     int nunits = 0;
@@ -2683,6 +2709,7 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
                 "write %.1f gap %.1f  total %.3g\n", 100 * pr[0] / tot, 100 * pr[1] / tot, 100 * pr[2] / tot,
                 100 * pr[3] / tot, 100 * pr[4] / tot, 100 * pr[7] / tot, tot);
     }
+    cx.put(tbase);
     cx.put(esplit);
     cx.put(ebase);
     cx.put(etab);
