@@ -773,8 +773,15 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
     // column-sorted.  Sparse tiles (few nonzeros per A tile, e.g. web graphs) then
     // need only the tile STRUCTURE of A and B; denser tiles keep the full
     // csr2tile payloads for step 2's tile-level mask ORs.
-    bool bsorted = false;
-    TSG_TRY(dev_rows_sorted(cx, *B, &bsorted, s));
+    // The sortedness check is queued ahead of A's tile counts; both results come
+    // back with the counts' host round trip.  (With unsorted B rows the counts are
+    // discarded: the full csr2tile below rebuilds A's tiles.)
+    TSG_TRY(dev_rows_sorted_async(cx, *B, cx.pinned + 1, s));
+    const char *md = getenv("TSG_STEP2_MODE");
+    const int forced = !md ? -1 : !strcmp(md, "elem") ? 1 : !strcmp(md, "tile") ? 0 : -1;
+    const double skip = forced == 1 ? 1e300 : forced == 0 ? 0.0 : kStep2ElemMaxTileDensity;
+    TSG_TRY(dev_tile_structure(cx, *A, tm, tn, tA, s, skip));  // synchronises the stream
+    const bool bsorted = cx.pinned[1] == 0;
     const bool alias = A->rowpointer == B->rowpointer && A->columnindex == B->columnindex && A->m == B->m &&
                        A->n == B->n && tm == tn;
     bool s2elem = false, b_is_a = false;
@@ -783,10 +790,6 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
         // step 2's tile-level ORs read (no sort-based csr2tile on this path)
         // element streaming throughout (sparse tiles) builds C's structure from the
         // CSR operands: then A's and B's tile counts are all that is needed
-        const char *md = getenv("TSG_STEP2_MODE");
-        const int forced = !md ? -1 : !strcmp(md, "elem") ? 1 : !strcmp(md, "tile") ? 0 : -1;
-        const double skip = forced == 1 ? 1e300 : forced == 0 ? 0.0 : kStep2ElemMaxTileDensity;
-        TSG_TRY(dev_tile_structure(cx, *A, tm, tn, tA, s, skip));
         s2elem = forced >= 0 ? forced == 1 : (double)A->nnz < kStep2ElemMaxTileDensity * (double)tA.numtile;
         if (alias) {
             tB = tA;
@@ -800,6 +803,7 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
             else TSG_TRY(dev_tile_masks(cx, *B, tB, &tB.rm_mask, s));
         }
     } else {  // unsorted B rows: full csr2tile, tile-payload steps 2 and 3
+        release_tiles(cx, tA);
         TSG_TRY(dev_csr2tile_row_major(cx, *A, tm, tn, tA, s));
         TSG_TRY(dev_csr2tile_col_major(cx, *B, tm, tn, tB, s));
     }

@@ -289,25 +289,38 @@ __global__ void k_set_i64(long long *p, long long v);
 // int32 exclusive scan whose block partials run in int64: *total = the exact
 // sum (read back synchronously); TSG_ERR_OVERFLOW, with `a` left unscanned,
 // when it does not fit an int32 index (C tile counts, nnz(C)).
-int scan_exclusive_i32_total(Context &cx, int *a, long n, hipStream_t s, long long *total) {
+// Exclusive int32 scan whose int64 total is read back to the host.  The apply
+// kernel is queued before the read (the host round trip overlaps it); a total
+// past INT_MAX returns TSG_ERR_OVERFLOW (the scanned values are then invalid).
+// `before_read` (optional) queues more work ahead of the read, and extra_d
+// (optional) is read back into *extra_h by the same host synchronisation.
+template <class Fn>
+static int scan_i32_total_impl(Context &cx, int *a, long n, hipStream_t s, long long *total, Fn &&before_read,
+                               const long long *extra_d, long long *extra_h) {
     *total = 0;
-    if (n <= 0) return TSG_OK;
-    const long nb = (n + SCAN_TILE - 1) / SCAN_TILE;
     long long *part = nullptr;
-    TSG_TRY(cx.get(&part, (size_t)nb + 1));
-    k_scan_reduce_wide<<<(unsigned)nb, WG, 0, s>>>(a, n, part);
-    k_set_i64<<<1, 1, 0, s>>>(part + nb, 0);
-    TSG_HIP(hipGetLastError());
-    TSG_TRY(scan_exclusive(cx, part, nb + 1, s));
-    TSG_TRY(read_i64(cx, part + nb, total, s));
-    if (*total > 0x7fffffffll) {
-        cx.put(part);
-        return TSG_ERR_OVERFLOW;
+    long nb = 0;
+    if (n > 0) {
+        nb = (n + SCAN_TILE - 1) / SCAN_TILE;
+        TSG_TRY(cx.get(&part, (size_t)nb + 1));
+        k_scan_reduce_wide<<<(unsigned)nb, WG, 0, s>>>(a, n, part);
+        k_set_i64<<<1, 1, 0, s>>>(part + nb, 0);
+        TSG_HIP(hipGetLastError());
+        TSG_TRY(scan_exclusive(cx, part, nb + 1, s));
+        k_scan_apply<int, long long><<<(unsigned)nb, WG, 0, s>>>(a, n, part);
+        TSG_HIP(hipGetLastError());
     }
-    k_scan_apply<int, long long><<<(unsigned)nb, WG, 0, s>>>(a, n, part);
-    TSG_HIP(hipGetLastError());
+    before_read();
+    if (part) TSG_HIP(hipMemcpyAsync(cx.pinned64, part + nb, sizeof(long long), hipMemcpyDeviceToHost, s));
+    if (extra_d) TSG_HIP(hipMemcpyAsync(cx.pinned64 + 1, extra_d, sizeof(long long), hipMemcpyDeviceToHost, s));
+    if (part || extra_d) TSG_HIP(hipStreamSynchronize(s));
+    if (part) *total = cx.pinned64[0];
+    if (extra_d) *extra_h = cx.pinned64[1];
     cx.put(part);
-    return TSG_OK;
+    return *total > 0x7fffffffll ? TSG_ERR_OVERFLOW : TSG_OK;
+}
+int scan_exclusive_i32_total(Context &cx, int *a, long n, hipStream_t s, long long *total) {
+    return scan_i32_total_impl(cx, a, n, s, total, [] {}, nullptr, nullptr);
 }
 int scan_exclusive_i64(Context &cx, long long *a, long n, hipStream_t s) {
     return scan_exclusive(cx, a, n, s);
@@ -1454,7 +1467,9 @@ __global__ __launch_bounds__(WG) void k_rows_unsorted3(const int *rp, const int 
         if (ci[p] < ci[p - 1] && !((bits[p >> 5] >> (p & 31)) & 1u)) *flag = 1;
 }
 
-int dev_rows_sorted(Context &cx, const tsg_dev_csr &M, bool *sorted, hipStream_t s) {
+// Queued only: the flag (1: some row is not column-sorted) lands in *host_flag
+// (pinned) at the caller's next stream synchronisation.
+int dev_rows_sorted_async(Context &cx, const tsg_dev_csr &M, int *host_flag, hipStream_t s) {
     int *flag = nullptr;
     TSG_TRY(cx.get(&flag, 1));
     TSG_HIP(hipMemsetAsync(flag, 0, sizeof(int), s));
@@ -1467,11 +1482,15 @@ int dev_rows_sorted(Context &cx, const tsg_dev_csr &M, bool *sorted, hipStream_t
         k_rows_unsorted3<<<grid_for(M.nnz, WG, 16384), WG, 0, s>>>(M.rowpointer, M.columnindex, M.m, bits, flag);
     }
     TSG_HIP(hipGetLastError());
-    int f = 0;
-    TSG_TRY(read_i32(cx, flag, &f, s));
-    cx.put(bits);
+    TSG_HIP(hipMemcpyAsync(host_flag, flag, sizeof(int), hipMemcpyDeviceToHost, s));
+    cx.put(bits);  // the pool's reuse is stream-ordered
     cx.put(flag);
-    *sorted = (f == 0);
+    return TSG_OK;
+}
+int dev_rows_sorted(Context &cx, const tsg_dev_csr &M, bool *sorted, hipStream_t s) {
+    TSG_TRY(dev_rows_sorted_async(cx, M, cx.pinned + 1, s));
+    TSG_HIP(hipStreamSynchronize(s));
+    *sorted = cx.pinned[1] == 0;
     return TSG_OK;
 }
 
@@ -2469,13 +2488,13 @@ int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_d
                                          nwin, win, ucnt, nullptr, nullptr, prod, bmst);
     }
     TSG_HIP(hipGetLastError());
-    long long numblk64 = 0;
-    TSG_TRY(scan_exclusive_i32_total(cx, ucnt, nunits1 + 1, s, &numblk64));  // overflow: > INT_MAX C tiles
-    k_rows_from_units<<<grid_for(tilemA + 1, WG, 4096), WG, 0, s>>>(ucnt, tilemA, nwin, C.tile_ptr);
-    TSG_HIP(hipMemcpyAsync(cx.pinned64, prod, sizeof(u64), hipMemcpyDeviceToHost, s));
-    TSG_HIP(hipStreamSynchronize(s));
+    long long numblk64 = 0, tile_products = 0;
+    // one host round trip for the C tile count (overflow: > INT_MAX C tiles) and the product count
+    TSG_TRY(scan_i32_total_impl(
+        cx, ucnt, nunits1 + 1, s, &numblk64,
+        [&] { k_rows_from_units<<<grid_for(tilemA + 1, WG, 4096), WG, 0, s>>>(ucnt, tilemA, nwin, C.tile_ptr); },
+        reinterpret_cast<const long long *>(prod), &tile_products));
     const int numblkC = (int)numblk64;
-    long long tile_products = cx.pinned64[0];
     C.numtile = numblkC;
     const size_t nb1 = (size_t)numblkC + 1;
     if (tbase_out) *tbase_out = nullptr;
@@ -2580,8 +2599,20 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     k_unit_rows<<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(uoff, C.tile_ptr, tilemA, urow, utab, tbase);
     if (C.tile_nnz) k_set_i32<<<1, 1, 0, s>>>(C.tile_nnz + numblkC, 0);
     TSG_HIP(hipGetLastError());
+    // element split tables: sizes queued ahead of the unit count's read (one round trip)
+    long long *ebase = nullptr;
+    if (s2elem || s3elem) {
+        TSG_TRY(cx.get(&ebase, (size_t)tilemA + 1));
+        k_esplit_counts<TM><<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(uoff, Acsr->rowpointer, A.m, tilemA, ebase);
+        TSG_TRY(scan_exclusive_i64(cx, ebase, (long)tilemA + 1, s));
+    }
     int nunits = 0;
-    TSG_TRY(read_i32(cx, uoff + tilemA, &nunits, s));
+    long long ne = 0;
+    TSG_HIP(hipMemcpyAsync(cx.pinned, uoff + tilemA, sizeof(int), hipMemcpyDeviceToHost, s));
+    if (ebase) TSG_HIP(hipMemcpyAsync(cx.pinned64, ebase + tilemA, sizeof(long long), hipMemcpyDeviceToHost, s));
+    TSG_HIP(hipStreamSynchronize(s));
+    nunits = cx.pinned[0];
+    if (ebase) ne = cx.pinned64[0];
     const int gu = grid_for(maxu, 1, 16384);
     // tile-product split points: every A tile's B tile row cut at its C tile row's unit boundaries
     long long *sbase = nullptr;
@@ -2611,14 +2642,8 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     // element split points: every A entry's B CSR row cut at the unit boundaries (+ row end)
     ECsr E{};
     int *esplit = nullptr;
-    long long *ebase = nullptr;
     int4 *etab = nullptr;
     if (s2elem || s3elem) {
-        TSG_TRY(cx.get(&ebase, (size_t)tilemA + 1));
-        k_esplit_counts<TM><<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(uoff, Acsr->rowpointer, A.m, tilemA, ebase);
-        TSG_TRY(scan_exclusive_i64(cx, ebase, (long)tilemA + 1, s));
-        long long ne = 0;
-        TSG_TRY(read_i64(cx, ebase + tilemA, &ne, s));
         TSG_TRY(cx.get(&esplit, (size_t)ne + 1));
         E = ECsr{A.m, Acsr->rowpointer, Acsr->columnindex, Acsr->value, Bcsr->rowpointer, Bcsr->columnindex,
                  Bcsr->value, esplit, ebase};

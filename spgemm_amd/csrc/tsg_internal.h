@@ -108,6 +108,7 @@ int dev_tile_structure(Context &cx, const tsg_dev_csr &M, int tr, int tc, tsg_de
 int dev_tile_masks(Context &cx, const tsg_dev_csr &M, tsg_dev_tiles &t, uint16_t **mask_out, hipStream_t s);
 // whether every CSR row is column-sorted (synchronous)
 int dev_rows_sorted(Context &cx, const tsg_dev_csr &M, bool *sorted, hipStream_t s);
+int dev_rows_sorted_async(Context &cx, const tsg_dev_csr &M, int *host_flag, hipStream_t s);
 int dev_tile2csr(Context &cx, const tsg_dev_tiles &C, tsg_dev_csr &out, hipStream_t s);
 
 // read a device int / long long synchronously through pinned memory
