@@ -282,9 +282,8 @@ __global__ __launch_bounds__(WG) void k_scan_reduce_wide(const int *a, long n, l
     }
     const long long tot = block_sum(s, red);
     if (threadIdx.x == 0) part[blockIdx.x] = tot;
+    if (blockIdx.x == 0 && threadIdx.x == 0) part[gridDim.x] = 0;  // the "n+1 scan" slot of the partials
 }
-
-__global__ void k_set_i64(long long *p, long long v);
 
 // int32 exclusive scan whose block partials run in int64: *total = the exact
 // sum (read back synchronously); TSG_ERR_OVERFLOW, with `a` left unscanned,
@@ -304,7 +303,6 @@ static int scan_i32_total_impl(Context &cx, int *a, long n, hipStream_t s, long 
         nb = (n + SCAN_TILE - 1) / SCAN_TILE;
         TSG_TRY(cx.get(&part, (size_t)nb + 1));
         k_scan_reduce_wide<<<(unsigned)nb, WG, 0, s>>>(a, n, part);
-        k_set_i64<<<1, 1, 0, s>>>(part + nb, 0);
         TSG_HIP(hipGetLastError());
         TSG_TRY(scan_exclusive(cx, part, nb + 1, s));
         k_scan_apply<int, long long><<<(unsigned)nb, WG, 0, s>>>(a, n, part);
@@ -1201,15 +1199,30 @@ __global__ __launch_bounds__(WG) void k_step1(const int *Aptr, const int *Acol, 
 
 // EL step 1 unit-buffer capacities: wave per A tile row, its element products
 // P (sum of its entries' B row lengths); every window of the row gets
-// min(P, window width) slots.
-__global__ __launch_bounds__(WG) void k_step1_cap(const int *Aptr, int mA, const int2 *ebnd, int tilemA, int nwin,
-                                                  int win, int tilenB, long long *cap) {
+// min(P, window width) slots.  With ciA / rpB it also fills the per-entry B
+// row bounds ebnd (k_entry_bounds fused: the tile rows cover every entry once).
+__global__ __launch_bounds__(WG) void k_step1_cap(const int *Aptr, int mA, int2 *ebnd, int tilemA, int nwin,
+                                                  int win, int tilenB, long long *cap, const int *ciA,
+                                                  const int *rpB, u64 *prod, int *ucnt) {
     const int lane = threadIdx.x & 63;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // step 1's counters and the scans' n+1 slots
+        const long nu = (long)tilemA * nwin;
+        *prod = 0;
+        ucnt[nu] = 0;
+        cap[nu] = 0;
+    }
     for (long i = ((long)blockIdx.x * WG + threadIdx.x) >> 6; i < tilemA; i += ((long)gridDim.x * WG) >> 6) {
         const int a0 = Aptr[min((int)i * 16, mA)], a1 = Aptr[min((int)i * 16 + 16, mA)];
         long long p = 0;
         for (int a = a0 + lane; a < a1; a += 64) {
-            const int2 e = ebnd[a];
+            int2 e;
+            if (ciA) {
+                const int k = ciA[a];
+                e = make_int2(rpB[k], rpB[k + 1]);
+                ebnd[a] = e;
+            } else {
+                e = ebnd[a];
+            }
             p += e.y - e.x;
         }
         p = wave_sum(p);
@@ -1290,6 +1303,7 @@ __global__ __launch_bounds__(WG) void k_tstruct(const int *rowptr, const int *co
 // k_tstruct's bitmap.
 constexpr int TC_SLOTS = 512;
 __global__ __launch_bounds__(WG) void k_tcount16(const int *rowptr, const int *col, int m, int tilem, int *unit_cnt) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) unit_cnt[tilem] = 0;  // the scan's n+1 slot
     __shared__ __align__(16) u32 ht_all[WAVES * TC_SLOTS];
     u32 *ht = ht_all + wave_id() * TC_SLOTS;
     const int lane = lane_id();
@@ -1376,10 +1390,10 @@ int dev_tile_structure(Context &cx, const tsg_dev_csr &M, int tr, int tc, tsg_de
     int *ucnt = nullptr;
     TSG_TRY(cx.get(&ucnt, (size_t)nunits + 1));
     TSG_TRY(cx.get(&out.tile_ptr, (size_t)out.tilem + 1));
-    TSG_HIP(hipMemsetAsync(ucnt + nunits, 0, sizeof(int), s));
     const int g = grid_for(nunits, 1, 16384);
+    const bool wave16 = out.tilem > 0 && tr == 16 && tc == 16 && nwin == 1 && !(ablate_bits() & 2048);
+    if (!wave16) TSG_HIP(hipMemsetAsync(ucnt + nunits, 0, sizeof(int), s));  // (k_tcount16 zeroes it)
     if (out.tilem > 0) {
-        const bool wave16 = tr == 16 && tc == 16 && nwin == 1 && !(ablate_bits() & 2048);
         if (wave16) {  // wave per tile row; the (rare) tile rows over 1024 entries then take the bitmap
             k_tcount16<<<grid_for((long)out.tilem * 64, WG, 16384), WG, 0, s>>>(M.rowpointer, M.columnindex, M.m,
                                                                                out.tilem, ucnt);
@@ -1453,7 +1467,8 @@ __global__ __launch_bounds__(WG) void k_entry_bounds(const int *ciA, long nnzA, 
 }
 
 // row starts as a bitmap over entry positions (bit p set: some non-empty row starts at p)
-__global__ __launch_bounds__(WG) void k_row_start_bits(const int *rp, int m, u32 *bits) {
+__global__ __launch_bounds__(WG) void k_row_start_bits(const int *rp, int m, u32 *bits, int *flag) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *flag = 0;  // (k_rows_unsorted3 sets it)
     for (int r = blockIdx.x * WG + threadIdx.x; r < m; r += gridDim.x * WG) {
         const int p = rp[r];
         if (p < rp[r + 1]) atomicOr(&bits[p >> 5], 1u << (p & 31));
@@ -1472,13 +1487,13 @@ __global__ __launch_bounds__(WG) void k_rows_unsorted3(const int *rp, const int 
 int dev_rows_sorted_async(Context &cx, const tsg_dev_csr &M, int *host_flag, hipStream_t s) {
     int *flag = nullptr;
     TSG_TRY(cx.get(&flag, 1));
-    TSG_HIP(hipMemsetAsync(flag, 0, sizeof(int), s));
     u32 *bits = nullptr;
+    if (!(M.m > 0 && M.nnz > 1)) TSG_HIP(hipMemsetAsync(flag, 0, sizeof(int), s));
     if (M.m > 0 && M.nnz > 1) {
         const size_t nw = ((size_t)M.nnz + 31) / 32;
         TSG_TRY(cx.get(&bits, nw));
         TSG_HIP(hipMemsetAsync(bits, 0, nw * sizeof(u32), s));
-        k_row_start_bits<<<grid_for(M.m, WG, 16384), WG, 0, s>>>(M.rowpointer, M.m, bits);
+        k_row_start_bits<<<grid_for(M.m, WG, 16384), WG, 0, s>>>(M.rowpointer, M.m, bits, flag);
         k_rows_unsorted3<<<grid_for(M.nnz, WG, 16384), WG, 0, s>>>(M.rowpointer, M.columnindex, M.m, bits, flag);
     }
     TSG_HIP(hipGetLastError());
@@ -2425,7 +2440,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(RST ? 5 : TS
 // tiles only; the CSR path, whose C tiles are internal).
 int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_dev_tiles &C,
               long long *tile_products_out, hipStream_t s, const tsg_dev_csr *Ael, const tsg_dev_csr *Bel,
-              const int2 *ebnd, long long **tbase_out, long long *tslots_out) {
+              int2 *ebnd, long long **tbase_out, long long *tslots_out, bool fill_ebnd) {
     const bool el = Ael && Bel;  // element-level structure (16x16 tiles, CSR operands)
     const int tilemA = A.tilem, tilenB = B.tilen;
     int win, nwin;
@@ -2437,9 +2452,12 @@ int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_d
     TSG_TRY(cx.get(&ucnt, (size_t)nunits1 + 1));
     TSG_TRY(cx.get(&prod, 1));
     TSG_TRY(cx.get(&C.tile_ptr, (size_t)tilemA + 1));
-    TSG_HIP(hipMemsetAsync(prod, 0, sizeof(u64), s));
-    TSG_HIP(hipMemsetAsync(ucnt + nunits1, 0, sizeof(int), s));
     const int g1 = grid_for(nunits1, 1, 16384);
+    const bool capk = el && ebnd && tilemA > 0 && !(ablate_bits() & 512);  // k_step1_cap runs (and zeroes these)
+    if (!capk) {
+        TSG_HIP(hipMemsetAsync(prod, 0, sizeof(u64), s));
+        TSG_HIP(hipMemsetAsync(ucnt + nunits1, 0, sizeof(int), s));
+    }
     // keep each unit's bitmask (window/8 bytes) for the emit pass when that fits
     // 4 GiB: one tile-product enumeration instead of two
     // (and when the products per unit -- estimated from the mean B tile row --
@@ -2450,11 +2468,17 @@ int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_d
     int *ubuf = nullptr;
     long long *ubuf_off = nullptr;
     long long slots = 0;
-    if (el && ebnd && tilemA > 0 && !(ablate_bits() & 512)) {
+    if (fill_ebnd && !capk) {  // no capacity kernel to fuse into
+        k_entry_bounds<<<grid_for(Ael->nnz, WG, 16384), WG, 0, s>>>(Ael->columnindex, Ael->nnz, Bel->rowpointer,
+                                                                   ebnd);
+        fill_ebnd = false;
+    }
+    if (capk) {
         TSG_TRY(cx.get(&ubuf_off, (size_t)nunits1 + 1));
-        TSG_HIP(hipMemsetAsync(ubuf_off + nunits1, 0, sizeof(long long), s));
-        k_step1_cap<<<grid_for((long)tilemA * 64, WG, 8192), WG, 0, s>>>(Ael->rowpointer, Ael->m, ebnd, tilemA, nwin,
-                                                                         win, tilenB, ubuf_off);
+        k_step1_cap<<<grid_for((long)tilemA * 64, WG, 8192), WG, 0, s>>>(
+            Ael->rowpointer, Ael->m, ebnd, tilemA, nwin, win, tilenB, ubuf_off,
+            fill_ebnd ? Ael->columnindex : nullptr, fill_ebnd ? Bel->rowpointer : nullptr, prod, ucnt);
+        fill_ebnd = false;
         TSG_HIP(hipGetLastError());
         TSG_TRY(scan_exclusive_i64(cx, ubuf_off, nunits1 + 1, s));
         TSG_TRY(read_i64(cx, ubuf_off + nunits1, &slots, s));
@@ -2566,16 +2590,19 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     int2 *ebnd = nullptr;
     if ((s2elem || s3elem) && Acsr->nnz > 0) {
         TSG_TRY(cx.get(&ebnd, (size_t)Acsr->nnz + 1));
-        k_entry_bounds<<<grid_for(Acsr->nnz, WG, 16384), WG, 0, s>>>(Acsr->columnindex, Acsr->nnz,
-                                                                    Bcsr->rowpointer, ebnd);
-        TSG_HIP(hipGetLastError());
+        if (!s1elem) {  // (element step 1 fills them in its capacity kernel)
+            k_entry_bounds<<<grid_for(Acsr->nnz, WG, 16384), WG, 0, s>>>(Acsr->columnindex, Acsr->nnz,
+                                                                        Bcsr->rowpointer, ebnd);
+            TSG_HIP(hipGetLastError());
+        }
     }
     // CSR path: C tiles indexed in step 1's unit-buffer space when it allows (no
     // column compaction; C's tile arrays are internal there)
     long long *tbase = nullptr;
     long long tslots = 0;  // size of the C tile index space: numblkC, or the unit-buffer slots
     TSG_TRY(dev_step1(cx, A, B, C, &tile_products, s, s1elem ? Acsr : nullptr, s1elem ? Bcsr : nullptr,
-                      s1elem ? ebnd : nullptr, (s1elem && !(g_ablate & 8192)) ? &tbase : nullptr, &tslots));
+                      s1elem ? ebnd : nullptr, (s1elem && !(g_ablate & 8192)) ? &tbase : nullptr, &tslots,
+                      s1elem && ebnd));
     const int numblkC = C.numtile;
     const size_t nb1 = (size_t)numblkC + 1;
     if (!tbase) tslots = numblkC;

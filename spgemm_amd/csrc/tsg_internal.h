@@ -96,8 +96,8 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
 // step 1 alone: C tile structure (tile_ptr, tile_columnidx, numtile) of any tile size
 int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_dev_tiles &C,
               long long *tile_products, hipStream_t s, const tsg_dev_csr *Ael = nullptr,
-              const tsg_dev_csr *Bel = nullptr, const int2 *ebnd = nullptr,
-              long long **tbase_out = nullptr, long long *tslots_out = nullptr);
+              const tsg_dev_csr *Bel = nullptr, int2 *ebnd = nullptr,
+              long long **tbase_out = nullptr, long long *tslots_out = nullptr, bool fill_ebnd = false);
 // C payload for a step-1 structure C (tile_m set) from the non-empty tiles Cne of C's CSR
 int dev_retile_c(Context &cx, const tsg_dev_tiles &Cne, tsg_dev_tiles &C, hipStream_t s);
 // tile_ptr + tile_columnidx of a CSR's tiling (tr x tc tiles), no payload;
