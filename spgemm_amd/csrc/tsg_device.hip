@@ -1528,7 +1528,7 @@ constexpr int CH = 256;          // C tiles per unit
 #define TSG_S3WPE 6
 #endif
 #ifndef TSG_S2WPE
-#define TSG_S2WPE 6
+#define TSG_S2WPE 8
 #endif
 constexpr int S3_NZCAP = TSG_S3CAP;  // fp64 accumulator slots per numeric pass
 
