@@ -795,7 +795,20 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
             tB = tA;
             b_is_a = true;
         } else {
-            TSG_TRY(dev_tile_structure(cx, *B, tn, tm, tB, s, s2elem ? 1e300 : 0.0));
+            const int rc = dev_tile_structure(cx, *B, tn, tm, tB, s, s2elem ? 1e300 : 0.0);
+            if (rc == TSG_ERR_UNSUPPORTED && s2elem) {
+                // B's tile count is a statistic on the element path (steps 1-3 read
+                // B's CSR).  A B too wide for the (tile row, window) count units --
+                // e.g. mawi, 14 M tile rows x 216 windows -- is reported as -1.
+                tB = tsg_dev_tiles{};
+                tB.m = B->m; tB.n = B->n; tB.nnz = B->nnz;
+                tB.tile_m = tn; tB.tile_n = tm;
+                tB.tilem = (B->m + tn - 1) / tn;
+                tB.tilen = (B->n + tm - 1) / tm;
+                tB.numtile = -1;
+            } else {
+                TSG_TRY(rc);
+            }
         }
         if (!s2elem) {
             TSG_TRY(dev_tile_masks(cx, *A, tA, &tA.mask, s));

@@ -2442,6 +2442,7 @@ int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_d
               long long *tile_products_out, hipStream_t s, const tsg_dev_csr *Ael, const tsg_dev_csr *Bel,
               int2 *ebnd, long long **tbase_out, long long *tslots_out, bool fill_ebnd) {
     const bool el = Ael && Bel;  // element-level structure (16x16 tiles, CSR operands)
+    if (el && !ebnd && Ael->nnz > 0) return TSG_ERR_INVALID;  // the element walks read the entry bounds
     const int tilemA = A.tilem, tilenB = B.tilen;
     int win, nwin;
     window_for(tilenB, &win, &nwin);
@@ -2546,7 +2547,7 @@ int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_d
         else if (el)
             k_step1<1, true><<<g1, WG, 0, s>>>(Ael->rowpointer, Ael->columnindex, Bel->rowpointer, Bel->columnindex,
                                                tilemA, tilenB, nwin, win, nullptr, ucnt, C.tile_columnidx, nullptr,
-                                               nullptr, Ael->m);
+                                               nullptr, Ael->m, ebnd);  // (the element walk reads ebnd)
         else
             k_step1<1><<<g1, WG, 0, s>>>(A.tile_ptr, A.tile_columnidx, B.tile_ptr, B.tile_columnidx, tilemA, tilenB,
                                          nwin, win, nullptr, ucnt, C.tile_columnidx, nullptr, nullptr);
