@@ -73,7 +73,8 @@ typedef struct tsg_stats {
     double t_kern_ms;      /* steps 1-3 incl. allocation (reference's timer)     */
     double t_e2e_ms;       /* device CSR in -> device CSR out                   */
     long long nnzCub;      /* sum_{a in A} rowlen_B(col(a))                     */
-    long long numtileA, numtileB, numblkC, nnzC;
+    long long numtileA, numtileB, numblkC, nnzC;  /* numtileB = -1: not counted (B too wide
+                                                      for the count units; CSR path only) */
     long long tile_products; /* tile-level intermediate products (step-1 work)  */
     double t_step3_kernel_ms;  /* the step-3 numeric kernel alone (dominant kernel) */
 } tsg_stats;
