@@ -2699,6 +2699,9 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     }
     TSG_HIP(hipGetLastError());
     long long nnz64 = 0;
+    // element path: nnz(C) is bounded by the element products (known on the host
+    // since step 1), so its read-back waits for the end of the pipeline
+    const bool defer_nnz = csr_out && s1elem && tile_products <= 0x7ffffffell && !(g_ablate & 16384);
     if (!csr_out) TSG_TRY(scan_exclusive_i32_total(cx, C.tile_nnz, (long)numblkC + 1, s, &nnz64));  // fits int32
     if (csr_out) {
         csr_out->m = A.m;
@@ -2710,9 +2713,13 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
             k_unit_rowbase<TM><<<grid_for((long)tilemA * TM, WG, 8192), WG, 0, s>>>(uoff, tilemA, A.m, unit_rc, unit_rb,
                                                                                   csr_out->rowpointer);
         TSG_HIP(hipGetLastError());
-        TSG_TRY(scan_exclusive_i32_total(cx, csr_out->rowpointer, (long)A.m + 1, s, &nnz64));  // nnz(C) fits int32
+        if (defer_nnz)  // nnz(C) <= element products <= INT_MAX: read back after step 3
+            TSG_TRY(scan_exclusive_i32(cx, csr_out->rowpointer, (long)A.m + 1, s));
+        else
+            TSG_TRY(scan_exclusive_i32_total(cx, csr_out->rowpointer, (long)A.m + 1, s, &nnz64));  // fits int32
     }
-    const int nnzC = (int)nnz64;
+    // (deferred: the element-product bound sizes step 3's outputs)
+    int nnzC = defer_nnz ? (int)tile_products : (int)nnz64;
     C.nnz = nnzC;
     if (ev) TSG_HIP(hipEventRecord(ev[2], s));
     // ---- step 3 ----
@@ -2727,7 +2734,7 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     }
     if (ev) TSG_HIP(hipEventRecord(ev[4], s));
     if (csr_out) {
-        if (nnzC > 0) {
+        if (nnzC > 0 || defer_nnz) {
             if (s3elem && !s2elem)  // denser tiles: row-start table
                 k_step3<TM, TN, true, false, true, true><<<gu, WG, 0, s>>>(
                     utab, etab, nunits, A.m, V, E, C.tile_columnidx, C.tile_nnz, C.mask, codeC, unit_rb,
@@ -2776,6 +2783,13 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     cx.put(split);
     cx.put(sbase);
     if (ev) TSG_HIP(hipEventRecord(ev[3], s));
+    if (defer_nnz) {  // the pipeline's one read-back after step 3
+        TSG_HIP(hipMemcpyAsync(cx.pinned, csr_out->rowpointer + A.m, sizeof(int), hipMemcpyDeviceToHost, s));
+        TSG_HIP(hipStreamSynchronize(s));
+        nnzC = cx.pinned[0];
+        C.nnz = nnzC;
+        csr_out->nnz = nnzC;
+    }
     if (st) {
         st->numblkC = numblkC;
         st->nnzC = nnzC;
