@@ -2123,7 +2123,8 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(RST ? 5 : TS
     __shared__ int s_rp[TM + 1];            // A CSR row starts of the tile row (ELEM)
     __shared__ unsigned char s_r[WG];
     __shared__ unsigned char s_key[S3_NZCAP];  // pass nonzero e: r << 4 | c
-    __shared__ u16 s_kt[S3_NZCAP];             // pass nonzero e: its tile
+    static_assert(CH <= 256, "a unit's tile index fits a byte");
+    __shared__ unsigned char s_kt[S3_NZCAP];   // pass nonzero e: its tile
     __shared__ unsigned char s_rs[RST ? CH * TM : 1];  // [tile][r]: in-tile rank of row r's first nonzero
     __shared__ int s_wcnt[WAVES][TM];       // per-wave row counts of the current 256 nonzeros
     __shared__ int s_run[TM];               // row-r nonzeros of this pass already placed
@@ -2363,7 +2364,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(RST ? 5 : TS
                     while (v) {
                         const int hb = 31 - __clz(v);  // MSB-first: lowest column first
                         s_key[e] = (unsigned char)((r << 4) | (15 - hb));
-                        s_kt[e++] = (u16)j;
+                        s_kt[e++] = (unsigned char)j;
                         v &= ~(1u << hb);
                     }
                 }
