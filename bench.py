@@ -121,8 +121,13 @@ def pmc_traffic(kernel, workload):
     the same workload (profiles/<round>_pmc.json, written by tools/profile.sh:
     2*FETCH_SIZE + WRITE_SIZE, separate --pmc passes).  (None, None) when absent."""
     import glob
+    def workload_of(f):
+        try:
+            return json.load(open(f)).get("_workload")
+        except (OSError, ValueError, AttributeError):  # unreadable / partial summary
+            return None
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc.json")))
-    files = [f for f in files if json.load(open(f)).get("_workload") == workload]
+    files = [f for f in files if workload_of(f) == workload]
     if not files:
         return None, None
     d = json.load(open(files[-1]))
