@@ -1811,9 +1811,11 @@ __device__ __forceinline__ EPre epre_load(const ECsr &E, int4 ue, bool with_va) 
     return p;
 }
 
-template <int TM, class F>
+// s_r: the A row (0..15) of each entry of a batch, in LDS (measured: int in
+// step 2, u8 in step 3)
+template <int TM, class SR, class F>
 __device__ __forceinline__ void elem_stream(const ECsr &E, int4 ue, const EPre &pre, const int *s_rp, bool narrow,
-                                            int clo, int chi, unsigned char *s_r, double *s_va, ProdLds &L, F &&f) {
+                                            int clo, int chi, SR *s_r, double *s_va, ProdLds &L, F &&f) {
     const int e0 = ue.x, ei = ue.y;
     const int *sp0 = etab_split(E, ue);
     for (int eb = 0; eb < ei; eb += WG) {
@@ -1825,7 +1827,7 @@ __device__ __forceinline__ void elem_stream(const ECsr &E, int4 ue, const EPre &
 #pragma unroll
             for (int st = TM / 2; st > 0; st >>= 1)
                 if (s_rp[r + st] <= p) r += st;
-            s_r[threadIdx.x] = (unsigned char)r;
+            s_r[threadIdx.x] = (SR)r;
             int be;
             if (eb == 0) {
                 bs = pre.bs;
@@ -1888,7 +1890,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(TSG_S2WPE)))
     __shared__ int s_cols[CH];
     __shared__ int s_rc[TM];
     __shared__ int s_rp[TM + 1];
-    __shared__ unsigned char s_r[WG];
+    __shared__ int s_r[WG];
     __shared__ int s_wm[WAVES];
     __shared__ ProdLds L;
     // Software pipeline over this workgroup's units (stride G): the unit tables
