@@ -1527,6 +1527,9 @@ constexpr int CH = 256;          // C tiles per unit
 #ifndef TSG_S3WPE
 #define TSG_S3WPE 6
 #endif
+#ifndef TSG_GU_CAP
+#define TSG_GU_CAP 65536  // measured: 16384 and 131072 both slower on webbase
+#endif
 #ifndef TSG_S2WPE
 #define TSG_S2WPE 8
 #endif
@@ -2644,7 +2647,7 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     TSG_HIP(hipStreamSynchronize(s));
     nunits = cx.pinned[0];
     if (ebase) ne = cx.pinned64[0];
-    const int gu = grid_for(maxu, 1, 16384);
+    const int gu = grid_for(maxu, 1, TSG_GU_CAP);  // workgroups of steps 2 and 3 (units strided over them)
     // tile-product split points: every A tile's B tile row cut at its C tile row's unit boundaries
     long long *sbase = nullptr;
     int *split = nullptr;
