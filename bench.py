@@ -7,16 +7,18 @@ step 3 + GPU tile2csr (SURVEY.md §8d t_e2e).  Inputs are resident in HBM
 (src/tilespgemm-cuda.h:2808).
 
   python bench.py                       # N=1, webbase-1M synthetic stand-in
-  python bench.py --gpus N ...          # under torch.distributed.run, weak scaling
-                                        # (default): rank r computes row block r of
-                                        # [A; A; ...; A] * B (one full A per rank, B
-                                        # replicated, C stays distributed: no
-                                        # data-path collective)
-  python bench.py --gpus N --scaling strong
-                                        # the fixed product A*B: A split by tile-row
-                                        # blocks of equal work, B replicated, C row
-                                        # blocks gathered to rank 0 over RCCL
-                                        # (inside the timed region)
+  python bench.py --gpus N ...          # under torch.distributed.run: the north-star
+                                        # (default, strong scaling): the fixed product
+                                        # A*B, A split by tile-row blocks of equal work,
+                                        # B replicated, C row blocks gathered to rank 0
+                                        # over RCCL inside the timed region
+  python bench.py --gpus N --scaling weak
+                                        # rank r computes row block r of [A; A; ...; A]*B
+                                        # (one full A per rank, C stays distributed)
+  python bench.py --matrix lj           # products past int32 nnz(C) (the reference's
+                                        # `int nnzC`, src/tilespgemm-cuda.h:2327) run as
+                                        # sequential tile-row blocks of <= 1.5e9 products
+                                        # each; every block's C stays on its device
 Rank 0 prints ONE JSON line.
 """
 import argparse
@@ -106,7 +108,13 @@ def cpu_baseline(m, n, rp, ci, vv, mb, nb, rpb, cib, vvb, budget_s):
     nrows, nt = _timed_prefix(lambda r: O.gustavson_rows(A, B, 0, r), m, budget_s / 2)
     ncub = nnzcub_rows(rp, ci, rpb, 0, nrows)
     thr = O.num_threads()
-    return {"value": round(2.0 * cub / t / 1e9, 4), "unit": "GFLOPS", "cores": thr,
+    nproc = os.cpu_count()
+    try:
+        nproc = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        pass
+    return {"value": round(2.0 * cub / t / 1e9, 4), "unit": "GFLOPS", "cores": thr, "nproc": nproc,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
             "kind": "port",
             "sample": f"spgemm_spa restatement (count+fill passes, symbolic), rows [0,{rows}) of {m} "
                       f"({cub} of the intermediate products), {t:.1f} s; {thr} OpenMP threads "
@@ -114,6 +122,35 @@ def cpu_baseline(m, n, rp, ci, vv, mb, nb, rpb, cib, vvb, budget_s):
             "numeric": {"value": round(2.0 * ncub / nt / 1e9, 4), "unit": "GFLOPS",
                         "sample": f"oracle Gustavson (dense-row accumulator, fp64 values), rows [0,{nrows}), "
                                   f"{nt:.1f} s"}}
+
+
+def tiled_leg(m, n, rp, ci, vv, mb, nb, rpb, cib, vvb, aat, tm, nnzcub, reps=3):
+    """The reference-layout drop-in path, timed like the reference: csr2tile of A
+    (row-major) and B (col-major) on the host API, then tsg_tilespgemm -- tiles
+    in, the reference's tiled C out (tile-pattern step 1 incl. empty C tiles,
+    step 2 masks + scan, step 3 values) -- whose time_tile is the reference's
+    timed region (steps 1-3 incl. device allocations, src/tilespgemm-cuda.h:
+    2358-2747).  Host<->device copies of the tile arrays are outside it, as in
+    the reference (its H2D precedes tstart, its D2H follows tend)."""
+    from spgemm_amd import tilespgemm as T
+    os.environ["TSG_QUIET"] = "1"  # the reference's printf lines would pollute stdout
+    A = T.Matrix.from_csr(m, n, rp, ci, vv)
+    B = T.Matrix.from_csr(mb, nb, rpb, cib, vvb)
+    T.csr2tile_row_major(A, tm, tm)
+    T.csr2tile_col_major(B, tm, tm)
+    runs = []
+    for _ in range(reps + 1):
+        Cm, info = T.tilespgemm(A, B, tm, tm, nnzCub=nnzcub)
+        runs.append((info, Cm.s.numtile))
+        del Cm
+    runs = runs[1:]  # first call warms the context's caching allocator
+    med = lambda k: float(np.median([r[0][k] for r in runs]))
+    t = med("time_tile")
+    return {"t_kern_tiled_ms": round(t, 4), "gflops": round(2.0 * nnzcub / (t * 1e-3) / 1e9, 3),
+            "t_step1_ms": round(med("time_step1"), 4), "t_step2_ms": round(med("time_step2"), 4),
+            "t_step3_ms": round(med("time_step3"), 4), "t_malloc_ms": round(med("time_malloc"), 4),
+            "numblkC": int(runs[0][1]), "nnzC": int(runs[0][0]["nnzC"]), "reps": reps,
+            "path": "tsg_tilespgemm (reference tiled layout in/out; the ./test CLI path)"}
 
 
 def pmc_traffic(kernel, workload):
@@ -158,10 +195,17 @@ def main():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N>1 (nccl = RCCL over xGMI; gloo = host-staged "
                          "rehearsal of the multi-rank path, e.g. several ranks on one GPU)")
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="N>1: weak = every rank owns one A-sized row block of the stacked "
-                         "product (fixed work per GPU, no collective on the data path); strong = "
-                         "A's tile rows partitioned by work + RCCL gather of C to rank 0")
+    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
+                    help="N>1: strong (default) = the fixed product, A's tile rows partitioned by "
+                         "work + RCCL gather of C to rank 0; weak = every rank owns one A-sized row "
+                         "block of the stacked product (fixed work per GPU, no data-path collective)")
+    ap.add_argument("--block-products", type=float, default=1.5e9,
+                    help="row-block size (intermediate products) when the product exceeds int32 "
+                         "nnz(C): such products run as sequential row blocks, C kept per block")
+    ap.add_argument("--tiled", type=int, default=None,
+                    help="also time the reference-layout host path tsg_tilespgemm (csr2tile tiles "
+                         "in, tiled C out; the reference's timed region) -> t_kern_tiled_ms; "
+                         "default on at N=1 for matrices with <= 4e8 intermediate products")
     args = ap.parse_args()
 
     import torch
@@ -194,38 +238,59 @@ def main():
         mb, nb, rpb, cib, vvb = m, n, rp, ci, vv
     tm = args.tile
     full_m = m
+    blen_b = np.diff(rpb.astype(np.int64))
+    cum = np.concatenate([[0], np.cumsum(blen_b[ci])])[rp]  # nnzCub of row prefixes
     rows = args.rows
-    if rows is None:
-        blen = np.diff(rpb.astype(np.int64))
-        cum = np.concatenate([[0], np.cumsum(blen[ci])])[rp]  # nnzCub of row prefixes
-        if cum[-1] > 1.5e9:  # C = A^2 would overflow int32 nnz (as in the reference)
-            rows = int(np.searchsorted(cum, 1.5e9, side="right") - 1) // tm * tm
-            log(f"full product infeasible (nnzCub {int(cum[-1])}); using rows [0,{rows})")
+    if rows is None and args.matrix == "mawi" and not args.mtx and cum[-1] > 1e12:
+        # mawi's hub makes the full A^2 ~1e14 products (~2000 s a step): the largest
+        # row prefix within one int32 C, as SURVEY §8d prescribes for infeasible sizes
+        rows = int(np.searchsorted(cum, args.block_products, side="right") - 1) // tm * tm
+        log(f"full product infeasible (nnzCub {int(cum[-1])}); using rows [0,{rows})")
     if rows is not None and rows < m:
         m, rp, ci, vv = rows, rp[:rows + 1].copy(), ci[:rp[rows]].copy(), vv[:rp[rows]].copy()
+        cum = cum[:rows + 1]
         name = f"{name} rows[0,{rows}) of {full_m}"
-    nnzcub_rank = nnzcub_rows(rp, ci, rpb, 0, m)
+    nnzcub_full = int(cum[-1])
     weak = world > 1 and args.scaling == "weak"
-    nnzcub_total = nnzcub_rank * world if weak else nnzcub_rank
+    nnzcub_total = nnzcub_full * world if weak else nnzcub_full
+    # this rank's tile rows: strong = a contiguous block of ~equal work
     if world > 1 and not weak:
         work = tdist.tile_row_work(rp, ci, rpb, m, tm)
-        parts = tdist.partition_tile_rows(work, world)
-        t0r, t1r = parts[rank]
-        mblk, rpblk, ciblk, vvblk = tdist.slice_rows(m, rp, ci, vv, t0r * tm, t1r * tm)
+        t0r, t1r = tdist.partition_tile_rows(work, world)[rank]
+        r_lo, r_hi = min(m, t0r * tm), min(m, t1r * tm)
     else:
-        mblk, rpblk, ciblk, vvblk = m, rp, ci, vv
-    dA = DeviceCSR.from_host(mblk, n, rpblk, ciblk, vvblk)
-    dB = dA if (not aat and (world == 1 or weak) and m == full_m) else DeviceCSR.from_host(mb, nb, rpb, cib, vvb)
+        r_lo, r_hi = 0, m
+    # products past int32 nnz(C) (the reference's `int nnzC`): sequential row
+    # blocks of <= block_products each, every block's C kept on the device
+    blocked = nnzcub_full > args.block_products
+    blocks = tdist.product_blocks(cum, r_lo, r_hi, args.block_products, tm) if blocked else [(r_lo, r_hi)]
+    gather = world > 1 and not weak and not blocked
+    dA_blocks = []
+    for (b0, b1) in blocks:
+        mb_, rpb_, cib_, vvb_ = tdist.slice_rows(m, rp, ci, vv, b0, b1)
+        dA_blocks.append((b0, b1, DeviceCSR.from_host(mb_, n, rpb_, cib_, vvb_)))
+    if len(dA_blocks) == 1 and not aat and dA_blocks[0][1] - dA_blocks[0][0] == full_m and m == full_m:
+        dB = dA_blocks[0][2]
+    else:
+        dB = DeviceCSR.from_host(mb, nb, rpb, cib, vvb)
     ctx = Context(dev_id)
     torch.cuda.synchronize()
+    if blocked:
+        log(f"rank {rank}: {len(blocks)} row block(s) of <= {args.block_products:.3g} products, C kept per block")
 
     gathered = [None]
     gather_ms = []
 
     def one_step():
-        ctx.reset()
-        c, st = ctx.spgemm(dA, dB, tm, tm)  # returns with C complete on the device
-        if world > 1 and not weak:
+        sts, nnz = [], 0
+        c = None
+        for (_, _, dAb) in dA_blocks:
+            ctx.reset()
+            c, st = ctx.spgemm(dAb, dB, tm, tm)  # returns with C complete on the device
+            sts.append(st)
+            nnz += c.nnz
+        st = {k: sum(s[k] for s in sts) for k in sts[0]}
+        if gather:
             g0 = time.perf_counter()
             cblk = ctx.view_torch(c)  # zero-copy views of the context-owned C block
             if host_coll:
@@ -234,7 +299,7 @@ def main():
                 gathered[0] = tdist.gather_csr_blocks(cblk.rowptr, cblk.col, cblk.val, rank, world)
                 torch.cuda.synchronize()
             gather_ms.append((time.perf_counter() - g0) * 1e3)
-        return c, st
+        return c, st, nnz
 
     for _ in range(args.warmup):
         one_step()
@@ -244,7 +309,7 @@ def main():
     stats = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        c, st = one_step()
+        c, st, nnz_rank = one_step()
         stats.append(st)
     torch.cuda.synchronize()
     if dist:
@@ -254,11 +319,11 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        nz = torch.tensor([c.nnz], dtype=torch.int64, device=red_dev)
+        nz = torch.tensor([nnz_rank], dtype=torch.int64, device=red_dev)
         dist.all_reduce(nz)
         nnzC = int(nz.item())
     else:
-        nnzC = c.nnz
+        nnzC = nnz_rank
     ms_per_step = elapsed * 1e3 / args.steps
     gflops = 2.0 * nnzcub_total * args.steps / elapsed / 1e9
 
@@ -266,29 +331,47 @@ def main():
     mins = {k: float(np.min([s[k] for s in stats])) for k in ("t_e2e_ms", "t_kern_ms")}
     dev_ms = med["t_csr2tile_ms"] + med["t_step1_ms"] + med["t_step2_ms"] + med["t_step3_ms"] + med["t_tile2csr_ms"]
     # SURVEY §8d algorithmic bytes (src/external/cusparse/main.cu:205-208), this rank's share
-    b_alg = 4.0 * (mblk + 1) + 12.0 * len(ciblk) + 4.0 * (mb + 1) + 12.0 * len(cib) + 4.0 * (mblk + 1) + 12.0 * c.nnz
+    mrank = r_hi - r_lo
+    nnza_rank = int(rp[r_hi] - rp[r_lo])
+    b_alg = (4.0 * (mrank + len(blocks)) + 12.0 * nnza_rank + (4.0 * (mb + 1) + 12.0 * len(cib)) * len(blocks)
+             + 4.0 * (mrank + len(blocks)) + 12.0 * nnz_rank)
     achieved_pipe = b_alg / (dev_ms * 1e-3) / 1e9
     # context only (never the graded figure): + one fp64 value and one u16 local column
     # per intermediate product of this rank (SURVEY §8d B_stream)
-    b_stream = b_alg + 10.0 * nnzcub_rows(rpblk, ciblk, rpb, 0, mblk)
-    # dominant kernel: step 3 (reads the CSR operands, writes the CSR result = B_alg's
-    # terms), timed with HIP events around its launch on the call's stream
+    b_stream = b_alg + 10.0 * float(cum[r_hi] - cum[r_lo])
+    # dominant kernel: the step-3 numeric kernel (reads the CSR operands, writes the
+    # CSR result = B_alg's terms), timed with HIP events around its launch on the
+    # call's stream
     k3_ms = med["t_step3_kernel_ms"]
     achieved = b_alg / (k3_ms * 1e-3) / 1e9
     workload = (f"{name} C=A{'*A^T' if aat else '^2'} fp64, {tm}x{tm} tiles, "
                 "csr2tile+steps1-3+tile2csr (device CSR in -> device CSR out)")
     traffic, traffic_src = pmc_traffic("k_step3", workload)
     chk = None
-    if args.check and (world == 1 or weak):
-        g_rp, g_ci, g_vv = ctx.to_host(c)[2:]
-        chk = [float(len(g_ci)), float(g_rp.astype(np.int64).sum()), float(g_ci.astype(np.int64).sum()),
-               float(g_vv.sum())]
+    if args.check and not gather:
+        # checksum of this rank's C (every block), recomputed outside the timed region
+        acc = np.zeros(4)
+        for (_, _, dAb) in dA_blocks:
+            ctx.reset()
+            cb, _ = ctx.spgemm(dAb, dB, tm, tm)
+            g_rp, g_ci, g_vv = ctx.to_host(cb)[2:]
+            acc += [float(len(g_ci)), float(g_rp.astype(np.int64).sum()), float(g_ci.astype(np.int64).sum()),
+                    float(g_vv.sum())]
+        chk = acc
         if weak:  # every rank's block of the stacked product is the same C
             t = torch.tensor(chk, dtype=torch.float64, device=red_dev)
             lo, hi = t.clone(), t.clone()
             dist.all_reduce(lo, op=dist.ReduceOp.MIN)
             dist.all_reduce(hi, op=dist.ReduceOp.MAX)
             assert torch.equal(lo, hi), "weak scaling: rank C blocks differ"
+        elif world > 1:  # blocked strong: C stays distributed, sum the rank checksums
+            t = torch.tensor(chk, dtype=torch.float64, device=red_dev)
+            dist.all_reduce(t)
+            chk = t.cpu().numpy()
+    tiled = None
+    want_tiled = args.tiled if args.tiled is not None else (world == 1 and nnzcub_full <= 4e8)
+    if want_tiled and rank == 0 and world == 1:
+        tiled = tiled_leg(m, n, rp, ci, vv, mb, nb, rpb, cib, vvb, aat, tm, nnzcub_full)
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -296,21 +379,32 @@ def main():
                 cpu = cpu_baseline(m, n, rp, ci, vv, mb, nb, rpb, cib, vvb, args.cpu_budget_s)
             except Exception as e:  # the baseline is reported, never required
                 log(f"cpu baseline failed: {e!r}")
+        if world == 1:
+            par = "single" + (f" ({len(blocks)} sequential row blocks, C per block)" if blocked else "")
+        elif weak:
+            par = f"stacked-row-block{world} (B replicated, C distributed)"
+        elif gather:
+            par = f"row-block{world} + RCCL gather"
+        else:
+            par = f"row-block{world} x {len(blocks)} sequential blocks (C distributed: past one int32 CSR)"
         out = {
             "metric": METRIC, "value": round(gflops, 3), "unit": "GFLOPS", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True, "scaling": args.scaling,
+            "higher_is_better": True, "scaling": "single" if world == 1 else args.scaling,
             "vs_baseline": None, "dtype": "f64", "data": data_kind,
             "config": {"workload": workload,
                        "m": m * world if weak else m, "m_per_rank": m if weak else None,
                        "nnzA": int(len(ci)) * (world if weak else 1), "nnzCub": nnzcub_total, "nnzC": nnzC,
-                       "numtileA": int(med["numtileA"]), "numblkC": int(med["numblkC"]),
-                       "parallelism": (f"stacked-row-block{world} (B replicated, C distributed)" if weak else
-                                       f"row-block{world} + RCCL gather" if world > 1 else "single")},
+                       "numtileA": int(med["numtileA"]),
+                       "numblkC": int(med["numblkC"]),
+                       "numblkC_kind": "element-level C tiles (non-empty 16x16 tiles of C; the reference's "
+                                       "tile-pattern step 1 also lists empty ones, see t_kern_tiled)",
+                       "row_blocks": len(blocks),
+                       "parallelism": par},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "kernel": "k_step3 (numeric + fused tile2csr): B_alg of SURVEY §8d / HIP-event kernel time",
+                         "kernel": "step-3 numeric kernel (fused tile2csr): B_alg of SURVEY §8d / HIP-event kernel time",
                          "algorithmic_bytes": int(b_alg), "kernel_ms": round(k3_ms, 4),
                          "pipeline": {"achieved": round(achieved_pipe, 2),
                                       "frac": round(achieved_pipe / HBM_PEAK_GBS, 5),
@@ -323,16 +417,17 @@ def main():
             "stage_ms_min": {k: round(v, 4) for k, v in mins.items()},
             "gather_ms": round(float(np.median(gather_ms[-args.steps:])), 4) if gather_ms else None,
             "gflops_kern": round(2.0 * nnzcub_total / (med["t_kern_ms"] * 1e-3) / 1e9, 3) if world == 1 else None,
+            "tiled": tiled,
             "cpu_baseline": cpu,
         }
         if args.check:
             if chk is not None:
                 out["check"] = {"nnz": int(chk[0]), "rowptr_sum": int(chk[1]), "col_sum": int(chk[2]),
-                                "val_sum": chk[3]}
+                                "val_sum": float(chk[3])}
             else:
                 g_rp, g_ci, g_vv = (x.cpu().numpy() for x in gathered[0])
                 out["check"] = {"nnz": int(len(g_ci)), "rowptr_sum": int(g_rp.astype(np.int64).sum()),
-                            "col_sum": int(g_ci.astype(np.int64).sum()), "val_sum": float(g_vv.sum())}
+                                "col_sum": int(g_ci.astype(np.int64).sum()), "val_sum": float(g_vv.sum())}
         print(json.dumps(out), flush=True)
     ctx.close()
     if dist:

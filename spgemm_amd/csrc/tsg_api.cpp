@@ -13,6 +13,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <map>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -122,6 +124,7 @@ using namespace tsg;
 
 struct tsg_context {
     Context cx;
+    hipStream_t stream = nullptr;  // host-layer leases only (tsg_dev_* take the caller's stream)
 };
 
 // ------------------------------------------------------------------ helpers
@@ -137,27 +140,71 @@ static int check_device() {
     return g_have_device ? TSG_OK : TSG_ERR_NO_DEVICE;
 }
 
-static tsg_context *g_default = nullptr;
+// Host-layer (reference-named) calls: each call leases a context of the calling
+// thread's current device from a per-device pool (mutex-guarded) and runs on that
+// context's own non-blocking stream, so concurrent host threads never share a
+// context, a stream or an allocator, and each call lands on the device the
+// thread selected (SURVEY.md §8b "Threading").  Leased contexts are kept for
+// reuse (their caches make repeated calls allocation-free).
+struct HostPools {
+    std::mutex mu;
+    std::map<int, std::vector<tsg_context *>> idle;
+};
+static HostPools &host_pools() {
+    static HostPools *p = new HostPools();  // never destroyed: safe at exit
+    return *p;
+}
 
-static int default_ctx(tsg_context **out) {
-    TSG_TRY(check_device());
-    if (!g_default) {
+class HostLease {
+  public:
+    HostLease() = default;
+    HostLease(const HostLease &) = delete;
+    HostLease &operator=(const HostLease &) = delete;
+    int acquire() {
+        TSG_TRY(check_device());
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess) {
             (void)hipGetLastError();
             dev = 0;
         }
-        tsg_context *c = new tsg_context();
-        int rc = c->cx.init(dev);
-        if (rc != TSG_OK) {
-            delete c;
-            return rc;
+        {
+            std::lock_guard<std::mutex> g(host_pools().mu);
+            auto &v = host_pools().idle[dev];
+            if (!v.empty()) {
+                c_ = v.back();
+                v.pop_back();
+            }
         }
-        g_default = c;
+        if (!c_) {
+            tsg_context *c = new tsg_context();
+            int rc = c->cx.init(dev);
+            if (rc == TSG_OK && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+                (void)hipGetLastError();
+                rc = TSG_ERR_HIP;
+            }
+            if (rc != TSG_OK) {
+                c->cx.destroy();
+                delete c;
+                return rc;
+            }
+            c_ = c;
+        }
+        return TSG_OK;
     }
-    *out = g_default;
-    return TSG_OK;
-}
+    ~HostLease() {
+        if (!c_) return;
+        (void)hipStreamSynchronize(c_->stream);
+        c_->cx.pool.release_all_live();
+        std::lock_guard<std::mutex> g(host_pools().mu);
+        host_pools().idle[c_->cx.device].push_back(c_);
+    }
+    tsg_context *ctx() { return c_; }
+    Context &cx() { return c_->cx; }
+    hipStream_t stream() { return c_->stream; }
+
+  private:
+    tsg_context *c_ = nullptr;
+};
 
 template <class T> static int upload(Context &cx, T **d, const T *h, size_t n, hipStream_t s) {
     TSG_TRY(cx.get(d, n ? n : 1));
@@ -487,10 +534,10 @@ void tsg_matrix_destroy(tsg_smatrix *M) {
 
 int tsg_transpose(const tsg_smatrix *A, tsg_smatrix *B) {
     if (!A || !B) return TSG_ERR_INVALID;
-    tsg_context *c;
-    TSG_TRY(default_ctx(&c));
-    Context &cx = c->cx;
-    hipStream_t s = 0;
+    HostLease lease;
+    TSG_TRY(lease.acquire());
+    Context &cx = lease.cx();
+    hipStream_t s = lease.stream();
     tsg_dev_csr dA, dB;
     TSG_TRY(upload_csr(cx, A, dA, s));
     TSG_TRY(dev_transpose(cx, dA, dB, s));
@@ -506,10 +553,10 @@ int tsg_transpose(const tsg_smatrix *A, tsg_smatrix *B) {
 
 int tsg_nnzcub(const tsg_smatrix *A, const tsg_smatrix *B, unsigned long long *out) {
     if (!A || !B || !out || A->n != B->m) return TSG_ERR_INVALID;
-    tsg_context *c;
-    TSG_TRY(default_ctx(&c));
-    Context &cx = c->cx;
-    hipStream_t s = 0;
+    HostLease lease;
+    TSG_TRY(lease.acquire());
+    Context &cx = lease.cx();
+    hipStream_t s = lease.stream();
     tsg_dev_csr dA, dB;
     TSG_TRY(upload_csr(cx, A, dA, s));
     TSG_TRY(upload(cx, &dB.rowpointer, B->rowpointer, (size_t)B->m + 1, s));
@@ -525,10 +572,10 @@ int tsg_nnzcub(const tsg_smatrix *A, const tsg_smatrix *B, unsigned long long *o
 int tsg_csr2tile_row_major(tsg_smatrix *A, int tm, int tn) {
     if (!A || !valid_tiles(tm, tn)) return TSG_ERR_INVALID;
     if (!tile_side_supported(tm) || !tile_side_supported(tn)) return TSG_ERR_UNSUPPORTED;
-    tsg_context *c;
-    TSG_TRY(default_ctx(&c));
-    Context &cx = c->cx;
-    hipStream_t s = 0;
+    HostLease lease;
+    TSG_TRY(lease.acquire());
+    Context &cx = lease.cx();
+    hipStream_t s = lease.stream();
     tsg_dev_csr d;
     tsg_dev_tiles t;
     TSG_TRY(upload_csr(cx, A, d, s));
@@ -541,10 +588,10 @@ int tsg_csr2tile_row_major(tsg_smatrix *A, int tm, int tn) {
 int tsg_csr2tile_col_major(tsg_smatrix *B, int tm, int tn) {
     if (!B || !valid_tiles(tm, tn)) return TSG_ERR_INVALID;
     if (!tile_side_supported(tm) || !tile_side_supported(tn)) return TSG_ERR_UNSUPPORTED;
-    tsg_context *c;
-    TSG_TRY(default_ctx(&c));
-    Context &cx = c->cx;
-    hipStream_t s = 0;
+    HostLease lease;
+    TSG_TRY(lease.acquire());
+    Context &cx = lease.cx();
+    hipStream_t s = lease.stream();
     tsg_dev_csr d;
     tsg_dev_tiles t;
     TSG_TRY(upload_csr(cx, B, d, s));
@@ -568,10 +615,10 @@ int tsg_tilespgemm(tsg_smatrix *A, tsg_smatrix *B, tsg_smatrix *C, unsigned int 
     if (!native && (!A->rowpointer || !A->columnindex || !A->value || !B->rowpointer || !B->columnindex ||
                     !B->value))
         return TSG_ERR_INVALID;
-    tsg_context *c;
-    TSG_TRY(default_ctx(&c));
-    Context &cx = c->cx;
-    hipStream_t s = 0;
+    HostLease lease;
+    TSG_TRY(lease.acquire());
+    Context &cx = lease.cx();
+    hipStream_t s = lease.stream();
     tsg_dev_tiles dA, dB, dC;
     tsg_dev_csr cA, cB;
     TSG_TRY(upload_tiles(cx, A, tm, tn, false, dA, s));
@@ -640,10 +687,10 @@ int tsg_tile2csr(tsg_smatrix *C, int tm, int tn) {
     (void)tn;
     if (!C || !C->tile_ptr || !valid_tiles(tm, tm)) return TSG_ERR_INVALID;
     if (!tile_side_supported(tm)) return TSG_ERR_UNSUPPORTED;
-    tsg_context *c;
-    TSG_TRY(default_ctx(&c));
-    Context &cx = c->cx;
-    hipStream_t s = 0;
+    HostLease lease;
+    TSG_TRY(lease.acquire());
+    Context &cx = lease.cx();
+    hipStream_t s = lease.stream();
     tsg_dev_tiles t;
     tsg_dev_csr d;
     TSG_TRY(upload_tiles(cx, C, tm, tm, false, t, s));
@@ -858,15 +905,15 @@ int tsg_spgemm_csr(const tsg_smatrix *A, const tsg_smatrix *B, tsg_smatrix *C, i
                    tsg_stats *stats) {
     if (!A || !B || !C || A->n != B->m || !valid_tiles(tm, tn)) return TSG_ERR_INVALID;
     if (!tile_side_supported(tm) || !tile_side_supported(tn)) return TSG_ERR_UNSUPPORTED;
-    tsg_context *c;
-    TSG_TRY(default_ctx(&c));
-    Context &cx = c->cx;
-    hipStream_t s = 0;
+    HostLease lease;
+    TSG_TRY(lease.acquire());
+    Context &cx = lease.cx();
+    hipStream_t s = lease.stream();
     tsg_dev_csr dA, dB, dC;
     TSG_TRY(upload_csr(cx, A, dA, s));
     TSG_TRY(upload_csr(cx, B, dB, s));
     TSG_HIP(hipStreamSynchronize(s));
-    int rc = tsg_dev_spgemm(c, &dA, &dB, tm, tn, s, &dC, stats);
+    int rc = tsg_dev_spgemm(lease.ctx(), &dA, &dB, tm, tn, s, &dC, stats);
     if (rc == TSG_OK) {
         memset(C, 0, sizeof(*C));
         C->m = dC.m; C->n = dC.n; C->nnz = dC.nnz;

@@ -37,6 +37,24 @@ def partition_tile_rows(work, world):
     return [(int(bounds[r]), int(bounds[r + 1])) for r in range(world)]
 
 
+def product_blocks(cum, r_lo, r_hi, cap, tile_m):
+    """Split rows [r_lo, r_hi) into consecutive tile-row-aligned blocks of at
+    most `cap` intermediate products each (cum = nnzCub of the row prefixes,
+    length m+1).  Products past the reference's int32 nnz(C)
+    (src/tilespgemm-cuda.h:2327) run as such blocks, one after another; a single
+    tile row heavier than `cap` becomes a block of its own."""
+    cum = np.asarray(cum, dtype=np.int64)
+    m = len(cum) - 1
+    bounds = [r_lo]
+    while bounds[-1] < r_hi:
+        lo = bounds[-1]
+        nxt = int(np.searchsorted(cum, cum[lo] + cap, side="right") - 1) // tile_m * tile_m
+        bounds.append(min(r_hi, m, max(nxt, lo + tile_m)))
+    if len(bounds) == 1:
+        bounds.append(r_hi)
+    return list(zip(bounds[:-1], bounds[1:]))
+
+
 def slice_rows(m, rowptr, col, val, r0, r1):
     """Rows [r0, r1) of a CSR as a standalone CSR (row pointers rebased)."""
     r0, r1 = max(0, min(r0, m)), max(0, min(r1, m))

@@ -106,3 +106,21 @@ def test_tile_row_work_is_nnzcub_per_tile_row():
     blen = np.diff(rp)
     ref = [sum(int(blen[ci[p]]) for p in range(rp[r0], rp[min(r0 + 16, m)])) for r0 in range(0, m, 16)]
     np.testing.assert_array_equal(w, ref)
+
+
+@pytest.mark.parametrize("cap", [1, 50, 1000, 10 ** 9])
+def test_product_blocks_cover_rows_within_cap(cap):
+    """Sequential row blocks (products past int32 nnz(C)): contiguous,
+    tile-row aligned, each within `cap` products unless one tile row alone
+    exceeds it."""
+    m, n, rp, ci, vv = synth.random_csr(1000, 1000, density=0.01, seed=3)
+    blen = np.diff(rp.astype(np.int64))
+    cum = np.concatenate([[0], np.cumsum(blen[ci])])[rp]
+    for r_lo, r_hi in [(0, m), (160, 800)]:
+        b = tdist.product_blocks(cum, r_lo, r_hi, cap, 16)
+        assert b[0][0] == r_lo and b[-1][1] == r_hi
+        assert all(b[i][1] == b[i + 1][0] for i in range(len(b) - 1))
+        for b0, b1 in b:
+            assert b1 > b0 and (b0 % 16 == 0)
+            work = cum[b1] - cum[b0]
+            assert work <= cap or b1 - b0 <= 16

@@ -20,16 +20,21 @@ def _port():
         return s.getsockname()[1]
 
 
-def _bench(nproc, mtx, aat, scaling="strong"):
-    args = ["bench.py", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--check", "--mtx", mtx,
-            "--aat", str(aat), "--gpus", str(nproc), "--scaling", scaling]
+def _bench(nproc, mtx, aat, scaling=None, extra=()):
+    args = ["bench.py", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--check", "--tiled", "0",
+            "--gpus", str(nproc)]
+    if mtx:
+        args += ["--mtx", mtx, "--aat", str(aat)]
+    if scaling:  # default invocation (no flag) = strong, the north-star measurement
+        args += ["--scaling", scaling]
+    args += list(extra)
     if nproc > 1:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
                "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args + ["--backend", "gloo"]
     else:
         cmd = [sys.executable] + args
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
-    r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=600, env=env)
+    r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=900, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith('{"metric"')]
     assert len(lines) == 1, r.stdout[-2000:]
@@ -38,8 +43,11 @@ def _bench(nproc, mtx, aat, scaling="strong"):
 
 @pytest.mark.parametrize("name,aat", [("x_powerlaw_400", 0), ("x_rect_50x130", 1)])
 def test_two_ranks_gather_equals_single_rank(name, aat):
+    """The DEFAULT multi-rank invocation is the north-star strong scaling:
+    fixed product, work-balanced tile-row blocks, gather of C to rank 0."""
     mtx = os.path.join(REPO, "tests", "golden", "fixtures", name + ".mtx")
     one = _bench(1, mtx, aat)
+    assert one["scaling"] == "single" and one["config"]["parallelism"] == "single"
     two = _bench(2, mtx, aat)
     assert two["n_gpus"] == 2 and two["config"]["parallelism"].startswith("row-block2")
     assert two["scaling"] == "strong"
@@ -49,7 +57,7 @@ def test_two_ranks_gather_equals_single_rank(name, aat):
 
 @pytest.mark.parametrize("name,aat", [("x_powerlaw_400", 1)])
 def test_two_ranks_weak_stacked_product(name, aat):
-    """Weak scaling (the bench default): each rank owns one A-sized row block of
+    """Weak scaling (--scaling weak): each rank owns one A-sized row block of
     [A; A] * B, no collective on the data path; every block equals the 1-rank C
     (bench asserts this across ranks) and the job counts twice the work."""
     mtx = os.path.join(REPO, "tests", "golden", "fixtures", name + ".mtx")
@@ -60,3 +68,50 @@ def test_two_ranks_weak_stacked_product(name, aat):
     assert two["config"]["nnzC"] == 2 * one["config"]["nnzC"]
     assert two["config"]["nnzCub"] == 2 * one["config"]["nnzCub"]
     assert two["gather_ms"] is None
+
+
+def _mawi_rows(scale, products):
+    from spgemm_amd import synth
+    import numpy as np
+    m, n, rp, ci, vv = synth.mawi(scale=scale)
+    blen = np.diff(rp.astype(np.int64))
+    cum = np.concatenate([[0], np.cumsum(blen[ci])])[rp]
+    rows = int(np.searchsorted(cum, products, side="right") - 1) // 16 * 16
+    return (m, n, rp, ci, vv), rows
+
+
+def test_mawi_eight_ranks_gather_vs_oracle():
+    """BASELINE config 5 rehearsed on one GPU: the mawi stand-in at 1e-2 scale
+    (2.26 M nodes, hub degree 1e5), a row prefix of ~2e8 intermediate products
+    (the full A^2 is ~1e10 products, past int32 nnz(C)), partitioned 8 ways by
+    work, each rank's block through the HIP pipeline, the C blocks gathered to
+    rank 0 (gloo here; RCCL on an 8-GPU node).  The gathered C's checksum must
+    equal the oracle's full product of the same rows."""
+    import numpy as np
+    import _oracle as O
+    (m, n, rp, ci, vv), rows = _mawi_rows(0.01, 2e8)
+    eight = _bench(8, None, 0, extra=("--matrix", "mawi", "--scale", "0.01", "--rows", str(rows)))
+    assert eight["n_gpus"] == 8 and eight["scaling"] == "strong"
+    assert eight["config"]["parallelism"] == "row-block8 + RCCL gather"
+    oA = O.OMat.from_csr(rows, n, rp[:rows + 1].copy(), ci[:rp[rows]].copy(), vv[:rp[rows]].copy())
+    oB = O.OMat.from_csr(m, n, rp, ci, vv)
+    _, _, erp, eci, evv = O.gustavson(oA, oB).csr()
+    want = {"nnz": int(len(eci)), "rowptr_sum": int(erp.astype(np.int64).sum()),
+            "col_sum": int(eci.astype(np.int64).sum()), "val_sum": float(evv.sum())}
+    assert eight["check"] == want
+    assert eight["config"]["nnzC"] == want["nnz"]
+
+
+def test_blocked_rows_equal_single_block():
+    """Sequential row blocks (the mode for products past int32 nnz(C), e.g. the
+    full LiveJournal stand-in): forcing tiny blocks gives the same C checksum
+    as one block, and the job still counts the whole product."""
+    mtx = os.path.join(REPO, "tests", "golden", "fixtures", "x_powerlaw_400.mtx")
+    one = _bench(1, mtx, 0)
+    blk = _bench(1, mtx, 0, extra=("--block-products", "2000"))
+    assert blk["config"]["row_blocks"] > 3
+    assert blk["check"] == one["check"]
+    assert blk["config"]["nnzCub"] == one["config"]["nnzCub"]
+    two = _bench(2, mtx, 0, extra=("--block-products", "2000"))
+    assert "sequential blocks" in two["config"]["parallelism"]
+    assert two["check"] == one["check"]

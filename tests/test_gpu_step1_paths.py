@@ -81,3 +81,31 @@ def test_b_too_wide_for_tile_counts():
     vvb = (np.arange(len(cib)) % 10 + 1).astype(np.float64)
     st = _check(m, n, rp, ci, vv, n, n, rpb, cib, vvb)
     assert st["numtileB"] == -1
+
+
+@pytest.mark.parametrize("nb", [300_000, 1_200_000])
+def test_wide_b_tile_mode_step1_vs_oracle(nb):
+    """The reference switches step 1 to the nsparse hash at > 16,384 B tile
+    columns (src/tilespgemm-cuda.h:2379-2395).  Through the reference-layout
+    host path (tsg_tilespgemm), C's tile-PATTERN structure (tile_ptr,
+    tile_columnidx, empty tiles included) and every C tile field must equal the
+    oracle's at 18,750 tile columns (one step-1 window) and 75,000 (two
+    windows of 65,536)."""
+    import _oracle as O
+    m, k = 300, 3000
+    mm, kk, rp, ci, vv = synth.random_csr(m, k, nnz_per_row=4, seed=nb % 97)
+    _, _, rpb, cib, vvb = synth.random_csr(k, nb, nnz_per_row=3, seed=nb % 89)
+    A = T.Matrix.from_csr(m, k, rp, ci, vv)
+    B = T.Matrix.from_csr(k, nb, rpb, cib, vvb)
+    oA = O.OMat.from_csr(m, k, rp, ci, vv)
+    oB = O.OMat.from_csr(k, nb, rpb, cib, vvb)
+    T.csr2tile_row_major(A, 16, 16)
+    T.csr2tile_col_major(B, 16, 16)
+    O.csr2tile_row_major(oA, 16, 16)
+    O.csr2tile_col_major(oB, 16, 16)
+    Cm, _ = T.tilespgemm(A, B, 16, 16)
+    oC = O.tilespgemm(oA, oB, 16, 16)
+    ct, oct_ = Cm.tiles(16, 1), O.c_tiles(oC, 16)
+    assert ct["numtile"] == oct_["numtile"]
+    for key in ("tile_ptr", "tile_columnidx", "tile_nnz", "tile_csr_Ptr", "tile_csr_Col", "tile_csr_Value"):
+        np.testing.assert_array_equal(ct[key], oct_[key], err_msg=key)
