@@ -110,10 +110,10 @@ def cpu_baseline(m, n, rp, ci, vv, mb, nb, rpb, cib, vvb, budget_s):
     thr = O.num_threads()
     nproc = os.cpu_count()
     try:
-        nproc = len(os.sched_getaffinity(0))
+        affinity = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
-        pass
-    return {"value": round(2.0 * cub / t / 1e9, 4), "unit": "GFLOPS", "cores": thr, "nproc": nproc,
+        affinity = None
+    return {"value": round(2.0 * cub / t / 1e9, 4), "unit": "GFLOPS", "cores": thr, "nproc": nproc, "affinity_cpus": affinity,
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
             "kind": "port",
             "sample": f"spgemm_spa restatement (count+fill passes, symbolic), rows [0,{rows}) of {m} "

@@ -108,10 +108,10 @@ def test_blocked_rows_equal_single_block():
     as one block, and the job still counts the whole product."""
     mtx = os.path.join(REPO, "tests", "golden", "fixtures", "x_powerlaw_400.mtx")
     one = _bench(1, mtx, 0)
-    blk = _bench(1, mtx, 0, extra=("--block-products", "2000"))
+    blk = _bench(1, mtx, 0, extra=("--block-products", "300"))
     assert blk["config"]["row_blocks"] > 3
     assert blk["check"] == one["check"]
     assert blk["config"]["nnzCub"] == one["config"]["nnzCub"]
-    two = _bench(2, mtx, 0, extra=("--block-products", "2000"))
+    two = _bench(2, mtx, 0, extra=("--block-products", "300"))
     assert "sequential blocks" in two["config"]["parallelism"]
     assert two["check"] == one["check"]
