@@ -349,25 +349,39 @@ def main():
     traffic, traffic_src = pmc_traffic("k_step3", workload)
     chk = None
     if args.check and not gather:
-        # checksum of this rank's C (every block), recomputed outside the timed region
+        # checksum of this rank's C (every block), recomputed outside the timed region;
+        # row pointers summed as the one global CSR would hold them
         acc = np.zeros(4)
+        off = 0
         for (_, _, dAb) in dA_blocks:
             ctx.reset()
             cb, _ = ctx.spgemm(dAb, dB, tm, tm)
             g_rp, g_ci, g_vv = ctx.to_host(cb)[2:]
-            acc += [float(len(g_ci)), float(g_rp.astype(np.int64).sum()), float(g_ci.astype(np.int64).sum()),
-                    float(g_vv.sum())]
-        chk = acc
+            acc += [float(len(g_ci)), float(g_rp[:-1].astype(np.int64).sum() + off * (len(g_rp) - 1)),
+                    float(g_ci.astype(np.int64).sum()), float(g_vv.sum())]
+            off += len(g_ci)
+        rows_rank = r_hi - r_lo
         if weak:  # every rank's block of the stacked product is the same C
+            chk = acc.copy()
+            chk[1] += off
             t = torch.tensor(chk, dtype=torch.float64, device=red_dev)
             lo, hi = t.clone(), t.clone()
             dist.all_reduce(lo, op=dist.ReduceOp.MIN)
             dist.all_reduce(hi, op=dist.ReduceOp.MAX)
             assert torch.equal(lo, hi), "weak scaling: rank C blocks differ"
-        elif world > 1:  # blocked strong: C stays distributed, sum the rank checksums
-            t = torch.tensor(chk, dtype=torch.float64, device=red_dev)
+        elif world > 1:  # blocked strong: C stays distributed; shift by the ranks before
+            cnt = torch.tensor([float(off), float(rows_rank)], dtype=torch.float64, device=red_dev)
+            allc = [torch.zeros_like(cnt) for _ in range(world)]
+            dist.all_gather(allc, cnt)
+            before = sum(float(allc[q][0]) for q in range(rank))
+            acc[1] += before * rows_rank
+            t = torch.tensor(acc, dtype=torch.float64, device=red_dev)
             dist.all_reduce(t)
             chk = t.cpu().numpy()
+            chk[1] += sum(float(c[0]) for c in allc)  # rowptr[m] = nnz(C)
+        else:
+            chk = acc
+            chk[1] += off
     tiled = None
     want_tiled = args.tiled if args.tiled is not None else (world == 1 and nnzcub_full <= 4e8)
     if want_tiled and rank == 0 and world == 1:

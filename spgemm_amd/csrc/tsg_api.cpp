@@ -824,6 +824,42 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
     // back with the counts' host round trip.  (With unsorted B rows the counts are
     // discarded: the full csr2tile below rebuilds A's tiles.)
     TSG_TRY(dev_rows_sorted_async(cx, *B, cx.pinned + 1, s));
+    // Fused element path (tsg_fused.hip: steps 1-3 + tile2csr in one persistent
+    // kernel over row units) for short-row products -- every C row within
+    // kFusedMaxRowProducts element products (longest A row x longest B row),
+    // B's rows column-sorted -- where its one-kernel pass beats the staged
+    // pipeline (mc2depi A*A^T: 0.40 vs 0.83 ms).  Web graphs and FEM matrices
+    // (long rows) take the staged tile pipeline below, which is faster there.
+    // TSG_PATH=fused / tiles forces either path.
+    const char *path = getenv("TSG_PATH");
+    const bool force_fused = path && !strcmp(path, "fused"), force_tiles = path && !strcmp(path, "tiles");
+    if (!force_tiles) {
+        TSG_TRY(dev_row_maxlen_async(cx, *A, cx.pinned + 2, s));
+        TSG_TRY(dev_row_maxlen_async(cx, *B, cx.pinned + 3, s));
+        TSG_HIP(hipStreamSynchronize(s));
+        const bool short_rows = (long long)cx.pinned[2] * (long long)cx.pinned[3] <= kFusedMaxRowProducts;
+        if (cx.pinned[1] == 0 && (short_rows || force_fused)) {
+            TSG_HIP(hipEventRecord(cx.ev[9], s));
+            TSG_TRY(dev_spgemm_fused(cx, *A, *B, *C, &st, s, cx.ev));
+            TSG_HIP(hipEventRecord(cx.ev[10], s));
+            TSG_HIP(hipEventSynchronize(cx.ev[10]));
+            auto h1 = std::chrono::steady_clock::now();
+            st.numtileA = -1;
+            st.numtileB = -1;
+            st.t_csr2tile_ms = ev_ms(cx.ev[8], cx.ev[9]);   // B sortedness check (no csr2tile on this path)
+            st.t_step1_ms = ev_ms(cx.ev[0], cx.ev[1]);      // entry ranges, row classes, heavy-row windows, units
+            st.t_step2_ms = 0.0;                            // (fused into the unit kernel)
+            st.t_step3_ms = ev_ms(cx.ev[1], cx.ev[3]);      // the unit kernel (steps 1-3 + tile2csr) + allocations
+            st.t_step3_kernel_ms = ev_ms(cx.ev[4], cx.ev[5]);
+            st.t_tile2csr_ms = 0.0;                         // (fused)
+            st.t_kern_ms = ev_ms(cx.ev[0], cx.ev[3]);
+            st.t_e2e_ms = std::chrono::duration<double, std::milli>(h1 - h0).count();
+            st.t_malloc_ms = st.t_e2e_ms - ev_ms(cx.ev[8], cx.ev[10]);
+            if (st.t_malloc_ms < 0) st.t_malloc_ms = 0;
+            if (stats) *stats = st;
+            return TSG_OK;
+        }
+    }
     const char *md = getenv("TSG_STEP2_MODE");
     const int forced = !md ? -1 : !strcmp(md, "elem") ? 1 : !strcmp(md, "tile") ? 0 : -1;
     const double skip = forced == 1 ? 1e300 : forced == 0 ? 0.0 : kStep2ElemMaxTileDensity;

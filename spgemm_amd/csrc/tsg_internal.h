@@ -110,6 +110,15 @@ int dev_tile_masks(Context &cx, const tsg_dev_csr &M, tsg_dev_tiles &t, uint16_t
 int dev_rows_sorted(Context &cx, const tsg_dev_csr &M, bool *sorted, hipStream_t s);
 int dev_rows_sorted_async(Context &cx, const tsg_dev_csr &M, int *host_flag, hipStream_t s);
 int dev_tile2csr(Context &cx, const tsg_dev_tiles &C, tsg_dev_csr &out, hipStream_t s);
+// fused element path (tsg_fused.hip): CSR in -> CSR out, B rows column-sorted.
+// ev (optional): 0 start | 1 units built | 4, 5 around the unit kernel | 3 end
+// longest row of M, copied (stream-ordered) into *host_out
+int dev_row_maxlen_async(Context &cx, const tsg_dev_csr &M, int *host_out, hipStream_t s);
+// rows of C with at most this many element products (max row length of A x of B)
+// route to the fused path by default
+constexpr long long kFusedMaxRowProducts = 256;
+int dev_spgemm_fused(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, tsg_dev_csr &C, tsg_stats *st,
+                     hipStream_t s, hipEvent_t *ev);
 
 // read a device int / long long synchronously through pinned memory
 int read_i32(Context &cx, const int *d, int *h, hipStream_t s);

@@ -185,8 +185,12 @@ def test_full_size_synthetic_vs_oracle(name):
     ref = O.gustavson(oA, oB)
     assert_csr_equal(Cm.csr(), ref.csr())
     assert st["nnzC"] == ref.s.nnz
-    # the pipeline's A/B tile counts (wave hash sets + bitmap fallback for tile
-    # rows over 256 entries) equal the oracle csr2tile's numtile
+    # the staged pipeline's A/B tile counts (wave hash sets + bitmap fallback for
+    # tile rows over 256 entries) equal the oracle csr2tile's numtile (the fused
+    # short-row path builds no A/B tiles and reports -1)
+    if st["numtileA"] < 0:
+        assert name == "mc2depi"
+        return
     tA = O.OMat.from_csr(m, n, rp, ci, vv)
     O.csr2tile_row_major(tA, 16, 16)
     assert st["numtileA"] == tA.s.numtile
