@@ -610,44 +610,31 @@ int tsg_tilespgemm(tsg_smatrix *A, tsg_smatrix *B, tsg_smatrix *C, unsigned int 
     if (!A || !B || !C || !valid_tiles(tm, tn)) return TSG_ERR_INVALID;
     if (!tile_side_supported(tm) || !tile_side_supported(tn)) return TSG_ERR_UNSUPPORTED;
     if (A->n != B->m || !A->tile_ptr || !B->tile_ptr || !B->mask || !B->csc_tile_ptr) return TSG_ERR_INVALID;
-    const bool native = tile_size_supported(tm, tn);
-    // other tile sizes: C by the 16x16 pipeline from the CSR operands, re-tiled
-    if (!native && (!A->rowpointer || !A->columnindex || !A->value || !B->rowpointer || !B->columnindex ||
-                    !B->value))
-        return TSG_ERR_INVALID;
+    // 16x16: the staged pipeline's tile-payload kernels; other sizes (32/48/64 x
+    // 16/32/48/64): step 1 at that size plus the general-size step-2/3 kernels
+    // (tsg_tile_steps.hip) -- steps 1-3 all run natively at tm x tn
+    const bool sq16 = tile_size_supported(tm, tn);
     HostLease lease;
     TSG_TRY(lease.acquire());
     Context &cx = lease.cx();
     hipStream_t s = lease.stream();
     tsg_dev_tiles dA, dB, dC;
-    tsg_dev_csr cA, cB;
     TSG_TRY(upload_tiles(cx, A, tm, tn, false, dA, s));
     TSG_TRY(upload_tiles(cx, B, tn, tm, true, dB, s));
-    if (!native) {
-        TSG_TRY(upload_csr(cx, A, cA, s));
-        TSG_TRY(upload_csr(cx, B, cB, s));
-    }
     TSG_HIP(hipStreamSynchronize(s));
     tsg_stats st{};
     auto h0 = std::chrono::steady_clock::now();
     int rc;
-    if (native) {
+    if (sq16) {
         rc = dev_tilespgemm(cx, dA, dB, dC, &st, s, cx.ev, nullptr);
     } else {
         dC = tsg_dev_tiles{};
         dC.m = A->m; dC.n = B->n; dC.tile_m = tm; dC.tile_n = tm;
         dC.tilem = dA.tilem; dC.tilen = dB.tilen;
         long long tp = 0;
-        tsg_dev_csr cC;
-        tsg_dev_tiles cne;
-        rc = hipEventRecord(cx.ev[11], s) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
+        rc = hipEventRecord(cx.ev[0], s) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
         if (rc == TSG_OK) rc = dev_step1(cx, dA, dB, dC, &tp, s);
-        if (rc == TSG_OK) rc = hipEventRecord(cx.ev[12], s) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
-        if (rc == TSG_OK) rc = dev_spgemm16(cx, &cA, &cB, s, &cC, nullptr);
-        if (rc == TSG_OK) rc = hipEventRecord(cx.ev[13], s) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
-        if (rc == TSG_OK) rc = dev_csr2tile_row_major(cx, cC, tm, tm, cne, s);
-        if (rc == TSG_OK) rc = dev_retile_c(cx, cne, dC, s);
-        if (rc == TSG_OK) rc = hipEventRecord(cx.ev[14], s) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
+        if (rc == TSG_OK) rc = dev_tile_steps23(cx, dA, dB, dC, s, cx.ev);
     }
     if (rc == TSG_OK) TSG_HIP(hipStreamSynchronize(s));
     auto h1 = std::chrono::steady_clock::now();
@@ -659,9 +646,8 @@ int tsg_tilespgemm(tsg_smatrix *A, tsg_smatrix *B, tsg_smatrix *C, unsigned int 
     }
     cx.pool.release_all_live();
     if (rc != TSG_OK) return rc;
-    const int e0 = native ? 0 : 11;  // re-tiled sizes: step 1 | 16x16 pipeline | re-tiling
-    const double t1 = ev_ms(cx.ev[e0], cx.ev[e0 + 1]), t2 = ev_ms(cx.ev[e0 + 1], cx.ev[e0 + 2]),
-                 t3 = ev_ms(cx.ev[e0 + 2], cx.ev[e0 + 3]);
+    // the reference's steps at every tile size: step 1 | step 2 + scan | step 3
+    const double t1 = ev_ms(cx.ev[0], cx.ev[1]), t2 = ev_ms(cx.ev[1], cx.ev[2]), t3 = ev_ms(cx.ev[2], cx.ev[3]);
     const double tk = std::chrono::duration<double, std::milli>(h1 - h0).count();
     if (time_step1) *time_step1 = t1;
     if (time_step2) *time_step2 = t2;

@@ -98,6 +98,10 @@ int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_d
               long long *tile_products, hipStream_t s, const tsg_dev_csr *Ael = nullptr,
               const tsg_dev_csr *Bel = nullptr, int2 *ebnd = nullptr,
               long long **tbase_out = nullptr, long long *tslots_out = nullptr, bool fill_ebnd = false);
+// steps 2 + 3 on the reference tiled layout at any tile size (tsg_tile_steps.hip):
+// C holds step 1's structure at C.tile_m x C.tile_m; ev (optional) gets ev[1..3]
+int dev_tile_steps23(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_dev_tiles &C, hipStream_t s,
+                     hipEvent_t *ev);
 // C payload for a step-1 structure C (tile_m set) from the non-empty tiles Cne of C's CSR
 int dev_retile_c(Context &cx, const tsg_dev_tiles &Cne, tsg_dev_tiles &C, hipStream_t s);
 // tile_ptr + tile_columnidx of a CSR's tiling (tr x tc tiles), no payload;

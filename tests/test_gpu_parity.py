@@ -296,3 +296,29 @@ def test_other_tile_sizes_vs_oracle(tm, tn, aat):
         np.testing.assert_array_equal(ct[k], oct_[k], err_msg="C " + k)
     T.tile2csr(Cm, tm, tm)
     assert_csr_equal(Cm.csr(), O.gustavson(oA, oB).csr())
+
+
+@pytest.mark.parametrize("tm,tn", [(32, 32), (64, 64), (48, 16), (64, 32)])
+def test_dense_accumulator_tiles(tm, tn):
+    """Tiles of C with more than 512 nonzeros (possible from 32x32 up) take the
+    dense per-wave LDS accumulator -- the reference's dns/ful bins
+    (src/tilespgemm-cuda.h:1954-2218) -- natively at tm x tm; every C tile
+    field against the oracle, and C's CSR against Gustavson."""
+    mm, nn, rp, ci, vv = synth.random_csr(300, 300, density=0.35, seed=tm + tn)
+    A = T.Matrix.from_csr(mm, nn, rp, ci, vv)
+    B = T.Matrix.alias(A)
+    oA = O.OMat.from_csr(mm, nn, rp, ci, vv)
+    oB = O.OMat.alias(oA)
+    T.csr2tile_row_major(A, tm, tn)
+    T.csr2tile_col_major(B, tm, tn)
+    O.csr2tile_row_major(oA, tm, tn)
+    O.csr2tile_col_major(oB, tm, tn)
+    Cm, info = T.tilespgemm(A, B, tm, tn)
+    oC = O.tilespgemm(oA, oB, tm, tn)
+    ct, oct_ = Cm.tiles(tm, tm // 16), O.c_tiles(oC, tm)
+    assert np.diff(ct["tile_nnz"]).max() > 512  # the dense accumulator ran
+    for k in C_KEYS:
+        np.testing.assert_array_equal(ct[k], oct_[k], err_msg="C " + k)
+    assert info["time_step2"] > 0 and info["time_step3"] > 0
+    T.tile2csr(Cm, tm, tm)
+    assert_csr_equal(Cm.csr(), O.gustavson(oA, oB).csr())
