@@ -1,5 +1,5 @@
 """Warm timing of the device pipeline (fused vs staged tiles) on stand-ins.
-usage: python tools/fz_time.py webbase [cant mc2depi ...] [--light]"""
+usage: python tools/fz_time.py webbase [cant mc2depi ...] [--light] [--path=fused,tiles]"""
 import os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
@@ -31,7 +31,7 @@ def run(name, light, reps=8):
     else:
         dB = dA
     ctx = Context(0)
-    for path in ("fused", "tiles"):
+    for path in PATHS:
         os.environ["TSG_PATH"] = path
         sts = []
         for i in range(reps):
@@ -47,7 +47,12 @@ def run(name, light, reps=8):
     ctx.close()
 
 
+PATHS = ("fused", "tiles")
+
 if __name__ == "__main__":
     light = "--light" in sys.argv
+    for a in sys.argv[1:]:
+        if a.startswith("--path="):
+            PATHS = tuple(a[7:].split(","))
     for nm in [a for a in sys.argv[1:] if not a.startswith("--")]:
         run(nm, light)
