@@ -83,13 +83,15 @@ def _cpu_model():
     return "unknown"
 
 
-def _timed_prefix(fn, m, budget_s):
-    """Run fn(rows) on a growing row prefix until it takes ~budget_s; (rows, seconds)."""
-    rows = min(m, 2000)
+def _timed_prefix(fn, m, budget_s, max_rows=None):
+    """Run fn(rows) on a growing row prefix until it takes ~budget_s; (rows, seconds).
+    max_rows caps the prefix (a sample whose C must fit int32 row pointers)."""
+    cap = m if max_rows is None else max(1, min(m, max_rows))
+    rows = min(cap, 2000)
     t0 = time.perf_counter()
     fn(rows)
     t = time.perf_counter() - t0
-    rows2 = int(min(m, max(rows, rows * budget_s / max(t, 1e-6))))
+    rows2 = int(min(cap, max(rows, rows * budget_s / max(t, 1e-6))))
     t0 = time.perf_counter()
     fn(rows2)
     return rows2, time.perf_counter() - t0
@@ -103,7 +105,12 @@ def cpu_baseline(m, n, rp, ci, vv, mb, nb, rpb, cib, vvb, budget_s):
     import _oracle as O
     A = O.OMat.from_csr(m, n, rp, ci, vv)
     B = O.OMat.from_csr(mb, nb, rpb, cib, vvb)
-    rows, t = _timed_prefix(lambda r: O.spa(A, B, 0, r), m, budget_s)
+    # the SPA sample holds its symbolic C (int32 row pointers, 4 B per column):
+    # rows whose intermediate products stay <= 2e8 (an upper bound of their nnz(C))
+    blen = np.diff(rpb.astype(np.int64))
+    cum = np.concatenate([[0], np.cumsum(blen[ci])])[rp]
+    max_rows = int(np.searchsorted(cum, 2e8, side="right") - 1)
+    rows, t = _timed_prefix(lambda r: O.spa(A, B, 0, r), m, budget_s, max_rows)
     cub = nnzcub_rows(rp, ci, rpb, 0, rows)
     nrows, nt = _timed_prefix(lambda r: O.gustavson_rows(A, B, 0, r), m, budget_s / 2)
     ncub = nnzcub_rows(rp, ci, rpb, 0, nrows)

@@ -564,6 +564,10 @@ int tsgo_spa(const tsgo_mat *A, const tsgo_mat *B, int *rowptrC, int *colidxC,
             run += v;
         }
         *nnzC = run;
+        if (run > 0x7fffffffLL) {  /* past int32 row pointers (the reference's int nnzC) */
+            free(flags);
+            return -2;
+        }
     } else {
 #pragma omp parallel for schedule(dynamic, 64)
         for (int i = row_begin; i < row_end; i++) {

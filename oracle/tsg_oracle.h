@@ -72,7 +72,7 @@ int tsgo_tile2csr(tsgo_mat *C, int tm, int tn);
  * rowptrC has mA+1 entries.  If get_nnzC_only, fills rowptrC (exclusive) and *nnzC.
  * Otherwise fills colidxC (ascending per row) using rowptrC from the first call.
  * row_begin/row_end restrict the rows processed (bounded CPU-baseline samples);
- * pass 0, mA for all rows. */
+ * pass 0, mA for all rows.  Returns -2 when nnz(C) of the rows exceeds int32. */
 int tsgo_spa(const tsgo_mat *A, const tsgo_mat *B, int *rowptrC, int *colidxC,
              long long *nnzC, int get_nnzC_only, int row_begin, int row_end);
 

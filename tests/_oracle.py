@@ -191,8 +191,11 @@ def spa(A, B, row_begin=0, row_end=None):
         row_end = A.s.m
     rp = np.zeros(A.s.m + 1, dtype=np.int32)
     nnz = C.c_longlong(0)
-    lib().tsgo_spa(C.byref(A.s), C.byref(B.s), rp.ctypes.data, None, C.byref(nnz), 1,
-                   row_begin, row_end)
+    rc = lib().tsgo_spa(C.byref(A.s), C.byref(B.s), rp.ctypes.data, None, C.byref(nnz), 1,
+                        row_begin, row_end)
+    if rc == -2:
+        raise OverflowError(f"spa: nnz(C) of rows [{row_begin},{row_end}) = {nnz.value} exceeds int32")
+    assert rc == 0, rc
     ci = np.zeros(max(int(nnz.value), 1), dtype=np.int32)
     lib().tsgo_spa(C.byref(A.s), C.byref(B.s), rp.ctypes.data, ci.ctypes.data, C.byref(nnz), 0,
                    row_begin, row_end)
