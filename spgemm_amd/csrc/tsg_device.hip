@@ -2641,59 +2641,6 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     return TSG_OK;
 }
 
-// ---------------------------------------------------------------------------
-// Re-tiling for tile sizes other than 16x16 (host tile API): the C CSR of the
-// 16x16 pipeline, tiled at tm x tm (csr2tile), is scattered into the step-1
-// C tile list of that size (which also holds the structurally empty tiles).
-// Payload order is the same in both lists (tiles ascending, then rows, then
-// columns), so Col/Value carry over; Ptr, mask and nnz move tile by tile.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(WG) void k_retile_scatter(int numne, const int *ne_row, const int *ne_col,
-                                                       const int *ne_nnz, const u16 *ne_Ptr, const u16 *ne_mask,
-                                                       int tm, const int *Cptr, const int *Ccol, int *cnt,
-                                                       u16 *Ptr, u16 *mask) {
-    const int mwords = tm * (tm / 16);
-    for (int t = blockIdx.x * WG + threadIdx.x; t < numne; t += gridDim.x * WG) {
-        const int i = ne_row[t];
-        const int p = lower_bound_dev(Ccol, Cptr[i], Cptr[i + 1], ne_col[t]);
-        cnt[p] = ne_nnz[t + 1] - ne_nnz[t];
-        for (int r = 0; r < tm; ++r) Ptr[(size_t)p * tm + r] = ne_Ptr[(size_t)t * tm + r];
-        for (int w = 0; w < mwords; ++w) mask[(size_t)p * mwords + w] = ne_mask[(size_t)t * mwords + w];
-    }
-}
-
-__global__ __launch_bounds__(WG) void k_col_local(const u16 *enc, long n, int tm, u16 *col) {
-    for (long k = (long)blockIdx.x * WG + threadIdx.x; k < n; k += (long)gridDim.x * WG) col[k] = enc[k] % tm;
-}
-
-int dev_retile_c(Context &cx, const tsg_dev_tiles &Cne, tsg_dev_tiles &C, hipStream_t s) {
-    const int tm = C.tile_m, mwords = tm * (tm / 16);
-    const size_t nb1 = (size_t)C.numtile + 1;
-    C.nnz = Cne.nnz;
-    TSG_TRY(cx.get(&C.tile_nnz, nb1));
-    TSG_TRY(cx.get(&C.tile_csr_Ptr, nb1 * tm));
-    TSG_TRY(cx.get(&C.mask, nb1 * mwords));
-    TSG_TRY(cx.get(&C.tile_csr_Col, (size_t)C.nnz + 1));
-    TSG_TRY(cx.get(&C.tile_csr_Value, (size_t)C.nnz + 1));
-    TSG_HIP(hipMemsetAsync(C.tile_nnz, 0, nb1 * sizeof(int), s));
-    TSG_HIP(hipMemsetAsync(C.tile_csr_Ptr, 0, nb1 * tm * sizeof(u16), s));
-    TSG_HIP(hipMemsetAsync(C.mask, 0, nb1 * mwords * sizeof(u16), s));
-    if (Cne.numtile > 0)
-        k_retile_scatter<<<grid_for(Cne.numtile, WG, 8192), WG, 0, s>>>(
-            Cne.numtile, Cne.tile_rowidx, Cne.tile_columnidx, Cne.tile_nnz, Cne.tile_csr_Ptr, Cne.mask, tm,
-            C.tile_ptr, C.tile_columnidx, C.tile_nnz, C.tile_csr_Ptr, C.mask);
-    TSG_HIP(hipGetLastError());
-    long long tot = 0;
-    TSG_TRY(scan_exclusive_i32_total(cx, C.tile_nnz, (long)nb1, s, &tot));
-    if (C.nnz > 0) {
-        k_col_local<<<grid_for(C.nnz, WG, 16384), WG, 0, s>>>(Cne.tile_csr_Col, C.nnz, tm, C.tile_csr_Col);
-        TSG_HIP(hipMemcpyAsync(C.tile_csr_Value, Cne.tile_csr_Value, (size_t)C.nnz * sizeof(double),
-                               hipMemcpyDeviceToDevice, s));
-    }
-    TSG_HIP(hipGetLastError());
-    return TSG_OK;
-}
-
 __global__ void k_zero_empty_ptr(const int *nnzoff, int numtile, int tm, u16 *Ptr, u16 *mask) {
     const int mw = tm / 16;
     for (long x = (long)blockIdx.x * WG + threadIdx.x; x < (long)numtile * tm; x += (long)gridDim.x * WG) {

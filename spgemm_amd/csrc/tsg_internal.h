@@ -102,8 +102,6 @@ int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_d
 // C holds step 1's structure at C.tile_m x C.tile_m; ev (optional) gets ev[1..3]
 int dev_tile_steps23(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_dev_tiles &C, hipStream_t s,
                      hipEvent_t *ev);
-// C payload for a step-1 structure C (tile_m set) from the non-empty tiles Cne of C's CSR
-int dev_retile_c(Context &cx, const tsg_dev_tiles &Cne, tsg_dev_tiles &C, hipStream_t s);
 // tile_ptr + tile_columnidx of a CSR's tiling (tr x tc tiles), no payload;
 // tile_columnidx is left null when M.nnz < skip_emit_density * numtile
 int dev_tile_structure(Context &cx, const tsg_dev_csr &M, int tr, int tc, tsg_dev_tiles &out, hipStream_t s,
