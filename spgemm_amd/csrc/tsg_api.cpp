@@ -288,6 +288,10 @@ static int upload_tiles(Context &cx, const tsg_smatrix *M, int tile_m, int tile_
     return TSG_OK;
 }
 
+// Step 2 streams element products when A averages fewer nonzeros per tile than
+// this (one 16-bit row-mask OR per A nonzero and B tile otherwise wins).
+static constexpr double kStep2ElemMaxTileDensity = 16.0;
+
 static bool quiet() { return getenv("TSG_QUIET") != nullptr; }
 static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B, hipStream_t s, tsg_dev_csr *C,
                         tsg_stats *stats);
@@ -621,12 +625,34 @@ int tsg_tilespgemm(tsg_smatrix *A, tsg_smatrix *B, tsg_smatrix *C, unsigned int 
     tsg_dev_tiles dA, dB, dC;
     TSG_TRY(upload_tiles(cx, A, tm, tn, false, dA, s));
     TSG_TRY(upload_tiles(cx, B, tn, tm, true, dB, s));
+    // The reference's SMatrix carries the CSR beside the tiles (src/main.cu builds
+    // both).  When both operands have it and B's rows are column-sorted, steps 2
+    // and 3 stream the element products from it (the CSR path's kernels, writing
+    // the tiled C); copied in with the tiles, outside the timed region.
+    // TSG_TILED_CSR=0 keeps the tile-payload kernels.
+    tsg_dev_csr cA{}, cB{};
+    bool use_csr = false, s2e = false;
+    {
+        const char *e = getenv("TSG_TILED_CSR");
+        const bool allow = !(e && !strcmp(e, "0"));
+        if (sq16 && allow && A->rowpointer && A->columnindex && A->value && B->rowpointer && B->columnindex &&
+            B->value && A->nnz == dA.nnz && B->nnz == dB.nnz) {
+            TSG_TRY(upload_csr(cx, A, cA, s));
+            TSG_TRY(upload_csr(cx, B, cB, s));
+            bool sorted = false;
+            TSG_TRY(dev_rows_sorted(cx, cB, &sorted, s));
+            use_csr = sorted;
+            // element masks for sparse tiles, tile-row mask ORs for denser ones (as dev_spgemm16)
+            s2e = use_csr && (double)dA.nnz < kStep2ElemMaxTileDensity * (double)dA.numtile;
+        }
+    }
     TSG_HIP(hipStreamSynchronize(s));
     tsg_stats st{};
     auto h0 = std::chrono::steady_clock::now();
     int rc;
     if (sq16) {
-        rc = dev_tilespgemm(cx, dA, dB, dC, &st, s, cx.ev, nullptr);
+        rc = dev_tilespgemm(cx, dA, dB, dC, &st, s, cx.ev, nullptr, use_csr ? &cA : nullptr, use_csr ? &cB : nullptr,
+                            s2e);
     } else {
         dC = tsg_dev_tiles{};
         dC.m = A->m; dC.n = B->n; dC.tile_m = tm; dC.tile_n = tm;
@@ -789,9 +815,6 @@ static void release_tiles(Context &cx, tsg_dev_tiles &t) {
     t = tsg_dev_tiles{};
 }
 
-// Step 2 streams element products when A averages fewer nonzeros per tile than
-// this (one 16-bit row-mask OR per A nonzero and B tile otherwise wins).
-static constexpr double kStep2ElemMaxTileDensity = 16.0;
 
 // CSR in -> CSR out through the 16x16 tiled pipeline (C does not depend on the
 // tile size; other sizes are a layout choice of the host tile API).

@@ -1436,9 +1436,11 @@ __global__ void k_unit_rowbase(const int *uoff, int tilem, int m, const int *uni
     }
 }
 
-__global__ void k_crow(const int *Cptr, int tilem, int *Crow) {
-    for (int i = blockIdx.x * WG + threadIdx.x; i < tilem; i += gridDim.x * WG)
-        for (int t = Cptr[i]; t < Cptr[i + 1]; ++t) Crow[t] = i;
+// tile row of every tile: one wave per tile row, coalesced stores (a thread per
+// row serialised the long rows of C)
+__global__ __launch_bounds__(WG) void k_crow(const int *Cptr, int tilem, int *Crow) {
+    for (int i = blockIdx.x * WAVES + wave_id(); i < tilem; i += gridDim.x * WAVES)
+        for (int t = Cptr[i] + lane_id(); t < Cptr[i + 1]; t += 64) Crow[t] = i;
 }
 
 // split entries per C tile row: (#units) x (#A tiles)
@@ -2413,7 +2415,7 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     if (A.tile_m != TM || A.tile_n != TN || B.tile_m != TN || B.tile_n != TM) return TSG_ERR_UNSUPPORTED;
     // element streaming needs the CSR operands (B rows column-sorted: caller's check)
     const bool have_csr = Acsr && Bcsr && Acsr->m == A.m && Bcsr->m == B.m;
-    const bool s3elem = csr_out && have_csr && !(g_ablate & 16);
+    const bool s3elem = have_csr && !(g_ablate & 16);  // (tiled C out too: the host tile API with CSR)
     const bool s2elem = step2_elem && have_csr;
     const bool tilepay = !(s2elem && s3elem);  // some step reads the tile payloads
     if (A.n != B.m) return TSG_ERR_INVALID;
@@ -2498,7 +2500,7 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
         int *trowA = A.tile_rowidx;
         if (!trowA) {
             TSG_TRY(cx.get(&trowA, (size_t)A.numtile + 1));
-            k_crow<<<grid_for(tilemA, WG, 4096), WG, 0, s>>>(A.tile_ptr, tilemA, trowA);
+            k_crow<<<grid_for(tilemA, WAVES, 8192), WG, 0, s>>>(A.tile_ptr, tilemA, trowA);
         }
         if (A.numtile > 0)
             k_unit_splits<<<grid_for(A.numtile, WG, 8192), WG, 0, s>>>(A.numtile, trowA, A.tile_ptr,
@@ -2591,8 +2593,16 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
                     utab, etab, nunits, A.m, V, E, C.tile_columnidx, C.tile_nnz, C.mask, codeC, unit_rb,
                     csr_out->rowpointer, csr_out->columnindex, csr_out->value, nullptr, nullptr, nullptr, g_ablate);
         }
-    } else {
-        if (nnzC > 0)
+    } else if (nnzC > 0) {  // the reference's tiled C (Ptr, Col, Value per tile)
+        if (s3elem && !s2elem)
+            k_step3<TM, TN, false, true, true, true><<<gu, WG, 0, s>>>(
+                utab, etab, nunits, A.m, V, E, C.tile_columnidx, C.tile_nnz, C.mask, nullptr, nullptr, nullptr,
+                nullptr, nullptr, C.tile_csr_Ptr, C.tile_csr_Col, C.tile_csr_Value, g_ablate);
+        else if (s3elem)
+            k_step3<TM, TN, false, true, true><<<gu, WG, 0, s>>>(
+                utab, etab, nunits, A.m, V, E, C.tile_columnidx, C.tile_nnz, C.mask, nullptr, nullptr, nullptr,
+                nullptr, nullptr, C.tile_csr_Ptr, C.tile_csr_Col, C.tile_csr_Value, g_ablate);
+        else
             k_step3<TM, TN, false, true, false><<<gu, WG, 0, s>>>(
                 utab, etab, nunits, A.m, V, E, C.tile_columnidx, C.tile_nnz, C.mask, nullptr, nullptr, nullptr,
                 nullptr, nullptr, C.tile_csr_Ptr, C.tile_csr_Col, C.tile_csr_Value, g_ablate);
@@ -2641,14 +2651,18 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     return TSG_OK;
 }
 
-__global__ void k_zero_empty_ptr(const int *nnzoff, int numtile, int tm, u16 *Ptr, u16 *mask) {
-    const int mw = tm / 16;
-    for (long x = (long)blockIdx.x * WG + threadIdx.x; x < (long)numtile * tm; x += (long)gridDim.x * WG) {
-        int t = (int)(x / tm);
-        if (nnzoff[t + 1] == nnzoff[t]) {
-            Ptr[x] = 0;
-            if (mask)
-                for (int w = 0; w < mw; ++w) mask[x * mw + w] = 0;
+// Ptr and mask of structurally empty C tiles := 0: a thread per tile, its
+// tm u16 of Ptr (tm*tm/16 of mask) written as 16-byte vectors
+__global__ __launch_bounds__(WG) void k_zero_empty_ptr(const int *nnzoff, int numtile, int tm, u16 *Ptr, u16 *mask) {
+    const int pv = tm / 8, mv = tm * (tm / 16) / 8;  // uint4 per tile
+    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+    for (long t = (long)blockIdx.x * WG + threadIdx.x; t < numtile; t += (long)gridDim.x * WG) {
+        if (nnzoff[t + 1] != nnzoff[t]) continue;
+        uint4 *p = reinterpret_cast<uint4 *>(Ptr + t * tm);
+        for (int k = 0; k < pv; ++k) p[k] = z;
+        if (mask) {
+            uint4 *q = reinterpret_cast<uint4 *>(mask + t * tm * (tm / 16));
+            for (int k = 0; k < mv; ++k) q[k] = z;
         }
     }
 }
@@ -2657,10 +2671,10 @@ __global__ void k_zero_empty_ptr(const int *nnzoff, int numtile, int tm, u16 *Pt
 // and fill tile_rowidx (the device pipeline needs neither).
 int dev_tiles_finalize_c(Context &cx, tsg_dev_tiles &C, hipStream_t s) {
     if (C.numtile <= 0) return TSG_OK;
-    k_zero_empty_ptr<<<grid_for((long)C.numtile * C.tile_m, WG, 8192), WG, 0, s>>>(C.tile_nnz, C.numtile,
-                                                                                  C.tile_m, C.tile_csr_Ptr, C.mask);
+    k_zero_empty_ptr<<<grid_for(C.numtile, WG, 16384), WG, 0, s>>>(C.tile_nnz, C.numtile, C.tile_m, C.tile_csr_Ptr,
+                                                                  C.mask);
     TSG_TRY(cx.get(&C.tile_rowidx, (size_t)C.numtile + 1));
-    k_crow<<<grid_for(C.tilem, WG, 4096), WG, 0, s>>>(C.tile_ptr, C.tilem, C.tile_rowidx);
+    k_crow<<<grid_for(C.tilem, WAVES, 8192), WG, 0, s>>>(C.tile_ptr, C.tilem, C.tile_rowidx);
     TSG_HIP(hipGetLastError());
     return TSG_OK;
 }
@@ -2681,13 +2695,22 @@ __global__ __launch_bounds__(WG) void k_rm2csc(const int *tile_ptr, const int *t
     }
 }
 
+// B's row-major views, one thread per output element (coalesced stores):
+// rm_rowstart[t][c] = absolute start of row c of row-major tile t (c = tn: its
+// end), rm_mask[t][k] = its mask word k
 __global__ __launch_bounds__(WG) void k_build_b_aux(int numtile, int tn, int mw, const int *rm2csc, const int *Bnnz,
                                                      const u16 *PtrB, const u16 *maskB, u16 *rm_mask, int *rm_rowstart) {
-    for (int t = blockIdx.x * WG + threadIdx.x; t < numtile; t += gridDim.x * WG) {
-        const int bc = rm2csc[t];
-        for (int c = 0; c < tn; ++c) rm_rowstart[(size_t)t * (tn + 1) + c] = Bnnz[bc] + PtrB[(size_t)bc * tn + c];
-        rm_rowstart[(size_t)t * (tn + 1) + tn] = Bnnz[bc + 1];
-        for (int k = 0; k < tn * mw; ++k) rm_mask[(size_t)t * tn * mw + k] = maskB[(size_t)bc * tn * mw + k];
+    const long nrs = (long)numtile * (tn + 1), nmk = (long)numtile * tn * mw;
+    for (long x = (long)blockIdx.x * WG + threadIdx.x; x < nrs + nmk; x += (long)gridDim.x * WG) {
+        if (x < nrs) {
+            const int t = (int)(x / (tn + 1)), c = (int)(x - (long)t * (tn + 1));
+            const int bc = rm2csc[t];
+            rm_rowstart[x] = c < tn ? Bnnz[bc] + PtrB[(size_t)bc * tn + c] : Bnnz[bc + 1];
+        } else {
+            const long y = x - nrs;
+            const int t = (int)(y / (tn * mw)), k = (int)(y - (long)t * tn * mw);
+            rm_mask[y] = maskB[(size_t)rm2csc[t] * tn * mw + k];
+        }
     }
 }
 
@@ -2699,7 +2722,7 @@ int dev_rm2csc_from_structs(Context &cx, tsg_dev_tiles &B, hipStream_t s) {
     TSG_TRY(cx.get(&B.rm_mask, ((size_t)B.numtile + 1) * B.tile_m * (B.tile_n / 16)));
     TSG_TRY(cx.get(&B.rm_rowstart, ((size_t)B.numtile + 1) * (B.tile_m + 1)));
     if (B.numtile > 0)
-        k_build_b_aux<<<grid_for(B.numtile, WG, 8192), WG, 0, s>>>(B.numtile, B.tile_m, B.tile_n / 16, B.tile_rm2csc,
+        k_build_b_aux<<<grid_for((long)B.numtile * (2 * B.tile_m + 1), WG, 16384), WG, 0, s>>>(B.numtile, B.tile_m, B.tile_n / 16, B.tile_rm2csc,
                                                                   B.tile_nnz, B.tile_csr_Ptr, B.mask, B.rm_mask,
                                                                   B.rm_rowstart);
     TSG_HIP(hipGetLastError());

@@ -322,3 +322,63 @@ def test_dense_accumulator_tiles(tm, tn):
     assert info["time_step2"] > 0 and info["time_step3"] > 0
     T.tile2csr(Cm, tm, tm)
     assert_csr_equal(Cm.csr(), O.gustavson(oA, oB).csr())
+
+
+CASES16 = [c for c in CASES if (c.values[3], c.values[4]) == (16, 16)]
+
+
+@pytest.mark.parametrize("path,name,aat,tm,tn", CASES16)
+def test_tiled_api_csr_streaming_and_tile_payload_agree(path, name, aat, tm, tn, monkeypatch):
+    """tsg_tilespgemm at 16x16 streams element products from the SMatrix's CSR
+    when B's rows are sorted (TSG_TILED_CSR unset) and reads the tile payloads
+    otherwise (TSG_TILED_CSR=0); both must give the reference's tiled C, every
+    field bit-exact.  A sorted-row copy of the fixture makes the CSR path run
+    for A^2 as well (the file's in-row order is kept in the first pass)."""
+    ref = np.load(path)
+    for srt in (False, True):
+        A, B, oA, oB = both(os.path.join(FIXTURES, name + ".mtx"), aat)
+        if srt:
+            m, n, rp, ci, vv = A.csr()
+            order = np.concatenate([rp[i] + np.argsort(ci[rp[i]:rp[i + 1]], kind="stable") for i in range(m)]
+                                   ).astype(np.int64) if len(ci) else np.zeros(0, np.int64)
+            A = T.Matrix.from_csr(m, n, rp, ci[order], vv[order])
+            B = T.transpose(A) if aat else T.Matrix.alias(A)
+            oA = O.OMat.from_csr(m, n, rp, ci[order], vv[order])
+            oB = O.transpose(oA) if aat else O.OMat.alias(oA)
+        T.csr2tile_row_major(A, tm, tn)
+        T.csr2tile_col_major(B, tm, tn)
+        O.csr2tile_row_major(oA, tm, tn)
+        O.csr2tile_col_major(oB, tm, tn)
+        oct_ = O.c_tiles(O.tilespgemm(oA, oB, tm, tn), tm)
+        for mode in (None, "0"):
+            if mode is None:
+                monkeypatch.delenv("TSG_TILED_CSR", raising=False)
+            else:
+                monkeypatch.setenv("TSG_TILED_CSR", mode)
+            Cm, info = T.tilespgemm(A, B, tm, tn, nnzCub=int(g(ref, "nnzCub")))
+            ct = Cm.tiles(tm, tm // 16)
+            np.testing.assert_array_equal(ct["tile_ptr"], g(ref, "Ct.tile_ptr"))
+            for k in C_KEYS:
+                np.testing.assert_array_equal(ct[k], oct_[k], err_msg=f"C {k} (sorted={srt}, mode={mode})")
+            del Cm
+
+
+def test_tiled_api_csr_streaming_real_values():
+    """The tiled host API on the CSR-streaming path with real fp64 values: C's
+    tile values within 1e-10 of the oracle's magnitude sums (pattern exact)."""
+    m, n, rp, ci, _ = synth.random_csr(1500, 1500, density=0.01, seed=41)
+    vv = np.random.default_rng(3).uniform(-1, 1, len(ci))
+    A = T.Matrix.from_csr(m, n, rp, ci, vv)
+    B = T.Matrix.alias(A)
+    T.csr2tile_row_major(A, 16, 16)
+    T.csr2tile_col_major(B, 16, 16)
+    Cm, _ = T.tilespgemm(A, B, 16, 16)
+    T.tile2csr(Cm, 16, 16)
+    got = Cm.csr()
+    oA = O.OMat.from_csr(m, n, rp, ci, vv)
+    ref = O.gustavson(oA, O.OMat.alias(oA)).csr()
+    oM = O.OMat.from_csr(m, n, rp, ci, np.abs(vv))
+    mag = O.gustavson(oM, O.OMat.alias(oM)).csr()[4]
+    np.testing.assert_array_equal(got[2], ref[2])
+    np.testing.assert_array_equal(got[3], ref[3])
+    assert np.all(np.abs(got[4] - ref[4]) <= RTOL * mag)
