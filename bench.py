@@ -29,6 +29,12 @@ import time
 
 import numpy as np
 
+# CPUs this process may run on, read before any OpenMP runtime binds the main
+# thread (with OMP_PROC_BIND the main thread's own mask shrinks to one CPU)
+try:
+    _AFFINITY = len(os.sched_getaffinity(0))
+except (AttributeError, OSError):
+    _AFFINITY = None
 # CPU baseline threads stay on neighbouring cores; must be set
 # before any OpenMP runtime (torch's or the oracle's) initialises
 os.environ.setdefault("OMP_PROC_BIND", "close")
@@ -116,16 +122,18 @@ def cpu_baseline(m, n, rp, ci, vv, mb, nb, rpb, cib, vvb, budget_s):
     ncub = nnzcub_rows(rp, ci, rpb, 0, nrows)
     thr = O.num_threads()
     nproc = os.cpu_count()
-    try:
-        affinity = len(os.sched_getaffinity(0))
-    except (AttributeError, OSError):
-        affinity = None
-    return {"value": round(2.0 * cub / t / 1e9, 4), "unit": "GFLOPS", "cores": thr, "nproc": nproc, "affinity_cpus": affinity,
+    affinity = _AFFINITY
+    # cores actually available to the threads: the OpenMP team, capped by the
+    # process's CPU affinity mask (a lease may expose fewer CPUs than nproc)
+    cores = min(thr, affinity) if affinity else thr
+    return {"value": round(2.0 * cub / t / 1e9, 4), "unit": "GFLOPS", "cores": cores, "omp_threads": thr,
+            "nproc": nproc, "affinity_cpus": affinity,
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
             "kind": "port",
             "sample": f"spgemm_spa restatement (count+fill passes, symbolic), rows [0,{rows}) of {m} "
-                      f"({cub} of the intermediate products), {t:.1f} s; {thr} OpenMP threads "
-                      f"(OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND', 'unset')}) on {_cpu_model()}",
+                      f"({cub} of the intermediate products), {t:.1f} s; {thr} OpenMP threads on {cores} "
+                      f"usable CPU(s) of {nproc} (affinity mask; OMP_PROC_BIND="
+                      f"{os.environ.get('OMP_PROC_BIND', 'unset')}) on {_cpu_model()}",
             "numeric": {"value": round(2.0 * ncub / nt / 1e9, 4), "unit": "GFLOPS",
                         "sample": f"oracle Gustavson (dense-row accumulator, fp64 values), rows [0,{nrows}), "
                                   f"{nt:.1f} s"}}
