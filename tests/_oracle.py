@@ -13,6 +13,8 @@ import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(REPO, "oracle")
 LIB_PATH = os.path.join(ORACLE_DIR, "libtsg_oracle.so")
+# diagnostics: another build of the same restatement (e.g. the ASan build, tools/asan_cpu.sh)
+LIB_PATH = os.environ.get("TSG_ORACLE_LIB", LIB_PATH)
 
 
 class TsgoMat(C.Structure):
