@@ -840,14 +840,50 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
     // pipeline (mc2depi A*A^T: 0.40 vs 0.83 ms).  Web graphs and FEM matrices
     // (long rows) take the staged tile pipeline below, which is faster there.
     // TSG_PATH=fused / tiles forces either path.
+    // Banded path (tsg_band.hip): when every C row's reachable columns fit one
+    // window of <= 2,048 columns holding at least as many products as columns
+    // (FEM-like operands with dense rows, e.g. cant), one walk accumulates the
+    // row in a dense LDS window.  Checked only for rows of >= 8 entries on
+    // average (a statistics kernel + one host round trip).
+    // TSG_PATH=fused / band / tiles forces a path (band when its check passes).
     const char *path = getenv("TSG_PATH");
     const bool force_fused = path && !strcmp(path, "fused"), force_tiles = path && !strcmp(path, "tiles");
+    const bool force_band = path && !strcmp(path, "band");
     if (!force_tiles) {
         TSG_TRY(dev_row_maxlen_async(cx, *A, cx.pinned + 2, s));
         TSG_TRY(dev_row_maxlen_async(cx, *B, cx.pinned + 3, s));
         TSG_HIP(hipStreamSynchronize(s));
         const bool short_rows = (long long)cx.pinned[2] * (long long)cx.pinned[3] <= kFusedMaxRowProducts;
-        if (cx.pinned[1] == 0 && (short_rows || force_fused)) {
+        const bool bsorted0 = cx.pinned[1] == 0;
+        bool band = false;
+        BandWin bw;
+        if (bsorted0 && !force_fused && (force_band || (!short_rows && A->m > 0 && A->nnz >= 8LL * A->m)))
+            TSG_TRY(dev_band_check(cx, *A, *B, force_band, &band, &bw, s));
+        if (band) {
+            TSG_HIP(hipEventRecord(cx.ev[9], s));
+            const int rc = dev_spgemm_band(cx, *A, *B, bw, *C, &st, s, cx.ev);
+            cx.put(bw.win);
+            cx.put(bw.width);
+            TSG_TRY(rc);
+            TSG_HIP(hipEventRecord(cx.ev[10], s));
+            TSG_HIP(hipEventSynchronize(cx.ev[10]));
+            auto h1 = std::chrono::steady_clock::now();
+            st.numtileA = -1;
+            st.numtileB = -1;
+            st.t_csr2tile_ms = ev_ms(cx.ev[8], cx.ev[9]);   // sortedness + window statistics (no csr2tile)
+            st.t_step1_ms = ev_ms(cx.ev[0], cx.ev[1]);      // entry ranges, staging offsets
+            st.t_step2_ms = 0.0;                            // (one walk: structure and values together)
+            st.t_step3_ms = ev_ms(cx.ev[1], cx.ev[3]);      // the row kernel, row pointers, compaction
+            st.t_step3_kernel_ms = ev_ms(cx.ev[4], cx.ev[5]);
+            st.t_tile2csr_ms = 0.0;
+            st.t_kern_ms = ev_ms(cx.ev[0], cx.ev[3]);
+            st.t_e2e_ms = std::chrono::duration<double, std::milli>(h1 - h0).count();
+            st.t_malloc_ms = st.t_e2e_ms - ev_ms(cx.ev[8], cx.ev[10]);
+            if (st.t_malloc_ms < 0) st.t_malloc_ms = 0;
+            if (stats) *stats = st;
+            return TSG_OK;
+        }
+        if (bsorted0 && (short_rows || force_fused)) {
             TSG_HIP(hipEventRecord(cx.ev[9], s));
             TSG_TRY(dev_spgemm_fused(cx, *A, *B, *C, &st, s, cx.ev));
             TSG_HIP(hipEventRecord(cx.ev[10], s));

@@ -1,0 +1,307 @@
+// tsg_band.hip -- banded path of the element TileSpGEMM for gfx950 (wave64):
+// C = A*B, device CSR in -> device CSR out, B's rows column-sorted, every C
+// row's reachable columns inside one window of <= BD_SPAN columns (banded /
+// FEM-like operands such as cant).
+//
+// Reference semantics (paths under /root/reference/src): the same C as steps
+// 1-3 + tile2csr (tilespgemm-cuda.h:279-2218, tile2csr.h:72-140); here the
+// row's window plays the part of the reference's dense accumulator
+// (tilespgemm-cuda.h:1954-2218, `dns`/`ful` bins): with the column span known,
+// every element product lands at acc[col - lo] directly, so structure and
+// values come from ONE walk over the products.
+//
+// One workgroup per C row:
+//   * zero the row's window: an LDS fp64 accumulator acc[span] and one byte
+//     per column;
+//   * walk: a wave per A entry (its entries' B ranges loaded once, one per
+//     lane; the next BD_U entries' B loads in flight during each group's LDS
+//     updates; lane l takes B entries l, l+64, ...): ds_add_f64 of a*b into
+//     acc[c - lo] and a plain byte store marking column c -- the row's C
+//     structure and values together;
+//   * the marks packed into a bitmap; a wave scan of its popcounts gives each
+//     column its rank;
+//   * the row's nonzeros are written in column order to a staging area at the
+//     prefix of the window widths (a window bounds its row's nnz, and for
+//     banded rows nearly equals it), and the row's nnz to the row pointers.
+// A scan of the row counts gives the CSR row pointers and one streaming pass
+// moves every row's run to its final place.  (A decoupled look-back over the
+// rows in place of the staging measured 0.39 ms slower on cant: its chains of
+// row-by-row resolution, not the walk, set the pace.)
+#include "tsg_internal.h"
+#include "tsg_dev_common.h"
+
+#include <cstdlib>
+
+namespace tsg {
+
+namespace {
+
+constexpr int BD_WG = 256;
+constexpr int BD_SPAN = 2048;            // window columns per row: 16 KB fp64 + 256 B bitmap of LDS
+constexpr int BD_WORDS = BD_SPAN / 32;   // bitmap words (= 64: one wave scans them)
+constexpr int BD_U = 4;                  // entries per wave in flight
+static_assert(BD_WORDS == 64, "one bitmap word per lane");
+
+}  // namespace
+
+// Per C row: its column window [lo, hi] (first / last column of the B rows its
+// entries reach; lo > hi for a row without products).  Statistics: bad[0] =
+// rows whose window is wider than BD_SPAN, bad[1] = the widest window,
+// bad[2..3] (u64) = the element products (they bound nnz(C)), bad[4..5] (u64)
+// = the windows' columns in all.
+__global__ __launch_bounds__(WG) void k_band_stats(const int *rpA, const int *ciA, int m, const int *rpB,
+                                                   const int *ciB, int2 *win, long long *width, int *bad) {
+    __shared__ int red[2 * WAVES];
+    __shared__ long long red64[WAVES];
+    int nbad = 0, wmax = 0;
+    long long prod = 0, wsum = 0;
+    for (int r = blockIdx.x * WG + threadIdx.x; r < m; r += gridDim.x * WG) {
+        int lo = INT_MAX, hi = -1;
+        long long q = 0;
+        for (int a = rpA[r]; a < rpA[r + 1]; ++a) {
+            const int k = ciA[a], b0 = rpB[k], b1 = rpB[k + 1];
+            if (b1 > b0) {
+                lo = min(lo, ciB[b0]);
+                hi = max(hi, ciB[b1 - 1]);
+                q += b1 - b0;
+            }
+            if (hi >= lo && hi - lo >= BD_SPAN) break;  // already too wide
+        }
+        const int w = hi >= lo ? hi - lo + 1 : 0;
+        if (w > BD_SPAN) ++nbad;
+        prod += q;
+        wsum += w;
+        wmax = max(wmax, w);
+        win[r] = make_int2(lo, hi);
+        width[r] = w;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) width[m] = 0;
+    int mn = 0;
+    block_minmax(mn, wmax, red);
+    const int tb = block_sum(nbad, red);
+    const long long tp = block_sum(prod, red64);
+    const long long tw = block_sum(wsum, red64);
+    if (threadIdx.x == 0) {
+        if (tb) atomicAdd(&bad[0], tb);
+        if (wmax) atomicMax(&bad[1], wmax);
+        if (tp) atomicAdd(reinterpret_cast<unsigned long long *>(bad + 2), (unsigned long long)tp);
+        if (tw) atomicAdd(reinterpret_cast<unsigned long long *>(bad + 4), (unsigned long long)tw);
+    }
+}
+
+struct BandArgs {
+    const int *rpA;
+    const double *vA;
+    const int2 *ebnd;
+    const int2 *win;
+    const long long *soff;  // staging offset of each row (prefix of the window widths)
+    const int *Bcol;
+    const double *Bval;
+    int *rnnz;              // nnz of each row (the row pointers after a scan)
+    int *Scol;              // staging: each row's columns / values from soff[r]
+    double *Sval;
+};
+
+__global__ __launch_bounds__(BD_WG) void k_band_rows(BandArgs g) {
+    __shared__ double acc[BD_SPAN];
+    __shared__ __align__(16) unsigned char hit[BD_SPAN];      // column reached
+    __shared__ __align__(16) unsigned char bmb[BD_SPAN / 8];  // the bitmap, 8 columns per byte
+    __shared__ int wpre[BD_WORDS];
+    const u32 *bm = reinterpret_cast<const u32 *>(bmb);
+    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    const int r = blockIdx.x;
+    const int2 w = g.win[r];
+    const int lo = w.x, span = w.y >= w.x ? w.y - w.x + 1 : 0;
+    const int nw = (span + 31) >> 5;
+    for (int i = tid; i < span; i += BD_WG) acc[i] = 0.0;
+    reinterpret_cast<uint2 *>(hit)[tid] = make_uint2(0u, 0u);  // 256 x 8 B = BD_SPAN bytes
+    __syncthreads();
+    // ---- the walk: a wave per A entry.  The wave's entries (a0 + wv + 4j) are
+    // loaded once, one per lane, and broadcast from there; the B loads of the
+    // next BD_U entries are issued before this group's LDS updates.
+    const int a0 = g.rpA[r], a1 = g.rpA[r + 1];
+    for (int base = a0 + wv; base < a1; base += 4 * 64) {  // wave-uniform
+        const int my = base + 4 * lane;
+        int2 me = make_int2(0, 0);
+        double mav = 0.0;
+        if (my < a1) {
+            me = g.ebnd[my];
+            mav = g.vA[my];
+        }
+        const int nj = min(64, (a1 - base + 3) / 4);
+        auto load = [&](int j, int o, int *c, double *x, int &mx) {
+            mx = 0;
+#pragma unroll
+            for (int k = 0; k < BD_U; ++k) {
+                const int jj = min(j + k, 63);
+                const int bs = __shfl(me.x, jj, 64), be = j + k < nj ? __shfl(me.y, jj, 64) : bs;
+                const double av = __shfl(mav, jj, 64);
+                mx = max(mx, be - bs);
+                const int bb = bs + o + lane;
+                c[k] = -1;
+                x[k] = 0.0;
+                if (bb < be) {
+                    c[k] = g.Bcol[bb] - lo;
+                    x[k] = av * g.Bval[bb];
+                }
+            }
+        };
+        int c0[BD_U], c1[BD_U], mx0 = 0, mx1 = 0;
+        double x0[BD_U], x1[BD_U];
+        load(0, 0, c0, x0, mx0);
+        for (int j = 0; j < nj; j += BD_U) {
+            if (j + BD_U < nj) load(j + BD_U, 0, c1, x1, mx1);  // in flight during this group's updates
+            for (int o = 0;;) {
+#pragma unroll
+                for (int k = 0; k < BD_U; ++k)
+                    if (c0[k] >= 0) {
+                        atomicAdd(&acc[c0[k]], x0[k]);
+                        hit[c0[k]] = 1;  // (byte stores: an atomicOr into the bitmap put 32 lanes on one word)
+                    }
+                o += 64;
+                if (o >= mx0) break;  // B rows longer than 64: their next 64 entries
+                int t;
+                load(j, o, c0, x0, t);
+            }
+#pragma unroll
+            for (int k = 0; k < BD_U; ++k) {
+                c0[k] = c1[k];
+                x0[k] = x1[k];
+            }
+            mx0 = mx1;
+        }
+    }
+    __syncthreads();
+    {  // pack the marks: thread t's 8 columns [8t, 8t+8) -> bitmap byte t
+        const uint2 v = reinterpret_cast<const uint2 *>(hit)[tid];
+        const unsigned long long x = (unsigned long long)v.x | ((unsigned long long)v.y << 32);
+        bmb[tid] = (unsigned char)((x * 0x0102040810204080ull) >> 56);  // bit j = byte j (each 0 or 1)
+    }
+    __syncthreads();
+    if (wv == 0) {  // ranks: popcount prefix of the bitmap words; the row's nnz
+        const int cnt = lane < nw ? __popc(bm[lane]) : 0;
+        const int inc = wave_incl_scan_dpp(cnt);
+        wpre[lane] = inc - cnt;
+        if (lane == 63) g.rnnz[r] = inc;
+    }
+    __syncthreads();
+    // ---- the row's columns and values, in column order, to the staging area
+    const long long E = g.soff[r];
+    for (int i = tid; i < span; i += BD_WG) {
+        const u32 word = bm[i >> 5], bit = 1u << (i & 31);
+        if (word & bit) {
+            const long long pos = E + wpre[i >> 5] + __popc(word & (bit - 1u));
+            g.Scol[pos] = lo + i;
+            g.Sval[pos] = acc[i];
+        }
+    }
+}
+
+// every row's run from the staging area to its CSR place (wave per row)
+__global__ __launch_bounds__(WG) void k_band_compact(int m, const long long *soff, const int *Crp, const int *Scol,
+                                                     const double *Sval, int *Ccol, double *Cval) {
+    for (int r = blockIdx.x * WAVES + wave_id(); r < m; r += gridDim.x * WAVES) {
+        const long long s0 = soff[r];
+        const int d0 = Crp[r], n = Crp[r + 1] - d0;
+        for (int i = lane_id(); i < n; i += 64) {
+            Ccol[d0 + i] = Scol[s0 + i];
+            Cval[d0 + i] = Sval[s0 + i];
+        }
+    }
+}
+
+// routing: whether every C row's window fits BD_SPAN and the windows are dense
+// (at least as many element products as window columns in all; `force` drops
+// the density test).  Leaves the windows in *win_out (caller-owned, cx.put)
+// when the answer is yes.
+int dev_band_check(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, bool force, bool *ok, BandWin *bw,
+                   hipStream_t s) {
+    *ok = false;
+    *bw = BandWin{};
+    if (A.m <= 0 || A.n != B.m) return TSG_OK;
+    int2 *win = nullptr;
+    long long *width = nullptr;
+    int *bad = nullptr;
+    TSG_TRY(cx.get(&win, (size_t)A.m));
+    TSG_TRY(cx.get(&width, (size_t)A.m + 1));
+    TSG_TRY(cx.get(&bad, 6));
+    TSG_HIP(hipMemsetAsync(bad, 0, 6 * sizeof(int), s));
+    k_band_stats<<<grid_for(A.m, WG, 4096), WG, 0, s>>>(A.rowpointer, A.columnindex, A.m, B.rowpointer,
+                                                        B.columnindex, win, width, bad);
+    TSG_HIP(hipGetLastError());
+    TSG_HIP(hipMemcpyAsync(cx.pinned + 8, bad, 6 * sizeof(int), hipMemcpyDeviceToHost, s));
+    TSG_HIP(hipStreamSynchronize(s));
+    cx.put(bad);
+    const long long products = *reinterpret_cast<const long long *>(cx.pinned + 10);
+    const long long wcols = *reinterpret_cast<const long long *>(cx.pinned + 12);
+    if (cx.pinned[8] == 0 && (force || products >= wcols)) {
+        *ok = true;
+        *bw = BandWin{win, width, products, wcols};
+    } else {
+        cx.put(win);
+        cx.put(width);
+    }
+    return TSG_OK;
+}
+
+__global__ __launch_bounds__(WG) void k_band_ebnd(const int *ciA, long nnzA, const int *rpB, int2 *ebnd) {
+    for (long a = (long)blockIdx.x * WG + threadIdx.x; a < nnzA; a += (long)gridDim.x * WG) {
+        const int k = ciA[a];
+        ebnd[a] = make_int2(rpB[k], rpB[k + 1]);
+    }
+}
+
+// CSR in -> CSR out for a banded product (windows from dev_band_check; their
+// width array becomes the staging offsets).
+// ev (optional): 0 start | 1 set up | 4..5 the row kernel | 3 end
+int dev_spgemm_band(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, BandWin &bw, tsg_dev_csr &C,
+                    tsg_stats *st, hipStream_t s, hipEvent_t *ev) {
+    const int m = A.m;
+    C = tsg_dev_csr{};
+    C.m = m;
+    C.n = B.n;
+    if (ev) TSG_HIP(hipEventRecord(ev[0], s));
+    int2 *ebnd = nullptr;
+    int *Scol = nullptr;
+    double *Sval = nullptr;
+    TSG_TRY(cx.get(&ebnd, (size_t)A.nnz + 1));
+    TSG_TRY(cx.get(&Scol, (size_t)bw.wcols + 1));
+    TSG_TRY(cx.get(&Sval, (size_t)bw.wcols + 1));
+    TSG_TRY(cx.get(&C.rowpointer, (size_t)m + 1));
+    if (A.nnz > 0) k_band_ebnd<<<grid_for(A.nnz, WG, 16384), WG, 0, s>>>(A.columnindex, A.nnz, B.rowpointer, ebnd);
+    TSG_HIP(hipGetLastError());
+    TSG_TRY(scan_exclusive_i64(cx, bw.width, (long)m + 1, s));  // window widths -> staging offsets
+    if (ev) TSG_HIP(hipEventRecord(ev[1], s));
+    if (ev) TSG_HIP(hipEventRecord(ev[4], s));
+    if (m > 0) {
+        BandArgs g{A.rowpointer, A.value, ebnd, bw.win, bw.width, B.columnindex, B.value, C.rowpointer, Scol, Sval};
+        k_band_rows<<<m, BD_WG, 0, s>>>(g);
+        TSG_HIP(hipGetLastError());
+    }
+    if (ev) TSG_HIP(hipEventRecord(ev[5], s));
+    // row counts -> CSR row pointers (nnz(C) <= the window columns; past int32 fails)
+    long long nnz = 0;
+    TSG_HIP(hipMemsetAsync(C.rowpointer + m, 0, sizeof(int), s));
+    TSG_TRY(scan_exclusive_i32_total(cx, C.rowpointer, (long)m + 1, s, &nnz));
+    if (nnz > 0x7fffffffLL) return TSG_ERR_OVERFLOW;
+    C.nnz = (int)nnz;
+    TSG_TRY(cx.get(&C.columnindex, (size_t)nnz + 1));
+    TSG_TRY(cx.get(&C.value, (size_t)nnz + 1));
+    if (m > 0)
+        k_band_compact<<<grid_for(m, WAVES, 16384), WG, 0, s>>>(m, bw.width, C.rowpointer, Scol, Sval, C.columnindex,
+                                                               C.value);
+    TSG_HIP(hipGetLastError());
+    if (ev) TSG_HIP(hipEventRecord(ev[3], s));
+    TSG_HIP(hipStreamSynchronize(s));
+    cx.put(ebnd);
+    cx.put(Scol);
+    cx.put(Sval);
+    if (st) {
+        st->nnzC = C.nnz;
+        st->tile_products = bw.products;
+        st->numblkC = -1;
+    }
+    return TSG_OK;
+}
+
+}  // namespace tsg

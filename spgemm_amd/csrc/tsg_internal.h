@@ -122,6 +122,23 @@ constexpr long long kFusedMaxRowProducts = 256;
 int dev_spgemm_fused(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, tsg_dev_csr &C, tsg_stats *st,
                      hipStream_t s, hipEvent_t *ev);
 
+// banded path (tsg_band.hip): every C row's reachable columns within one
+// window of <= 2,048 columns, the windows holding at least as many products as
+// columns in all (FEM-like operands; force: any density).  BandWin holds the
+// check's results for the product (caller-owned device arrays: win, width).
+struct BandWin {
+    int2 *win = nullptr;         // per row: first and last reachable column
+    long long *width = nullptr;  // per row: window width (+1 slot), scanned into staging offsets
+    long long products = 0;      // element products (nnzCub)
+    long long wcols = 0;         // window columns in all (bounds nnz(C))
+};
+int dev_band_check(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, bool force, bool *ok, BandWin *bw,
+                   hipStream_t s);
+int dev_spgemm_band(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, BandWin &bw, tsg_dev_csr &C,
+                    tsg_stats *st, hipStream_t s, hipEvent_t *ev);
+// exclusive scan (n+1 idiom) whose total is read back
+int scan_exclusive_i32_total(Context &cx, int *a, long n, hipStream_t s, long long *total);
+
 // read a device int / long long synchronously through pinned memory
 int read_i32(Context &cx, const int *d, int *h, hipStream_t s);
 int read_i64(Context &cx, const long long *d, long long *h, hipStream_t s);

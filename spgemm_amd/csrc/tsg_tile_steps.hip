@@ -169,7 +169,6 @@ __global__ __launch_bounds__(WG) void k_tile_crow(const int *Cptr, int tilem, in
         for (int t = Cptr[i]; t < Cptr[i + 1]; ++t) Crow[t] = i;
 }
 
-int scan_exclusive_i32_total(Context &cx, int *a, long n, hipStream_t s, long long *total);
 
 // Steps 2 and 3 at tile size C.tile_m x C.tile_m on the step-1 structure already
 // in C (tile_ptr, tile_columnidx, numtile): fills tile_rowidx, tile_nnz

@@ -167,10 +167,15 @@ def test_mawi_star_small_scale_vs_oracle():
     assert st["nnzC"] == ref.s.nnz
 
 
+@pytest.mark.parametrize("path", [None, "tiles"])
 @pytest.mark.parametrize("name", ["cant", "mc2depi", "webbase"])
-def test_full_size_synthetic_vs_oracle(name):
+def test_full_size_synthetic_vs_oracle(name, path, monkeypatch):
     """BASELINE configs at full size (synthetic stand-ins): pattern bit-exact,
-    values exact, against the numeric Gustavson oracle."""
+    values exact, against the numeric Gustavson oracle -- on the default route
+    (cant: banded path, mc2depi: fused path, webbase: staged) and forced
+    through the staged tile pipeline."""
+    if path:
+        monkeypatch.setenv("TSG_PATH", path)
     m, n, rp, ci, vv = synth.GENERATORS[name]()
     A = T.Matrix.from_csr(m, n, rp, ci, vv)
     if name == "mc2depi":  # config 3 is C = A*A^T
@@ -187,9 +192,9 @@ def test_full_size_synthetic_vs_oracle(name):
     assert st["nnzC"] == ref.s.nnz
     # the staged pipeline's A/B tile counts (wave hash sets + bitmap fallback for
     # tile rows over 256 entries) equal the oracle csr2tile's numtile (the fused
-    # short-row path builds no A/B tiles and reports -1)
+    # and banded paths build no A/B tiles and report -1)
     if st["numtileA"] < 0:
-        assert name == "mc2depi"
+        assert path is None and name in ("mc2depi", "cant")
         return
     tA = O.OMat.from_csr(m, n, rp, ci, vv)
     O.csr2tile_row_major(tA, 16, 16)
@@ -246,6 +251,7 @@ def test_step2_modes_match_oracle(mode, case, monkeypatch):
     the CSR operands vs tile-level mask ORs) give the oracle's product; an
     unsorted B falls back to the tile payload path in either mode."""
     monkeypatch.setenv("TSG_STEP2_MODE", mode)
+    monkeypatch.setenv("TSG_PATH", "tiles")  # the staged pipeline (the banded input would route elsewhere)
     if case == "rand_sparse":
         m, n, rp, ci, vv = synth.random_csr(5000, 5000, density=0.0008, seed=21)
     elif case == "rand_dense":

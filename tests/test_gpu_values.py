@@ -71,6 +71,7 @@ def test_fixtures_real_values(name, kind):
 @pytest.mark.parametrize("name", ["webbase", "cant"])
 def test_full_size_real_values_both_step2_modes(name, mode, monkeypatch):
     monkeypatch.setenv("TSG_STEP2_MODE", mode)
+    monkeypatch.setenv("TSG_PATH", "tiles")  # the staged pipeline's step-2 modes
     m, n, rp, ci, _ = synth.GENERATORS[name]()
     va = _vals("uniform", len(ci), 3)
     _check(m, n, rp, ci, va, m, n, rp, ci, va, alias=True)
@@ -86,3 +87,11 @@ def test_wide_magnitude_random_and_rerun_spread():
     oA = O.OMat.from_csr(m, n, rp, ci, np.abs(va))
     mag = O.gustavson(oA, O.OMat.alias(oA)).csr()[4]
     assert np.all(np.abs(g1 - g2) <= 2 * RTOL * mag)
+
+
+def test_full_size_real_values_default_routes():
+    """cant's default route (the banded path) with real values."""
+    m, n, rp, ci, _ = synth.GENERATORS["cant"]()
+    va = _vals("uniform", len(ci), 7)
+    _, st = _check(m, n, rp, ci, va, m, n, rp, ci, va, alias=True)
+    assert st["numblkC"] == -1
