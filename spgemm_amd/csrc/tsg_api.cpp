@@ -848,7 +848,7 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
     // TSG_PATH=fused / band / tiles forces a path (band when its check passes).
     const char *path = getenv("TSG_PATH");
     const bool force_fused = path && !strcmp(path, "fused"), force_tiles = path && !strcmp(path, "tiles");
-    const bool force_band = path && !strcmp(path, "band");
+    const bool force_band = path && !strcmp(path, "band"), force_rows = path && !strcmp(path, "rows");
     if (!force_tiles) {
         TSG_TRY(dev_row_maxlen_async(cx, *A, cx.pinned + 2, s));
         TSG_TRY(dev_row_maxlen_async(cx, *B, cx.pinned + 3, s));
@@ -857,23 +857,29 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
         const bool bsorted0 = cx.pinned[1] == 0;
         bool band = false;
         BandWin bw;
-        if (bsorted0 && !force_fused && (force_band || (!short_rows && A->m > 0 && A->nnz >= 8LL * A->m)))
+        if (bsorted0 && !force_fused && !force_rows &&
+            (force_band || (!short_rows && A->m > 0 && A->nnz >= 8LL * A->m)))
             TSG_TRY(dev_band_check(cx, *A, *B, force_band, &band, &bw, s));
-        if (band) {
+        const bool rows = bsorted0 && force_rows;
+        if (band || rows) {
             TSG_HIP(hipEventRecord(cx.ev[9], s));
-            const int rc = dev_spgemm_band(cx, *A, *B, bw, *C, &st, s, cx.ev);
-            cx.put(bw.win);
-            cx.put(bw.width);
-            TSG_TRY(rc);
+            if (band) {
+                const int rc = dev_spgemm_band(cx, *A, *B, bw, *C, &st, s, cx.ev);
+                cx.put(bw.win);
+                cx.put(bw.width);
+                TSG_TRY(rc);
+            } else {
+                TSG_TRY(dev_spgemm_rows(cx, *A, *B, *C, &st, s, cx.ev));
+            }
             TSG_HIP(hipEventRecord(cx.ev[10], s));
             TSG_HIP(hipEventSynchronize(cx.ev[10]));
             auto h1 = std::chrono::steady_clock::now();
             st.numtileA = -1;
             st.numtileB = -1;
-            st.t_csr2tile_ms = ev_ms(cx.ev[8], cx.ev[9]);   // sortedness + window statistics (no csr2tile)
-            st.t_step1_ms = ev_ms(cx.ev[0], cx.ev[1]);      // entry ranges, staging offsets
+            st.t_csr2tile_ms = ev_ms(cx.ev[8], cx.ev[9]);   // sortedness (+ band: window statistics; no csr2tile)
+            st.t_step1_ms = ev_ms(cx.ev[0], cx.ev[1]);      // entry ranges, staging offsets (+ rows: classes)
             st.t_step2_ms = 0.0;                            // (one walk: structure and values together)
-            st.t_step3_ms = ev_ms(cx.ev[1], cx.ev[3]);      // the row kernel, row pointers, compaction
+            st.t_step3_ms = ev_ms(cx.ev[1], cx.ev[3]);      // the row kernel(s), row pointers, compaction
             st.t_step3_kernel_ms = ev_ms(cx.ev[4], cx.ev[5]);
             st.t_tile2csr_ms = 0.0;
             st.t_kern_ms = ev_ms(cx.ev[0], cx.ev[3]);

@@ -136,6 +136,12 @@ int dev_band_check(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, bool
                    hipStream_t s);
 int dev_spgemm_band(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, BandWin &bw, tsg_dev_csr &C,
                     tsg_stats *st, hipStream_t s, hipEvent_t *ev);
+// row-merge path (tsg_rows.hip): CSR in -> CSR out, B's rows column-sorted;
+// rows binned by element products, each row's B rows merged (or, for the
+// longest rows, marked in an LDS column bitmap).
+// ev (optional): 0 start | 1 set up | 4..5 the row kernels | 3 end
+int dev_spgemm_rows(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, tsg_dev_csr &C, tsg_stats *st,
+                    hipStream_t s, hipEvent_t *ev);
 // exclusive scan (n+1 idiom) whose total is read back
 int scan_exclusive_i32_total(Context &cx, int *a, long n, hipStream_t s, long long *total);
 

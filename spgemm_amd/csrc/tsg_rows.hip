@@ -1,0 +1,710 @@
+// tsg_rows.hip -- row-merge path of the element TileSpGEMM for gfx950 (wave64):
+// C = A*B, device CSR in -> device CSR out, B's rows column-sorted, for
+// operands whose C rows are long and spread over the whole column range with
+// little merging (web graphs such as webbase-1M: 69 M element products give
+// 65 M nonzeros, so C is nearly the product expansion itself).
+//
+// Reference semantics (paths under /root/reference/src): the same C as steps
+// 1-3 + tile2csr (tilespgemm-cuda.h:279-2218, tile2csr.h:72-140) -- every C
+// row the column-sorted union of the scaled B rows its A entries select, equal
+// columns summed.  The reference reaches it through the tile structure; here a
+// row's B rows ARE its sorted runs, so the row is built by merging them:
+//
+//   * entry table: each A entry's B range and a prefix of the element products
+//     over all entries (one int64 scan) -- a row's products, its staging
+//     offset and its runs' offsets are differences of that prefix;
+//   * rows binned by products (and runs) into four classes, each with a kernel
+//     shaped for it:
+//       S  <= 64 products : a wave per row, ranks by counting in registers;
+//       M1 <= 512         : a wave per row, pairwise merges of the runs in LDS;
+//       M2 <= 4,096       : a workgroup per row, the same merges;
+//       H  longer         : a workgroup per row, a bitmap of a column window in
+//                           LDS, ranks by popcount, values by f64 atomics;
+//     the merge keys are (column, run, position) so they are unique and the
+//     merged order -- hence every sum's order -- is deterministic (class H's
+//     atomics are the exception);
+//   * each row writes its nonzeros, column-sorted, to a staging area at the
+//     prefix of the products (products bound nnz), and its nnz; a scan of the
+//     counts gives the CSR row pointers, one streaming pass the final arrays.
+#include "tsg_internal.h"
+#include "tsg_dev_common.h"
+
+#include <cstdio>
+
+namespace tsg {
+
+namespace {
+
+constexpr int RS_MAX = 64;            // class S: products (and runs) per row
+// merge classes M1..M4: products and runs per row, threads per row -- each
+// sized so its LDS (16 B per product + 16 B per run) keeps several rows per CU
+constexpr int M1_CAP = 512, M1_RUNS = 128, M1_NT = 128;    // 10 KB
+constexpr int M2_CAP = 1024, M2_RUNS = 256, M2_NT = 256;   // 20 KB
+constexpr int M3_CAP = 2048, M3_RUNS = 512, M3_NT = 512;   // 40 KB
+constexpr int M4_CAP = 4096, M4_RUNS = 512, M4_NT = 1024;  // 72 KB
+constexpr int NCLS = 6;               // S, M1..M4, H
+constexpr int BIN_ROWS = 2048;        // rows per workgroup of the binning kernel
+constexpr int RH_NT = 1024;           // class H: workgroup
+constexpr int RH_WORDS = 8192;        // class H: bitmap words (u64) per window
+constexpr long long RH_SPAN = (long long)RH_WORDS * 64;  // columns per window (524,288)
+constexpr int RH_BLK = 512;           // words per u16 in-block prefix block (<= 32,768 bits)
+constexpr int RH_NBLK = RH_WORDS / RH_BLK;
+
+__device__ __forceinline__ u32 lanes_below(u64 b) {
+    return __builtin_amdgcn_mbcnt_hi((u32)(b >> 32), __builtin_amdgcn_mbcnt_lo((u32)b, 0u));
+}
+__device__ __forceinline__ int key_col(u64 k) { return (int)(k >> 32); }
+
+}  // namespace
+
+// TSG_ROWS_PROF builds (make prof): per-phase wall-clock totals of the class
+// kernels' workgroups (thread 0 after each phase's barrier), printed per call
+#ifdef TSG_ROWS_PROF
+__device__ unsigned long long g_rows_prof[3][256][8];  // (spread over 256 slots: few same-address atomics)
+#define RP_INIT unsigned long long rp_acc[8] = {}, rp_t = wall_clock64();
+#define RP(k)                                         \
+    do {                                              \
+        const unsigned long long _t = wall_clock64(); \
+        rp_acc[k] += _t - rp_t;                       \
+        rp_t = _t;                                    \
+    } while (0)
+#define RP_DONE(K)                                                          \
+    do {                                                                    \
+        if (threadIdx.x == 0)                                               \
+            for (int _k = 0; _k < 8; ++_k) atomicAdd(&g_rows_prof[K][blockIdx.x & 255][_k], rp_acc[_k]); \
+    } while (0)
+#else
+#define RP_INIT
+#define RP(k) \
+    do {      \
+    } while (0)
+#define RP_DONE(K) \
+    do {           \
+    } while (0)
+#endif
+
+struct RowsArgs {
+    const int *rpA;
+    const double *vA;
+    const int2 *ebnd;      // per A entry: its B row's [start, end)
+    const long long *E;    // per A entry: prefix of the element products (E[nnzA] = all)
+    const int *Bcol;
+    const double *Bval;
+    const int *list;       // the class's rows
+    int nrows;
+    int *rnnz;             // nnz of each row (the row pointers after a scan)
+    int *Scol;             // staging: row r's nonzeros from E[rpA[r]]
+    double *Sval;
+};
+
+// per A entry: its B row's range and products (the latter scanned into E)
+__global__ __launch_bounds__(WG) void k_rows_entries(const int *ciA, long nnzA, const int *rpB, int2 *ebnd,
+                                                     long long *E) {
+    for (long a = (long)blockIdx.x * WG + threadIdx.x; a <= nnzA; a += (long)gridDim.x * WG) {
+        if (a == nnzA) {
+            E[a] = 0;
+            break;
+        }
+        const int k = ciA[a], b0 = rpB[k], b1 = rpB[k + 1];
+        ebnd[a] = make_int2(b0, b1);
+        E[a] = b1 - b0;
+    }
+}
+
+__device__ __forceinline__ int row_class(const int *rpA, const long long *E, int r) {
+    const int a0 = rpA[r], a1 = rpA[r + 1], k = a1 - a0;
+    const long long P = E[a1] - E[a0];
+    if (P == 0) return -1;
+    if (P <= RS_MAX && k <= RS_MAX) return 0;
+    if (P <= M1_CAP && k <= M1_RUNS) return 1;
+    if (P <= M2_CAP && k <= M2_RUNS) return 2;
+    if (P <= M3_CAP && k <= M3_RUNS) return 3;
+    if (P <= M4_CAP && k <= M4_RUNS) return 4;
+    return 5;
+}
+
+// rows -> classes: lists (class c's rows from lists + c*m) and counts cls[0..NCLS);
+// rows without products get nnz 0.  A workgroup per BIN_ROWS rows: its counts
+// first (one atomic per class), then its rows in order into the reserved slots.
+__global__ __launch_bounds__(WG) void k_rows_bin(const int *rpA, int m, const long long *E, int *rnnz, int *lists,
+                                                 int *cls) {
+    __shared__ int wc[NCLS][WAVES];
+    __shared__ int gb[NCLS];
+    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    const int r0 = blockIdx.x * BIN_ROWS, r1 = min(m, r0 + BIN_ROWS);
+    int n[NCLS] = {};
+    for (int r = r0 + tid; r < r1; r += WG) {
+        const int c = row_class(rpA, E, r);
+        if (c < 0) rnnz[r] = 0;
+#pragma unroll
+        for (int t = 0; t < NCLS; ++t) n[t] += c == t;
+    }
+#pragma unroll
+    for (int t = 0; t < NCLS; ++t) {
+        const int v = wave_sum(n[t]);
+        if (lane == 0) wc[t][wv] = v;
+    }
+    __syncthreads();
+    if (tid < NCLS) {
+        int v = 0;
+        for (int w = 0; w < WAVES; ++w) v += wc[tid][w];
+        gb[tid] = v ? atomicAdd(&cls[tid], v) : 0;
+    }
+    __syncthreads();
+    int run[NCLS];
+#pragma unroll
+    for (int t = 0; t < NCLS; ++t) run[t] = gb[t];
+    for (int rb = r0; rb < r1; rb += WG) {
+        const int r = rb + tid;
+        const int c = r < r1 ? row_class(rpA, E, r) : -1;
+        u64 bt[NCLS];
+#pragma unroll
+        for (int t = 0; t < NCLS; ++t) {
+            bt[t] = __ballot(c == t);
+            if (lane == 0) wc[t][wv] = __popcll(bt[t]);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < NCLS; ++t) {
+            int pre = 0, tot = 0;
+            for (int w = 0; w < WAVES; ++w) {
+                const int v = wc[t][w];
+                pre += w < wv ? v : 0;
+                tot += v;
+            }
+            if (c == t) lists[(long)t * m + run[t] + pre + lanes_below(bt[t])] = r;
+            run[t] += tot;
+        }
+        __syncthreads();
+    }
+}
+
+// ---- class S: a wave per row, the products one per lane, ranks by counting
+__global__ __launch_bounds__(WG) void k_rows_small(RowsArgs g) {
+    __shared__ u64 sk[WAVES][64];
+    __shared__ double sv[WAVES][64];
+    const int lane = lane_id(), wv = wave_id();
+    const int i = blockIdx.x * WAVES + wv;
+    if (i >= g.nrows) return;  // wave-uniform
+    const int r = g.list[i];
+    const int a0 = g.rpA[r], k = g.rpA[r + 1] - a0;
+    const long long base = g.E[a0];
+    const int P = (int)(g.E[a0 + k] - base);
+    // lane j < k: run j's offset in the row, B start and A value
+    int roff = 0, bs = 0;
+    double av = 0.0;
+    if (lane < k) {
+        roff = (int)(g.E[a0 + lane] - base);
+        bs = g.ebnd[a0 + lane].x;
+        av = g.vA[a0 + lane];
+    }
+    // lane e < P: its run = the last run starting at or before e
+    int run = 0;
+    for (int j = 1; j < k; ++j) run = (__builtin_amdgcn_readlane(roff, j) <= lane) ? j : run;
+    const int rs = __shfl(roff, run, 64), rb = __shfl(bs, run, 64);
+    const double ra = __shfl(av, run, 64);
+    u64 key = ~0ull;
+    double x = 0.0;
+    if (lane < P) {
+        const int p = rb + lane - rs;
+        key = ((u64)(u32)g.Bcol[p] << 32) | (u32)lane;
+        x = ra * g.Bval[p];
+    }
+    int rank = 0;
+    for (int f = 0; f < P; ++f) {
+        const u64 kf = ((u64)(u32)__builtin_amdgcn_readlane((int)(key >> 32), f) << 32) |
+                       (u32)__builtin_amdgcn_readlane((int)(u32)key, f);
+        rank += kf < key;
+    }
+    if (lane < P) {
+        sk[wv][rank] = key;
+        sv[wv][rank] = x;
+    }
+    wave_lds_sync();
+    int col = -1;
+    bool head = false;
+    if (lane < P) {
+        col = key_col(sk[wv][lane]);
+        head = lane == 0 || key_col(sk[wv][lane - 1]) != col;
+    }
+    const u64 hb = __ballot(head);
+    if (head) {
+        double s = sv[wv][lane];
+        for (int j = lane + 1; j < P && key_col(sk[wv][j]) == col; ++j) s += sv[wv][j];
+        const long long o = base + lanes_below(hb);
+        g.Scol[o] = col;
+        g.Sval[o] = s;
+    }
+    if (lane == 0) g.rnnz[r] = __popcll(hb);
+}
+
+// U independent searches in lockstep (U LDS reads in flight per step): first
+// index in [b, b + len) whose element is >= key (or > key where ub[u])
+template <int U, class T>
+__device__ __forceinline__ void search_ilp(const T *a, int (&b)[U], int (&len)[U], const T (&key)[U],
+                                           const bool (&ub)[U]) {
+    for (;;) {
+        bool more = false;
+#pragma unroll
+        for (int u = 0; u < U; ++u) more |= len[u] > 0;
+        if (!more) break;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int half = len[u] >> 1, idx = b[u] + half;
+            const T v = a[len[u] > 0 ? idx : 0];  // (finished searches: one broadcast address)
+            const bool go = len[u] > 0 && (v < key[u] || (ub[u] && v == key[u]));
+            b[u] = go ? idx + 1 : b[u];
+            len[u] = go ? len[u] - half - 1 : half;
+        }
+    }
+}
+
+// ---- classes M1..M4: pairwise stable merges of the row's runs in LDS.  NT
+// threads per row, at most CAP products and RUNS runs.  Keys are the columns
+// (u32) with a (run, position) payload.  Thread t owns the positions
+// [t*ipt, t*ipt + ipt) of every pass (ipt odd, so the lanes' LDS accesses
+// spread over the banks): its global loads are issued together (IPM = the
+// largest ipt, unrolled), and each merge round is a merge path -- one co-rank
+// search per pair the chunk touches, then a sequential merge with ties taken
+// from the left group first, so equal columns stay in run order and every sum
+// is taken in one fixed order.
+template <int NT, int CAP, int RUNS>
+__global__ __launch_bounds__(NT) void k_rows_merge(RowsArgs g) {
+    constexpr int NW = NT / 64;
+    constexpr int IPM = (CAP + NT - 1) / NT | 1;
+    __shared__ u32 kp[2][2][CAP];   // [buffer][keys | payloads]
+    __shared__ int roff[RUNS + 1];
+    __shared__ int rbs[RUNS];       // each run's B start
+    __shared__ double rav[RUNS];    // each run's A value
+    __shared__ int red[NW];
+    RP_INIT
+    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    const int r = g.list[blockIdx.x];
+    const int a0 = g.rpA[r], k = g.rpA[r + 1] - a0;
+    const long long base = g.E[a0];
+    const int P = (int)(g.E[a0 + k] - base);
+    for (int j = tid; j <= k; j += NT) {
+        roff[j] = (int)(g.E[a0 + j] - base);
+        if (j < k) {
+            rbs[j] = g.ebnd[a0 + j].x;
+            rav[j] = g.vA[a0 + j];
+        }
+    }
+    __syncthreads();
+    RP(0);
+    const int ipt = ((P + NT - 1) / NT) | 1;
+    const int q0 = min(P, tid * ipt), q1 = min(P, q0 + ipt), nq = q1 - q0;
+    // expansion: position q of run j at roff[j] + t -> key Bcol, payload (j, t)
+    {
+        int j = 0;
+        if (nq > 0) {  // the run holding q0: the last run starting at or before it
+            int lo = 0, len = k;
+            while (len > 0) {
+                const int half = len >> 1;
+                if (roff[lo + half] <= q0) {
+                    lo += half + 1;
+                    len -= half + 1;
+                } else {
+                    len = half;
+                }
+            }
+            j = lo - 1;
+        }
+        int pa[IPM];
+        u32 py[IPM];
+#pragma unroll
+        for (int u = 0; u < IPM; ++u)
+            if (u < nq) {
+                const int q = q0 + u;
+                while (roff[j + 1] <= q) ++j;
+                pa[u] = rbs[j] + q - roff[j];
+                py[u] = ((u32)j << 16) | (u32)(q - roff[j]);
+            }
+        int c[IPM];
+#pragma unroll
+        for (int u = 0; u < IPM; ++u)
+            if (u < nq) c[u] = g.Bcol[pa[u]];
+#pragma unroll
+        for (int u = 0; u < IPM; ++u)
+            if (u < nq) {
+                kp[0][0][q0 + u] = (u32)c[u];
+                kp[0][1][q0 + u] = py[u];
+            }
+    }
+    __syncthreads();
+    RP(1);
+    // rounds: groups of 2^lw runs merged pairwise
+    int src = 0;
+    for (int lw = 0; (1 << lw) < k; ++lw) {
+        const u32 *ik = kp[src][0], *ip = kp[src][1];
+        u32 *ok = kp[src ^ 1][0], *op = kp[src ^ 1][1];
+        for (int q = q0; q < q1;) {
+            const int pr = (int)(ip[q] >> 16) >> (lw + 1);  // input position q lies in the pair it outputs to
+            const int ps = roff[pr << (lw + 1)];
+            const int pm = roff[min((2 * pr + 1) << lw, k)];
+            const int pe = roff[min((pr + 1) << (lw + 1), k)];
+            const int la = pm - ps, lb = pe - pm, qq = q - ps;
+            int lo = max(0, qq - lb), hi = min(qq, la);
+            while (lo < hi) {
+                const int i = (lo + hi) >> 1;
+                if (ik[ps + i] <= ik[pm + qq - i - 1]) lo = i + 1; else hi = i;
+            }
+            int i = lo, j = qq - lo;
+            u32 ka = i < la ? ik[ps + i] : ~0u, kb = j < lb ? ik[pm + j] : ~0u;  // (columns < 2^31)
+            const int qe = min(q1, pe);
+            for (; q < qe; ++q) {
+                const bool ta = ka <= kb;
+                const int from = ta ? ps + i : pm + j;
+                ok[q] = ta ? ka : kb;
+                op[q] = ip[from];
+                i += ta;
+                j += !ta;
+                const int nx = ta ? (i < la ? ps + i : -1) : (j < lb ? pm + j : -1);
+                const u32 kn = nx >= 0 ? ik[nx] : ~0u;
+                ka = ta ? kn : ka;
+                kb = ta ? kb : kn;
+            }
+        }
+        __syncthreads();
+        src ^= 1;
+    }
+    RP(2);
+    const u32 *sk = kp[src][0], *sp = kp[src][1];
+    double *vb = reinterpret_cast<double *>(&kp[src ^ 1][0][0]);  // the free buffer: each position's product
+    int nh = 0;  // heads (first position of each column) in the chunk
+    {
+        int pa[IPM];
+        double av[IPM];
+#pragma unroll
+        for (int u = 0; u < IPM; ++u)
+            if (u < nq) {
+                const u32 pj = sp[q0 + u];
+                const int ru = (int)(pj >> 16);
+                pa[u] = rbs[ru] + (int)(pj & 0xffffu);
+                av[u] = rav[ru];
+                nh += (q0 + u == 0 || sk[q0 + u] != sk[q0 + u - 1]);
+            }
+        double x[IPM];
+#pragma unroll
+        for (int u = 0; u < IPM; ++u)
+            if (u < nq) x[u] = av[u] * g.Bval[pa[u]];
+#pragma unroll
+        for (int u = 0; u < IPM; ++u)
+            if (u < nq) vb[q0 + u] = x[u];
+    }
+    // the chunk's first output slot: exclusive scan of the head counts
+    const int inc = wave_incl_scan_dpp(nh);
+    if (lane == 63) red[wv] = inc;
+    __syncthreads();
+    RP(3);
+    int o = inc - nh, tot = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        o += w < wv ? red[w] : 0;
+        tot += red[w];
+    }
+    if (tid == 0) g.rnnz[r] = tot;
+    for (int q = q0; q < q1; ++q) {
+        const u32 col = sk[q];
+        if (q == 0 || sk[q - 1] != col) {
+            double sum = vb[q];
+            for (int j = q + 1; j < P && sk[j] == col; ++j) sum += vb[j];  // ascending: deterministic
+            g.Scol[base + o] = (int)col;
+            g.Sval[base + o] = sum;
+            ++o;
+        }
+    }
+    RP(4);
+    RP_DONE(CAP == M1_CAP ? 2 : 1);  // (M1 | M2..M4)
+}
+
+// ---- class H: a workgroup per row; windows of RH_SPAN columns, each a bitmap
+// in LDS.  The row's products are walked in batches of RH_NT runs (a thread per
+// run: lengths scanned over the workgroup, then the batch's products flattened
+// over all threads, U at a time).
+struct WalkTab {
+    int pre[RH_NT];     // products before each run of the batch
+    int bs[RH_NT];      // B start
+    double av[RH_NT];   // A value
+    int red[RH_NT / 64];
+};
+template <bool VAL, class F>
+__device__ __forceinline__ void rows_walk(const RowsArgs &g, int a0, int k, WalkTab &tb, F &&f) {
+    constexpr int U = 4, NW = RH_NT / 64;
+    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    for (int b0 = 0; b0 < k; b0 += RH_NT) {
+        const int j = b0 + tid;
+        int2 be = make_int2(0, 0);
+        double av = 0.0;
+        if (j < k) {
+            be = g.ebnd[a0 + j];
+            av = g.vA[a0 + j];
+        }
+        const int len = be.y - be.x;
+        const int inc = wave_incl_scan_dpp(len);
+        if (lane == 63) tb.red[wv] = inc;
+        __syncthreads();
+        int woff = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            const int v = tb.red[w];
+            woff += w < wv ? v : 0;
+            tot += v;
+        }
+        tb.pre[tid] = woff + inc - len;
+        tb.bs[tid] = be.x;
+        tb.av[tid] = av;
+        __syncthreads();
+        const int nb = min(RH_NT, k - b0);
+        for (int q0 = 0; q0 < tot; q0 += U * RH_NT) {
+            int b[U], len2[U], q[U], p[U], c[U];
+            double x[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                q[u] = q0 + u * RH_NT + tid;
+                b[u] = 0;
+                len2[u] = q[u] < tot ? nb : 0;
+            }
+            const bool ub[U] = {true, true, true, true};
+            search_ilp(tb.pre, b, len2, q, ub);  // b - 1 = the run holding product q
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (q[u] < tot) {
+                    p[u] = tb.bs[b[u] - 1] + q[u] - tb.pre[b[u] - 1];
+                    c[u] = g.Bcol[p[u]];
+                    if (VAL) x[u] = tb.av[b[u] - 1] * g.Bval[p[u]];
+                }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (q[u] < tot) f(c[u], VAL ? x[u] : 0.0);
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(RH_NT) void k_rows_bitmap(RowsArgs g) {
+    __shared__ u64 bm[RH_WORDS];
+    __shared__ u16 wpre[RH_WORDS];     // each word's bits before it in its block
+    __shared__ int bpre_blk[RH_NBLK];  // each block's bits before it in the window
+    __shared__ WalkTab wt;
+    __shared__ int red[2 * (RH_NT / 64)];
+    constexpr int NW = RH_NT / 64;
+    RP_INIT
+    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    const int r = g.list[blockIdx.x];
+    const int a0 = g.rpA[r], k = g.rpA[r + 1] - a0;
+    const long long base = g.E[a0];
+    // the row's columns [lo, hi]
+    int lo = INT_MAX, hi = -1;
+    for (int j = tid; j < k; j += RH_NT) {
+        const int2 be = g.ebnd[a0 + j];
+        if (be.y > be.x) {
+            lo = min(lo, g.Bcol[be.x]);
+            hi = max(hi, g.Bcol[be.y - 1]);
+        }
+    }
+    lo = wave_last(wave_incl_dpp(lo, INT_MAX, OpMin{}));
+    hi = wave_last(wave_incl_dpp(hi, INT_MIN, OpMax{}));
+    if (lane == 0) {
+        red[wv] = lo;
+        red[NW + wv] = hi;
+    }
+    __syncthreads();
+    lo = red[0];
+    hi = red[NW];
+    for (int w = 1; w < NW; ++w) {
+        lo = min(lo, red[w]);
+        hi = max(hi, red[NW + w]);
+    }
+    RP(0);
+    long long out = 0;  // nonzeros of the earlier windows
+    for (long long wlo = lo; wlo <= hi; wlo += RH_SPAN) {
+        const long long whi = min((long long)hi, wlo + RH_SPAN - 1);
+        const int nwd = (int)((whi - wlo + 64) >> 6);
+        for (int i = tid; i < nwd; i += RH_NT) bm[i] = 0ull;
+        __syncthreads();
+        RP(1);
+        rows_walk<false>(g, a0, k, wt, [&](int col, double) {
+            const long long c = (long long)col - wlo;
+            if (c >= 0 && c < RH_SPAN) atomicOr(&bm[c >> 6], 1ull << (c & 63));
+        });
+        __syncthreads();
+        RP(2);
+        // ranks: u16 prefix inside each 512-word block, then the blocks' prefix
+        if (wv < RH_NBLK) {  // wave per block: 8 words per lane
+            int s = 0;
+            int cw[RH_BLK / 64];
+#pragma unroll
+            for (int u = 0; u < RH_BLK / 64; ++u) {
+                const int wi = wv * RH_BLK + lane * (RH_BLK / 64) + u;
+                cw[u] = wi < nwd ? __popcll(bm[wi]) : 0;
+                s += cw[u];
+            }
+            const int inc = wave_incl_scan_dpp(s);
+            int acc = inc - s;
+#pragma unroll
+            for (int u = 0; u < RH_BLK / 64; ++u) {
+                wpre[wv * RH_BLK + lane * (RH_BLK / 64) + u] = (u16)acc;
+                acc += cw[u];
+            }
+            if (lane == 63) bpre_blk[wv] = inc;
+        }
+        __syncthreads();
+        if (wv == 0) {
+            const int v = lane < RH_NBLK ? bpre_blk[lane] : 0;
+            const int inc = wave_incl_scan_dpp(v);
+            if (lane < RH_NBLK) bpre_blk[lane] = inc - v;
+            if (lane == 63) red[0] = inc;
+        }
+        __syncthreads();
+        const int wn = red[0];
+        RP(3);
+        // the window's nonzeros: columns, zeroed values, then the f64 sums
+        for (int i = tid; i < nwd; i += RH_NT) {
+            u64 b = bm[i];
+            long long o = base + out + bpre_blk[i / RH_BLK] + wpre[i];
+            while (b) {
+                const int t = __builtin_ctzll(b);
+                g.Scol[o] = (int)(wlo + ((long long)i << 6) + t);
+                g.Sval[o] = 0.0;
+                ++o;
+                b &= b - 1;
+            }
+        }
+        __syncthreads();  // (workgroup scope: the zeros and the atomics meet in this XCD's L2; an
+                          // agent-scope fence here wrote the L2 back, ~85 us per window)
+        RP(4);
+        rows_walk<true>(g, a0, k, wt, [&](int col, double x) {
+            const long long c = (long long)col - wlo;
+            if (c >= 0 && c < RH_SPAN) {
+                const int wi = (int)(c >> 6);
+                const u64 below = bm[wi] & ((1ull << (c & 63)) - 1ull);
+                const long long o = base + out + bpre_blk[wi / RH_BLK] + wpre[wi] + __popcll(below);
+                __hip_atomic_fetch_add(&g.Sval[o], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        });
+        out += wn;
+        __syncthreads();
+        RP(5);
+    }
+    if (tid == 0) g.rnnz[r] = (int)out;
+    RP_DONE(0);
+}
+
+// every row's run from the staging area (at E[rpA[r]]) to its CSR place
+__global__ __launch_bounds__(WG) void k_rows_compact(int m, const int *rpA, const long long *E, const int *Crp,
+                                                     const int *Scol, const double *Sval, int *Ccol, double *Cval) {
+    for (int r = blockIdx.x * WAVES + wave_id(); r < m; r += gridDim.x * WAVES) {
+        const int d0 = Crp[r], n = Crp[r + 1] - d0;
+        if (n == 0) continue;
+        const long long s0 = E[rpA[r]];
+        for (int i = lane_id(); i < n; i += 64) {
+            Ccol[d0 + i] = Scol[s0 + i];
+            Cval[d0 + i] = Sval[s0 + i];
+        }
+    }
+}
+
+// CSR in -> CSR out (B's rows column-sorted; the caller checked).
+// ev (optional): 0 start | 1 set up | 4..5 the row kernels | 3 end
+int dev_spgemm_rows(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, tsg_dev_csr &C, tsg_stats *st,
+                    hipStream_t s, hipEvent_t *ev) {
+    const int m = A.m;
+    C = tsg_dev_csr{};
+    C.m = m;
+    C.n = B.n;
+    if (ev) TSG_HIP(hipEventRecord(ev[0], s));
+    int2 *ebnd = nullptr;
+    long long *E = nullptr;
+    int *lists = nullptr, *cls = nullptr;
+    TSG_TRY(cx.get(&ebnd, (size_t)A.nnz + 1));
+    TSG_TRY(cx.get(&E, (size_t)A.nnz + 1));
+    TSG_TRY(cx.get(&lists, (size_t)NCLS * (m > 0 ? m : 1)));
+    TSG_TRY(cx.get(&cls, 8));
+    TSG_TRY(cx.get(&C.rowpointer, (size_t)m + 1));
+    TSG_HIP(hipMemsetAsync(cls, 0, 8 * sizeof(int), s));
+    k_rows_entries<<<grid_for((long)A.nnz + 1, WG, 16384), WG, 0, s>>>(A.columnindex, A.nnz, B.rowpointer, ebnd, E);
+    TSG_HIP(hipGetLastError());
+    TSG_TRY(scan_exclusive_i64(cx, E, (long)A.nnz + 1, s));
+    if (m > 0) k_rows_bin<<<(m + BIN_ROWS - 1) / BIN_ROWS, WG, 0, s>>>(A.rowpointer, m, E, C.rowpointer, lists, cls);
+    TSG_HIP(hipGetLastError());
+    TSG_HIP(hipMemcpyAsync(cx.pinned64, E + A.nnz, sizeof(long long), hipMemcpyDeviceToHost, s));
+    TSG_HIP(hipMemcpyAsync(cx.pinned64 + 1, cls, NCLS * sizeof(int), hipMemcpyDeviceToHost, s));
+    TSG_HIP(hipStreamSynchronize(s));
+    const long long products = cx.pinned64[0];
+    int ncls[NCLS];
+    for (int t = 0; t < NCLS; ++t) ncls[t] = reinterpret_cast<const int *>(cx.pinned64 + 1)[t];
+    int *Scol = nullptr;
+    double *Sval = nullptr;
+    TSG_TRY(cx.get(&Scol, (size_t)products + 1));
+    TSG_TRY(cx.get(&Sval, (size_t)products + 1));
+    if (ev) TSG_HIP(hipEventRecord(ev[1], s));
+    if (ev) TSG_HIP(hipEventRecord(ev[4], s));
+#ifdef TSG_ROWS_PROF
+    unsigned long long *dprof = nullptr;
+    TSG_HIP(hipGetSymbolAddress((void **)&dprof, HIP_SYMBOL(g_rows_prof)));
+    TSG_HIP(hipMemsetAsync(dprof, 0, sizeof(unsigned long long) * 3 * 256 * 8, s));
+#endif
+    RowsArgs g{A.rowpointer, A.value, ebnd, E, B.columnindex, B.value, nullptr, 0, C.rowpointer, Scol, Sval};
+    // heaviest classes first: their workgroups start before the short rows fill the machine
+    auto launch = [&](int c, auto kern, int grid, int nt) -> int {
+        if (ncls[c] == 0) return TSG_OK;
+        g.list = lists + (long)c * m;
+        g.nrows = ncls[c];
+        kern<<<grid, nt, 0, s>>>(g);
+        TSG_HIP(hipGetLastError());
+        return TSG_OK;
+    };
+    TSG_TRY(launch(5, k_rows_bitmap, ncls[5], RH_NT));
+    TSG_TRY(launch(4, k_rows_merge<M4_NT, M4_CAP, M4_RUNS>, ncls[4], M4_NT));
+    TSG_TRY(launch(3, k_rows_merge<M3_NT, M3_CAP, M3_RUNS>, ncls[3], M3_NT));
+    TSG_TRY(launch(2, k_rows_merge<M2_NT, M2_CAP, M2_RUNS>, ncls[2], M2_NT));
+    TSG_TRY(launch(1, k_rows_merge<M1_NT, M1_CAP, M1_RUNS>, ncls[1], M1_NT));
+    TSG_TRY(launch(0, k_rows_small, (ncls[0] + WAVES - 1) / WAVES, WG));
+    if (ev) TSG_HIP(hipEventRecord(ev[5], s));
+#ifdef TSG_ROWS_PROF
+    {
+        static unsigned long long raw[3 * 256 * 8];
+        unsigned long long pr[24] = {};
+        TSG_HIP(hipMemcpyAsync(raw, dprof, sizeof(raw), hipMemcpyDeviceToHost, s));
+        TSG_HIP(hipStreamSynchronize(s));
+        for (int c = 0; c < 3; ++c)
+            for (int b = 0; b < 256; ++b)
+                for (int k = 0; k < 8; ++k) pr[c * 8 + k] += raw[(c * 256 + b) * 8 + k];
+        static const char *nm[3] = {"H", "M2-M4", "M1"};
+        for (int c = 0; c < 3; ++c) {
+            const int cnt = c == 0 ? ncls[5] : c == 1 ? ncls[2] + ncls[3] + ncls[4] : ncls[1];
+            fprintf(stderr, "rows %s (%d rows) us/row:", nm[c], cnt);
+            for (int k = 0; k < 6; ++k) fprintf(stderr, " %.2f", cnt ? pr[c * 8 + k] / 100.0 / cnt : 0.0);
+            fprintf(stderr, "\n");
+        }
+    }
+#endif
+    long long nnz = 0;
+    TSG_HIP(hipMemsetAsync(C.rowpointer + m, 0, sizeof(int), s));
+    TSG_TRY(scan_exclusive_i32_total(cx, C.rowpointer, (long)m + 1, s, &nnz));
+    if (nnz > 0x7fffffffLL) return TSG_ERR_OVERFLOW;
+    C.nnz = (int)nnz;
+    TSG_TRY(cx.get(&C.columnindex, (size_t)nnz + 1));
+    TSG_TRY(cx.get(&C.value, (size_t)nnz + 1));
+    if (m > 0)
+        k_rows_compact<<<grid_for(m, WAVES, 16384), WG, 0, s>>>(m, A.rowpointer, E, C.rowpointer, Scol, Sval,
+                                                               C.columnindex, C.value);
+    TSG_HIP(hipGetLastError());
+    if (ev) TSG_HIP(hipEventRecord(ev[3], s));
+    TSG_HIP(hipStreamSynchronize(s));
+    cx.put(ebnd);
+    cx.put(E);
+    cx.put(lists);
+    cx.put(cls);
+    cx.put(Scol);
+    cx.put(Sval);
+    if (st) {
+        st->nnzC = C.nnz;
+        st->tile_products = products;
+        st->numblkC = -1;
+    }
+    return TSG_OK;
+}
+
+}  // namespace tsg

@@ -1,0 +1,168 @@
+"""The row-merge path (spgemm_amd/csrc/tsg_rows.hip): rows binned by element
+products into six classes -- S (<= 64, ranks by counting in a wave), M1..M4
+(<= 512 / 1,024 / 2,048 / 4,096 products: pairwise merge-path merges of the
+runs in LDS) and H (longer rows or more runs: an LDS column bitmap per window
+of 524,288 columns, f64 atomics for the values).  TSG_PATH=rows forces it.  Pattern
+bit-exact, values within 1e-10 relative, against the oracle (the reference's
+semantics: steps 1-3 + tile2csr, tilespgemm-cuda.h:279-2218)."""
+import numpy as np
+import pytest
+
+import _oracle as O
+from spgemm_amd import synth
+from spgemm_amd import tilespgemm as T
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def rows_path(monkeypatch):
+    monkeypatch.setenv("TSG_PATH", "rows")
+
+
+def _csr(m, n, rows):
+    """CSR from a list of per-row column arrays (kept in the given order)"""
+    lens = [len(c) for c in rows]
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    ci = (np.concatenate(rows) if sum(lens) else np.zeros(0)).astype(np.int32)
+    vv = (np.arange(len(ci)) % 10).astype(np.float64)
+    return m, n, rp, ci, vv
+
+
+def _check(A_, B_=None, aat=False, real=False, seed=0):
+    m, n, rp, ci, vv = A_
+    if real:
+        vv = np.random.default_rng(seed).uniform(-1, 1, len(ci))
+    A = T.Matrix.from_csr(m, n, rp, ci, vv)
+    oA = O.OMat.from_csr(m, n, rp, ci, vv)
+    if aat:
+        B, oB = T.transpose(A), O.transpose(oA)
+    elif B_ is None:
+        B, oB = T.Matrix.alias(A), O.OMat.alias(oA)
+    else:
+        bm, bn, brp, bci, bvv = B_
+        if real:
+            bvv = np.random.default_rng(seed + 1).uniform(-1, 1, len(bci))
+        B, oB = T.Matrix.from_csr(bm, bn, brp, bci, bvv), O.OMat.from_csr(bm, bn, brp, bci, bvv)
+    Cm, st = T.spgemm(A, B)
+    got, ref = Cm.csr(), O.gustavson(oA, oB).csr()
+    np.testing.assert_array_equal(got[2], ref[2])
+    np.testing.assert_array_equal(got[3], ref[3])
+    if real:
+        oM = O.OMat.from_csr(m, n, rp, ci, np.abs(vv))
+        oMb = O.transpose(oM) if aat else (O.OMat.alias(oM) if B_ is None else
+                                           O.OMat.from_csr(bm, bn, brp, bci, np.abs(bvv)))
+        mag = O.gustavson(oM, oMb).csr()[4]
+        assert np.all(np.abs(got[4] - ref[4]) <= 1e-10 * mag)
+    else:
+        np.testing.assert_allclose(got[4], ref[4], rtol=1e-10, atol=0)
+    assert st["nnzC"] == len(ref[3])
+    assert st["numblkC"] == -1 and st["numtileA"] == -1  # the row-merge path ran
+    return st
+
+
+# (products, runs) caps of the classes S, M1..M4; longer rows are class H (= 5)
+CAPS = [(64, 64), (512, 128), (1024, 256), (2048, 512), (4096, 512)]
+
+
+def _classes(m, n, rp, ci, rpB):
+    """per row: (products, runs) -> class as tsg_rows.hip bins them (-1: no products)"""
+    blen = np.diff(rpB.astype(np.int64))
+    cum = np.concatenate([[0], np.cumsum(blen[ci])])
+    P = cum[rp[1:]] - cum[rp[:-1]]
+    k = np.diff(rp)
+    c = np.full(m, -1)
+    c[(P > 0)] = 5
+    for i in range(4, -1, -1):
+        c[(P > 0) & (P <= CAPS[i][0]) & (k <= CAPS[i][1])] = i
+    return c
+
+
+@pytest.mark.parametrize("name", ["webbase", "cant", "mc2depi"])
+def test_rows_full_size_synthetic(name):
+    m, n, rp, ci, vv = synth.GENERATORS[name]()
+    cls = _classes(m, n, rp, ci, rp)
+    if name == "webbase":  # every class is populated
+        assert all((cls == c).any() for c in range(6))
+    _check((m, n, rp, ci, vv), aat=name == "mc2depi")
+
+
+def test_rows_webbase_real_values():
+    _check(synth.GENERATORS["webbase"](), real=True, seed=3)
+
+
+def test_rows_random_mixed_classes_real_values():
+    rng = np.random.default_rng(11)
+    n = 5000
+    rows = []
+    for i in range(3000):  # row lengths spread over 0..600 so every class appears
+        L = int(rng.choice([0, 1, 2, 3, 5, 8, 20, 60, 150, 600], p=[.1, .2, .15, .15, .1, .1, .08, .06, .04, .02]))
+        rows.append(np.sort(rng.choice(n, size=min(L, n), replace=False)))
+    A = _csr(3000, n, rows)
+    Bm = synth.random_csr(n, 7000, density=0.003, seed=12)
+    B = (Bm[0], Bm[1], Bm[2], np.concatenate([np.sort(Bm[3][Bm[2][i]:Bm[2][i + 1]]) for i in range(n)]).astype(np.int32),
+         Bm[4])
+    cls = _classes(3000, n, A[2], A[3], B[2])
+    assert all((cls == c).any() for c in range(5))
+    _check(A, B, real=True, seed=5)
+
+
+def test_rows_edge_cases():
+    # empty matrix rows, a single row, a row selecting empty B rows only
+    _check(_csr(5, 5, [[], [0, 1], [], [4], []]))
+    _check(_csr(1, 1, [[0]]))
+    B = _csr(4, 6, [[], [1, 5], [], [0, 2, 3]])
+    _check(_csr(3, 4, [[0, 2], [1, 3], [0]]), B)
+
+
+def test_rows_duplicate_runs_sum():
+    # an A row naming the same B row twice (duplicate entries): equal keys of two
+    # runs merge and sum
+    A = _csr(2, 3, [[1, 1, 2], [0, 2, 2, 2]])
+    B = _csr(3, 8, [[0, 7], [1, 3, 4], [3, 4, 6]])
+    _check(A, B, real=True, seed=9)
+
+
+def test_rows_many_runs_go_to_bitmap():
+    # 2,000 runs of one column each (k > 1,024 -> class H) + a dense tail
+    n = 40000
+    rng = np.random.default_rng(4)
+    hub = np.sort(rng.choice(n, size=2000, replace=False))
+    rows = [hub] + [np.sort(rng.choice(n, size=3, replace=False)) for _ in range(200)]
+    A = _csr(201, n, rows)
+    Bm, Bn, Brp, Bci, Bvv = synth.random_csr(n, n, density=3e-5, seed=6)
+    Bci = np.concatenate([np.sort(Bci[Brp[i]:Brp[i + 1]]) for i in range(n)]).astype(np.int32)
+    assert _classes(201, n, A[2], A[3], Brp)[0] == 5
+    _check(A, (Bm, Bn, Brp, Bci, Bvv), real=True, seed=8)
+
+
+def test_rows_bitmap_several_windows():
+    # class H rows over 2,000,000 columns: four windows of 524,288 columns,
+    # including empty windows in between
+    n = 2_000_000
+    rng = np.random.default_rng(7)
+    k = 20
+    Brows = []
+    for j in range(k):
+        lo = 0 if j % 2 == 0 else 1_600_000
+        Brows.append(np.sort(rng.choice(np.arange(lo, lo + 400_000), size=400, replace=False)))
+    B = _csr(k, n, Brows)
+    A = _csr(3, k, [np.arange(k), np.arange(0, k, 2), np.array([1, 3])])
+    assert _classes(3, k, A[2], A[3], B[2])[0] == 5
+    _check(A, B, real=True, seed=2)
+
+
+def test_rows_merge_long_runs_and_collisions():
+    # class M3 / M4 rows whose runs collide heavily (banded B): many equal columns
+    rows = [np.arange(max(0, i - 30), min(2000, i + 31)) for i in range(2000)]
+    A = _csr(2000, 2000, rows)
+    cls = _classes(2000, 2000, A[2], A[3], A[2])
+    assert (cls == 4).any() and (cls == 3).any() and (cls >= 3).all()
+    _check(A, real=True, seed=4)
+
+
+def test_rows_aat_lj_prefix():
+    m, n, rp, ci, vv = synth.GENERATORS["lj"]()
+    r = 20000
+    e = int(rp[r])
+    _check((r, n, rp[:r + 1].copy(), ci[:e].copy(), vv[:e].copy()), aat=True)
