@@ -45,10 +45,11 @@ constexpr int M4_CAP = 4096, M4_RUNS = 512, M4_NT = 1024;  // 72 KB
 constexpr int NCLS = 6;               // S, M1..M4, H
 constexpr int BIN_ROWS = 2048;        // rows per workgroup of the binning kernel
 constexpr int RH_NT = 1024;           // class H: workgroup
-constexpr int RH_WORDS = 8192;        // class H: bitmap words (u64) per window
-constexpr long long RH_SPAN = (long long)RH_WORDS * 64;  // columns per window (524,288)
-constexpr int RH_BLK = 512;           // words per u16 in-block prefix block (<= 32,768 bits)
+constexpr int RH_WORDS = 16384;       // class H: bitmap words (u64) per window: 128 KB of LDS
+constexpr long long RH_SPAN = (long long)RH_WORDS * 64;  // columns per window (1,048,576)
+constexpr int RH_BLK = 512;           // words per rank block (int prefix); u16 prefix per 4-word group inside
 constexpr int RH_NBLK = RH_WORDS / RH_BLK;
+constexpr int RH_NGRP = RH_WORDS / 4;
 
 __device__ __forceinline__ u32 lanes_below(u64 b) {
     return __builtin_amdgcn_mbcnt_hi((u32)(b >> 32), __builtin_amdgcn_mbcnt_lo((u32)b, 0u));
@@ -111,9 +112,10 @@ __global__ __launch_bounds__(WG) void k_rows_entries(const int *ciA, long nnzA, 
     }
 }
 
-__device__ __forceinline__ int row_class(const int *rpA, const long long *E, int r) {
+__device__ __forceinline__ int row_class(const int *rpA, const long long *E, int r, long long *soff = nullptr) {
     const int a0 = rpA[r], a1 = rpA[r + 1], k = a1 - a0;
-    const long long P = E[a1] - E[a0];
+    const long long e0 = E[a0], P = E[a1] - e0;
+    if (soff) soff[r] = e0;
     if (P == 0) return -1;
     if (P <= RS_MAX && k <= RS_MAX) return 0;
     if (P <= M1_CAP && k <= M1_RUNS) return 1;
@@ -127,14 +129,14 @@ __device__ __forceinline__ int row_class(const int *rpA, const long long *E, int
 // rows without products get nnz 0.  A workgroup per BIN_ROWS rows: its counts
 // first (one atomic per class), then its rows in order into the reserved slots.
 __global__ __launch_bounds__(WG) void k_rows_bin(const int *rpA, int m, const long long *E, int *rnnz, int *lists,
-                                                 int *cls) {
+                                                 int *cls, long long *soff) {
     __shared__ int wc[NCLS][WAVES];
     __shared__ int gb[NCLS];
     const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
     const int r0 = blockIdx.x * BIN_ROWS, r1 = min(m, r0 + BIN_ROWS);
     int n[NCLS] = {};
     for (int r = r0 + tid; r < r1; r += WG) {
-        const int c = row_class(rpA, E, r);
+        const int c = row_class(rpA, E, r, soff);  // (+ the row's staging offset)
         if (c < 0) rnnz[r] = 0;
 #pragma unroll
         for (int t = 0; t < NCLS; ++t) n[t] += c == t;
@@ -427,35 +429,45 @@ struct WalkTab {
     int bs[RH_NT];      // B start
     double av[RH_NT];   // A value
     int red[RH_NT / 64];
+    int tot;            // the batch's products
 };
+// a batch's run table (thread per run; lengths scanned over the workgroup)
+__device__ __forceinline__ void rows_batch(const RowsArgs &g, int a0, int k, int b0, WalkTab &tb) {
+    constexpr int NW = RH_NT / 64;
+    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    const int j = b0 + tid;
+    int2 be = make_int2(0, 0);
+    double av = 0.0;
+    if (j < k) {
+        be = g.ebnd[a0 + j];
+        av = g.vA[a0 + j];
+    }
+    const int len = be.y - be.x;
+    const int inc = wave_incl_scan_dpp(len);
+    if (lane == 63) tb.red[wv] = inc;
+    __syncthreads();
+    int woff = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        const int v = tb.red[w];
+        woff += w < wv ? v : 0;
+        tot += v;
+    }
+    tb.pre[tid] = woff + inc - len;
+    tb.bs[tid] = be.x;
+    tb.av[tid] = av;
+    if (tid == 0) tb.tot = tot;
+    __syncthreads();
+}
+// every product of the row (its column, and with VAL its a*b) to f; the run
+// table is reloaded per batch unless the row has one batch (loaded by the caller)
 template <bool VAL, class F>
 __device__ __forceinline__ void rows_walk(const RowsArgs &g, int a0, int k, WalkTab &tb, F &&f) {
-    constexpr int U = 4, NW = RH_NT / 64;
-    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    constexpr int U = 4;
+    const int tid = threadIdx.x;
     for (int b0 = 0; b0 < k; b0 += RH_NT) {
-        const int j = b0 + tid;
-        int2 be = make_int2(0, 0);
-        double av = 0.0;
-        if (j < k) {
-            be = g.ebnd[a0 + j];
-            av = g.vA[a0 + j];
-        }
-        const int len = be.y - be.x;
-        const int inc = wave_incl_scan_dpp(len);
-        if (lane == 63) tb.red[wv] = inc;
-        __syncthreads();
-        int woff = 0, tot = 0;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) {
-            const int v = tb.red[w];
-            woff += w < wv ? v : 0;
-            tot += v;
-        }
-        tb.pre[tid] = woff + inc - len;
-        tb.bs[tid] = be.x;
-        tb.av[tid] = av;
-        __syncthreads();
-        const int nb = min(RH_NT, k - b0);
+        if (k > RH_NT) rows_batch(g, a0, k, b0, tb);
+        const int nb = min(RH_NT, k - b0), tot = tb.tot;
         for (int q0 = 0; q0 < tot; q0 += U * RH_NT) {
             int b[U], len2[U], q[U], p[U], c[U];
             double x[U];
@@ -478,14 +490,28 @@ __device__ __forceinline__ void rows_walk(const RowsArgs &g, int a0, int k, Walk
             for (int u = 0; u < U; ++u)
                 if (q[u] < tot) f(c[u], VAL ? x[u] : 0.0);
         }
-        __syncthreads();
+        if (k > RH_NT) __syncthreads();
     }
 }
 
+// ranks inside a window: blk[w / RH_BLK] + g4[w / 4] + the bits of the
+// group's earlier words + the bits below c in its word
+__device__ __forceinline__ int bm_rank(const u64 *bm, const u16 *g4, const int *blk, long long c) {
+    const int w = (int)(c >> 6), gi = w >> 2, sub = w & 3;
+    const ulonglong2 lo = reinterpret_cast<const ulonglong2 *>(bm)[gi * 2];
+    const ulonglong2 hi = reinterpret_cast<const ulonglong2 *>(bm)[gi * 2 + 1];
+    const u64 word = sub == 0 ? lo.x : sub == 1 ? lo.y : sub == 2 ? hi.x : hi.y;
+    int rk = blk[w / RH_BLK] + g4[gi] + __popcll(word & ((1ull << (c & 63)) - 1ull));
+    rk += sub > 0 ? __popcll(lo.x) : 0;
+    rk += sub > 1 ? __popcll(lo.y) : 0;
+    rk += sub > 2 ? __popcll(hi.x) : 0;
+    return rk;
+}
+
 __global__ __launch_bounds__(RH_NT) void k_rows_bitmap(RowsArgs g) {
-    __shared__ u64 bm[RH_WORDS];
-    __shared__ u16 wpre[RH_WORDS];     // each word's bits before it in its block
-    __shared__ int bpre_blk[RH_NBLK];  // each block's bits before it in the window
+    __shared__ __align__(16) u64 bm[RH_WORDS];
+    __shared__ u16 g4[RH_NGRP];       // each 4-word group's bits before it in its block
+    __shared__ int blk[RH_NBLK];      // each block's bits before it in the window
     __shared__ WalkTab wt;
     __shared__ int red[2 * (RH_NT / 64)];
     constexpr int NW = RH_NT / 64;
@@ -516,6 +542,7 @@ __global__ __launch_bounds__(RH_NT) void k_rows_bitmap(RowsArgs g) {
         lo = min(lo, red[w]);
         hi = max(hi, red[NW + w]);
     }
+    if (k <= RH_NT) rows_batch(g, a0, k, 0, wt);  // one batch: its run table serves every walk
     RP(0);
     long long out = 0;  // nonzeros of the earlier windows
     for (long long wlo = lo; wlo <= hi; wlo += RH_SPAN) {
@@ -530,56 +557,41 @@ __global__ __launch_bounds__(RH_NT) void k_rows_bitmap(RowsArgs g) {
         });
         __syncthreads();
         RP(2);
-        // ranks: u16 prefix inside each 512-word block, then the blocks' prefix
-        if (wv < RH_NBLK) {  // wave per block: 8 words per lane
-            int s = 0;
-            int cw[RH_BLK / 64];
+        // ranks: a wave per 512-word block (lane: two 4-word groups), then the blocks
+        for (int b = wv; b < RH_NBLK; b += NW) {
+            const int w0 = b * RH_BLK + lane * 8;
+            int s0 = 0, s1 = 0;
 #pragma unroll
-            for (int u = 0; u < RH_BLK / 64; ++u) {
-                const int wi = wv * RH_BLK + lane * (RH_BLK / 64) + u;
-                cw[u] = wi < nwd ? __popcll(bm[wi]) : 0;
-                s += cw[u];
+            for (int u = 0; u < 4; ++u) {
+                s0 += w0 + u < nwd ? __popcll(bm[w0 + u]) : 0;
+                s1 += w0 + 4 + u < nwd ? __popcll(bm[w0 + 4 + u]) : 0;
             }
-            const int inc = wave_incl_scan_dpp(s);
-            int acc = inc - s;
-#pragma unroll
-            for (int u = 0; u < RH_BLK / 64; ++u) {
-                wpre[wv * RH_BLK + lane * (RH_BLK / 64) + u] = (u16)acc;
-                acc += cw[u];
-            }
-            if (lane == 63) bpre_blk[wv] = inc;
+            const int inc = wave_incl_scan_dpp(s0 + s1);
+            g4[w0 / 4] = (u16)(inc - s0 - s1);
+            g4[w0 / 4 + 1] = (u16)(inc - s1);
+            if (lane == 63) blk[b] = inc;
         }
         __syncthreads();
         if (wv == 0) {
-            const int v = lane < RH_NBLK ? bpre_blk[lane] : 0;
+            const int v = lane < RH_NBLK ? blk[lane] : 0;
             const int inc = wave_incl_scan_dpp(v);
-            if (lane < RH_NBLK) bpre_blk[lane] = inc - v;
+            if (lane < RH_NBLK) blk[lane] = inc - v;
             if (lane == 63) red[0] = inc;
         }
         __syncthreads();
         const int wn = red[0];
         RP(3);
-        // the window's nonzeros: columns, zeroed values, then the f64 sums
-        for (int i = tid; i < nwd; i += RH_NT) {
-            u64 b = bm[i];
-            long long o = base + out + bpre_blk[i / RH_BLK] + wpre[i];
-            while (b) {
-                const int t = __builtin_ctzll(b);
-                g.Scol[o] = (int)(wlo + ((long long)i << 6) + t);
-                g.Sval[o] = 0.0;
-                ++o;
-                b &= b - 1;
-            }
-        }
+        // the window's values zeroed (coalesced); the walk below stores each column
+        // at its rank (a column's products store the same value) and adds the values
+        for (int i = tid; i < wn; i += RH_NT) g.Sval[base + out + i] = 0.0;
         __syncthreads();  // (workgroup scope: the zeros and the atomics meet in this XCD's L2; an
                           // agent-scope fence here wrote the L2 back, ~85 us per window)
         RP(4);
         rows_walk<true>(g, a0, k, wt, [&](int col, double x) {
             const long long c = (long long)col - wlo;
             if (c >= 0 && c < RH_SPAN) {
-                const int wi = (int)(c >> 6);
-                const u64 below = bm[wi] & ((1ull << (c & 63)) - 1ull);
-                const long long o = base + out + bpre_blk[wi / RH_BLK] + wpre[wi] + __popcll(below);
+                const long long o = base + out + bm_rank(bm, g4, blk, c);
+                g.Scol[o] = col;
                 __hip_atomic_fetch_add(&g.Sval[o], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
         });
@@ -591,16 +603,43 @@ __global__ __launch_bounds__(RH_NT) void k_rows_bitmap(RowsArgs g) {
     RP_DONE(0);
 }
 
-// every row's run from the staging area (at E[rpA[r]]) to its CSR place
-__global__ __launch_bounds__(WG) void k_rows_compact(int m, const int *rpA, const long long *E, const int *Crp,
-                                                     const int *Scol, const double *Sval, int *Ccol, double *Cval) {
-    for (int r = blockIdx.x * WAVES + wave_id(); r < m; r += gridDim.x * WAVES) {
-        const int d0 = Crp[r], n = Crp[r + 1] - d0;
-        if (n == 0) continue;
-        const long long s0 = E[rpA[r]];
-        for (int i = lane_id(); i < n; i += 64) {
-            Ccol[d0 + i] = Scol[s0 + i];
-            Cval[d0 + i] = Sval[s0 + i];
+// every row's run from the staging area (at E[rpA[r]]) to its CSR place: a
+// wave per 4 consecutive rows -- 16 lanes per row while all four are short,
+// else the whole wave on each row in turn; the next group's row pointers and
+// staging offsets are loaded before this group's copy
+__global__ __launch_bounds__(WG) void k_rows_compact(int m, const long long *soff, const int *Crp, const int *Scol,
+                                                     const double *Sval, int *Ccol, double *Cval) {
+    const int lane = lane_id(), sub = lane >> 4, sl = lane & 15;
+    const int step = gridDim.x * WAVES * 4;
+    int rb = (blockIdx.x * WAVES + wave_id()) * 4;
+    int nd0 = 0, nd1 = 0;
+    long long ns0 = 0;
+    auto fetch = [&](int b) {
+        const int r = min(b + sub, m - 1);
+        nd0 = Crp[r];
+        nd1 = b + sub < m ? Crp[r + 1] : nd0;
+        ns0 = soff[r];
+    };
+    if (rb < m) fetch(rb);
+    for (; rb < m; rb += step) {
+        const int d0 = nd0, n = nd1 - nd0;
+        const long long s0 = ns0;
+        if (rb + step < m) fetch(rb + step);
+        const int mx = max(max(__shfl(n, 0, 64), __shfl(n, 16, 64)), max(__shfl(n, 32, 64), __shfl(n, 48, 64)));
+        if (mx <= 32) {
+            for (int i = sl; i < n; i += 16) {
+                Ccol[d0 + i] = Scol[s0 + i];
+                Cval[d0 + i] = Sval[s0 + i];
+            }
+        } else {
+            for (int q = 0; q < 4; ++q) {
+                const int dq = __shfl(d0, q * 16, 64), nq = __shfl(n, q * 16, 64);
+                const long long sq = __shfl(s0, q * 16, 64);
+                for (int i = lane; i < nq; i += 64) {
+                    Ccol[dq + i] = Scol[sq + i];
+                    Cval[dq + i] = Sval[sq + i];
+                }
+            }
         }
     }
 }
@@ -620,13 +659,15 @@ int dev_spgemm_rows(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, tsg
     TSG_TRY(cx.get(&ebnd, (size_t)A.nnz + 1));
     TSG_TRY(cx.get(&E, (size_t)A.nnz + 1));
     TSG_TRY(cx.get(&lists, (size_t)NCLS * (m > 0 ? m : 1)));
+    long long *soff = nullptr;
+    TSG_TRY(cx.get(&soff, (size_t)m + 1));
     TSG_TRY(cx.get(&cls, 8));
     TSG_TRY(cx.get(&C.rowpointer, (size_t)m + 1));
     TSG_HIP(hipMemsetAsync(cls, 0, 8 * sizeof(int), s));
     k_rows_entries<<<grid_for((long)A.nnz + 1, WG, 16384), WG, 0, s>>>(A.columnindex, A.nnz, B.rowpointer, ebnd, E);
     TSG_HIP(hipGetLastError());
     TSG_TRY(scan_exclusive_i64(cx, E, (long)A.nnz + 1, s));
-    if (m > 0) k_rows_bin<<<(m + BIN_ROWS - 1) / BIN_ROWS, WG, 0, s>>>(A.rowpointer, m, E, C.rowpointer, lists, cls);
+    if (m > 0) k_rows_bin<<<(m + BIN_ROWS - 1) / BIN_ROWS, WG, 0, s>>>(A.rowpointer, m, E, C.rowpointer, lists, cls, soff);
     TSG_HIP(hipGetLastError());
     TSG_HIP(hipMemcpyAsync(cx.pinned64, E + A.nnz, sizeof(long long), hipMemcpyDeviceToHost, s));
     TSG_HIP(hipMemcpyAsync(cx.pinned64 + 1, cls, NCLS * sizeof(int), hipMemcpyDeviceToHost, s));
@@ -646,21 +687,24 @@ int dev_spgemm_rows(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, tsg
     TSG_HIP(hipMemsetAsync(dprof, 0, sizeof(unsigned long long) * 3 * 256 * 8, s));
 #endif
     RowsArgs g{A.rowpointer, A.value, ebnd, E, B.columnindex, B.value, nullptr, 0, C.rowpointer, Scol, Sval};
-    // heaviest classes first: their workgroups start before the short rows fill the machine
-    auto launch = [&](int c, auto kern, int grid, int nt) -> int {
+    // the classes are independent: each on a stream of its own, so that the short
+    // rows' workgroups fill the CUs around the long rows' (H first: longest)
+    TSG_TRY(cx.aux_fork(s));
+    auto launch = [&](int c, auto kern, int grid, int nt, hipStream_t st) -> int {
         if (ncls[c] == 0) return TSG_OK;
         g.list = lists + (long)c * m;
         g.nrows = ncls[c];
-        kern<<<grid, nt, 0, s>>>(g);
+        kern<<<grid, nt, 0, st>>>(g);
         TSG_HIP(hipGetLastError());
         return TSG_OK;
     };
-    TSG_TRY(launch(5, k_rows_bitmap, ncls[5], RH_NT));
-    TSG_TRY(launch(4, k_rows_merge<M4_NT, M4_CAP, M4_RUNS>, ncls[4], M4_NT));
-    TSG_TRY(launch(3, k_rows_merge<M3_NT, M3_CAP, M3_RUNS>, ncls[3], M3_NT));
-    TSG_TRY(launch(2, k_rows_merge<M2_NT, M2_CAP, M2_RUNS>, ncls[2], M2_NT));
-    TSG_TRY(launch(1, k_rows_merge<M1_NT, M1_CAP, M1_RUNS>, ncls[1], M1_NT));
-    TSG_TRY(launch(0, k_rows_small, (ncls[0] + WAVES - 1) / WAVES, WG));
+    TSG_TRY(launch(5, k_rows_bitmap, ncls[5], RH_NT, cx.aux[0]));
+    TSG_TRY(launch(4, k_rows_merge<M4_NT, M4_CAP, M4_RUNS>, ncls[4], M4_NT, cx.aux[1]));
+    TSG_TRY(launch(3, k_rows_merge<M3_NT, M3_CAP, M3_RUNS>, ncls[3], M3_NT, cx.aux[2]));
+    TSG_TRY(launch(2, k_rows_merge<M2_NT, M2_CAP, M2_RUNS>, ncls[2], M2_NT, cx.aux[3]));
+    TSG_TRY(launch(1, k_rows_merge<M1_NT, M1_CAP, M1_RUNS>, ncls[1], M1_NT, s));
+    TSG_TRY(launch(0, k_rows_small, (ncls[0] + WAVES - 1) / WAVES, WG, s));
+    TSG_TRY(cx.aux_join(s));
     if (ev) TSG_HIP(hipEventRecord(ev[5], s));
 #ifdef TSG_ROWS_PROF
     {
@@ -688,7 +732,7 @@ int dev_spgemm_rows(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, tsg
     TSG_TRY(cx.get(&C.columnindex, (size_t)nnz + 1));
     TSG_TRY(cx.get(&C.value, (size_t)nnz + 1));
     if (m > 0)
-        k_rows_compact<<<grid_for(m, WAVES, 16384), WG, 0, s>>>(m, A.rowpointer, E, C.rowpointer, Scol, Sval,
+        k_rows_compact<<<grid_for(m, 4 * WAVES, 16384), WG, 0, s>>>(m, soff, C.rowpointer, Scol, Sval,
                                                                C.columnindex, C.value);
     TSG_HIP(hipGetLastError());
     if (ev) TSG_HIP(hipEventRecord(ev[3], s));
@@ -696,6 +740,7 @@ int dev_spgemm_rows(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, tsg
     cx.put(ebnd);
     cx.put(E);
     cx.put(lists);
+    cx.put(soff);
     cx.put(cls);
     cx.put(Scol);
     cx.put(Sval);
