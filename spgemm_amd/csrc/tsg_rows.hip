@@ -354,19 +354,21 @@ __global__ __launch_bounds__(NT) void k_rows_merge(RowsArgs g) {
             int i = lo, j = qq - lo;
             u32 ka = i < la ? ik[ps + i] : ~0u, kb = j < lb ? ik[pm + j] : ~0u;  // (columns < 2^31)
             const int qe = min(q1, pe);
-            for (; q < qe; ++q) {
+            for (; q < qe; ++q) {  // one dependent LDS read per output; payloads after the loop
                 const bool ta = ka <= kb;
-                const int from = ta ? ps + i : pm + j;
                 ok[q] = ta ? ka : kb;
-                op[q] = ip[from];
+                op[q] = ta ? ps + i : pm + j;  // (the source position, for now)
                 i += ta;
                 j += !ta;
-                const int nx = ta ? (i < la ? ps + i : -1) : (j < lb ? pm + j : -1);
-                const u32 kn = nx >= 0 ? ik[nx] : ~0u;
-                ka = ta ? kn : ka;
-                kb = ta ? kb : kn;
+                const u32 kn = ik[ta ? ps + i : pm + j];  // (an exhausted side reads a neighbour: masked)
+                const bool live = ta ? i < la : j < lb;
+                ka = ta ? (live ? kn : ~0u) : ka;
+                kb = ta ? kb : (live ? kn : ~0u);
             }
         }
+#pragma unroll
+        for (int u = 0; u < IPM; ++u)  // the payloads: independent reads
+            if (u < nq) op[q0 + u] = ip[op[q0 + u]];
         __syncthreads();
         src ^= 1;
     }
@@ -603,44 +605,59 @@ __global__ __launch_bounds__(RH_NT) void k_rows_bitmap(RowsArgs g) {
     RP_DONE(0);
 }
 
-// every row's run from the staging area (at E[rpA[r]]) to its CSR place: a
-// wave per 4 consecutive rows -- 16 lanes per row while all four are short,
-// else the whole wave on each row in turn; the next group's row pointers and
-// staging offsets are loaded before this group's copy
-__global__ __launch_bounds__(WG) void k_rows_compact(int m, const long long *soff, const int *Crp, const int *Scol,
-                                                     const double *Sval, int *Ccol, double *Cval) {
-    const int lane = lane_id(), sub = lane >> 4, sl = lane & 15;
-    const int step = gridDim.x * WAVES * 4;
-    int rb = (blockIdx.x * WAVES + wave_id()) * 4;
-    int nd0 = 0, nd1 = 0;
-    long long ns0 = 0;
-    auto fetch = [&](int b) {
-        const int r = min(b + sub, m - 1);
-        nd0 = Crp[r];
-        nd1 = b + sub < m ? Crp[r + 1] : nd0;
-        ns0 = soff[r];
-    };
-    if (rb < m) fetch(rb);
-    for (; rb < m; rb += step) {
-        const int d0 = nd0, n = nd1 - nd0;
-        const long long s0 = ns0;
-        if (rb + step < m) fetch(rb + step);
-        const int mx = max(max(__shfl(n, 0, 64), __shfl(n, 16, 64)), max(__shfl(n, 32, 64), __shfl(n, 48, 64)));
-        if (mx <= 32) {
-            for (int i = sl; i < n; i += 16) {
-                Ccol[d0 + i] = Scol[s0 + i];
-                Cval[d0 + i] = Sval[s0 + i];
-            }
-        } else {
-            for (int q = 0; q < 4; ++q) {
-                const int dq = __shfl(d0, q * 16, 64), nq = __shfl(n, q * 16, 64);
-                const long long sq = __shfl(s0, q * 16, 64);
-                for (int i = lane; i < nq; i += 64) {
-                    Ccol[dq + i] = Scol[sq + i];
-                    Cval[dq + i] = Sval[sq + i];
-                }
-            }
-        }
+// every row's run from the staging area (at soff[r]) to its CSR place, by
+// chunks of CP_CH output positions (a workgroup each, consecutive lanes on
+// consecutive positions): the chunk's rows from cfirst (the row holding each
+// chunk's first position), each nonempty row marks its first position in LDS, a
+// running max gives every position its row.
+constexpr int CP_CH = 2048;
+
+__global__ __launch_bounds__(WG) void k_rows_cfirst(int m, const int *Crp, int *cfirst) {
+    for (int r = blockIdx.x * WG + threadIdx.x; r < m; r += gridDim.x * WG) {
+        const int s = Crp[r], e = Crp[r + 1];
+        for (long long b = ((long long)s + CP_CH - 1) / CP_CH; b * CP_CH < e; ++b) cfirst[b] = r;
+    }
+}
+
+__global__ __launch_bounds__(WG) void k_rows_compact(int m, int nnz, const int *cfirst, const long long *soff,
+                                                     const int *Crp, const int *Scol, const double *Sval, int *Ccol,
+                                                     double *Cval) {
+    __shared__ int rowof[CP_CH];
+    __shared__ int red[WAVES];
+    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    const int c0 = blockIdx.x * CP_CH, n = min(CP_CH, nnz - c0);
+    const int rf = cfirst[blockIdx.x];
+    const int rl = c0 + CP_CH < nnz ? cfirst[blockIdx.x + 1] : m - 1;
+    for (int i = tid; i < CP_CH; i += WG) rowof[i] = i == 0 ? rf : -1;
+    __syncthreads();
+    for (int r = rf + 1 + tid; r <= rl; r += WG) {
+        const int s = Crp[r];
+        if (s < c0 + n && Crp[r + 1] > s) rowof[s - c0] = r;
+    }
+    __syncthreads();
+    // running max over the chunk: 8 positions per thread, then the threads
+    constexpr int PT = CP_CH / WG;
+    int loc[PT], mx = -1;
+#pragma unroll
+    for (int u = 0; u < PT; ++u) {
+        mx = max(mx, rowof[tid * PT + u]);
+        loc[u] = mx;
+    }
+    int inc = wave_incl_max(mx);
+    if (lane == 63) red[wv] = inc;
+    __syncthreads();
+    int carry = __shfl_up(inc, 1, 64);
+    if (lane == 0) carry = -1;
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) carry = w < wv ? max(carry, red[w]) : carry;
+#pragma unroll
+    for (int u = 0; u < PT; ++u) rowof[tid * PT + u] = max(carry, loc[u]);
+    __syncthreads();
+    for (int i = tid; i < n; i += WG) {
+        const int r = rowof[i];
+        const long long src = soff[r] + (c0 + i - Crp[r]);
+        Ccol[c0 + i] = Scol[src];
+        Cval[c0 + i] = Sval[src];
     }
 }
 
@@ -687,9 +704,10 @@ int dev_spgemm_rows(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, tsg
     TSG_HIP(hipMemsetAsync(dprof, 0, sizeof(unsigned long long) * 3 * 256 * 8, s));
 #endif
     RowsArgs g{A.rowpointer, A.value, ebnd, E, B.columnindex, B.value, nullptr, 0, C.rowpointer, Scol, Sval};
-    // the classes are independent: each on a stream of its own, so that the short
-    // rows' workgroups fill the CUs around the long rows' (H first: longest)
-    TSG_TRY(cx.aux_fork(s));
+    // class H first, alone: its workgroups take a whole CU's LDS and would
+    // starve behind the short rows' workgroups; then the other classes, each on
+    // a stream of its own so that their tails overlap (4 streams: the hardware
+    // queues a process gets)
     auto launch = [&](int c, auto kern, int grid, int nt, hipStream_t st) -> int {
         if (ncls[c] == 0) return TSG_OK;
         g.list = lists + (long)c * m;
@@ -698,10 +716,11 @@ int dev_spgemm_rows(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, tsg
         TSG_HIP(hipGetLastError());
         return TSG_OK;
     };
-    TSG_TRY(launch(5, k_rows_bitmap, ncls[5], RH_NT, cx.aux[0]));
-    TSG_TRY(launch(4, k_rows_merge<M4_NT, M4_CAP, M4_RUNS>, ncls[4], M4_NT, cx.aux[1]));
-    TSG_TRY(launch(3, k_rows_merge<M3_NT, M3_CAP, M3_RUNS>, ncls[3], M3_NT, cx.aux[2]));
-    TSG_TRY(launch(2, k_rows_merge<M2_NT, M2_CAP, M2_RUNS>, ncls[2], M2_NT, cx.aux[3]));
+    TSG_TRY(launch(5, k_rows_bitmap, ncls[5], RH_NT, s));
+    TSG_TRY(cx.aux_fork(s));
+    TSG_TRY(launch(4, k_rows_merge<M4_NT, M4_CAP, M4_RUNS>, ncls[4], M4_NT, cx.aux[0]));
+    TSG_TRY(launch(3, k_rows_merge<M3_NT, M3_CAP, M3_RUNS>, ncls[3], M3_NT, cx.aux[1]));
+    TSG_TRY(launch(2, k_rows_merge<M2_NT, M2_CAP, M2_RUNS>, ncls[2], M2_NT, cx.aux[2]));
     TSG_TRY(launch(1, k_rows_merge<M1_NT, M1_CAP, M1_RUNS>, ncls[1], M1_NT, s));
     TSG_TRY(launch(0, k_rows_small, (ncls[0] + WAVES - 1) / WAVES, WG, s));
     TSG_TRY(cx.aux_join(s));
@@ -731,9 +750,16 @@ int dev_spgemm_rows(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, tsg
     C.nnz = (int)nnz;
     TSG_TRY(cx.get(&C.columnindex, (size_t)nnz + 1));
     TSG_TRY(cx.get(&C.value, (size_t)nnz + 1));
-    if (m > 0)
-        k_rows_compact<<<grid_for(m, 4 * WAVES, 16384), WG, 0, s>>>(m, soff, C.rowpointer, Scol, Sval,
-                                                               C.columnindex, C.value);
+    if (nnz > 0) {
+        const int nch = (int)((nnz + CP_CH - 1) / CP_CH);
+        int *cfirst = nullptr;
+        TSG_TRY(cx.get(&cfirst, (size_t)nch + 1));
+        k_rows_cfirst<<<grid_for(m, WG, 8192), WG, 0, s>>>(m, C.rowpointer, cfirst);
+        TSG_HIP(hipGetLastError());
+        k_rows_compact<<<nch, WG, 0, s>>>(m, (int)nnz, cfirst, soff, C.rowpointer, Scol, Sval, C.columnindex,
+                                          C.value);
+        cx.put(cfirst);
+    }
     TSG_HIP(hipGetLastError());
     if (ev) TSG_HIP(hipEventRecord(ev[3], s));
     TSG_HIP(hipStreamSynchronize(s));
