@@ -49,7 +49,7 @@ class Stats(C.Structure):
         "t_csr2tile_ms", "t_step1_ms", "t_step2_ms", "t_step3_ms", "t_tile2csr_ms",
         "t_malloc_ms", "t_kern_ms", "t_e2e_ms")] + [(n, C.c_longlong) for n in (
             "nnzCub", "numtileA", "numtileB", "numblkC", "nnzC", "tile_products")] + [
-            ("t_step3_kernel_ms", C.c_double)]
+            ("t_step3_kernel_ms", C.c_double), ("path", C.c_longlong)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -868,7 +868,12 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
     // (FEM-like operands with dense rows, e.g. cant), one walk accumulates the
     // row in a dense LDS window.  Checked only for rows of >= 8 entries on
     // average (a statistics kernel + one host round trip).
-    // TSG_PATH=fused / band / tiles forces a path (band when its check passes).
+    // Row-merge path (tsg_rows.hip): the remaining sorted-B products, unless its
+    // binning finds them hub-dominated (class-H rows over a quarter of the work,
+    // or a row over kRowsMaxRowProducts products: R-MAT, mawi), which then take
+    // the staged tile pipeline (web graphs: webbase 1.95 vs 2.75 ms).
+    // TSG_PATH=fused / band / rows / tiles forces a path (band when its check
+    // passes).
     const char *path = getenv("TSG_PATH");
     const bool force_fused = path && !strcmp(path, "fused"), force_tiles = path && !strcmp(path, "tiles");
     const bool force_band = path && !strcmp(path, "band"), force_rows = path && !strcmp(path, "rows");
@@ -883,22 +888,27 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
         if (bsorted0 && !force_fused && !force_rows &&
             (force_band || (!short_rows && A->m > 0 && A->nnz >= 8LL * A->m)))
             TSG_TRY(dev_band_check(cx, *A, *B, force_band, &band, &bw, s));
-        const bool rows = bsorted0 && force_rows;
+        bool rows = false;
+        if (!band) TSG_HIP(hipEventRecord(cx.ev[9], s));
+        if (!band && bsorted0 && !force_fused && !force_band && (force_rows || !short_rows)) {
+            bool declined = false;
+            TSG_TRY(dev_spgemm_rows(cx, *A, *B, *C, &st, s, cx.ev, force_rows, &declined));
+            rows = !declined;
+        }
         if (band || rows) {
-            TSG_HIP(hipEventRecord(cx.ev[9], s));
             if (band) {
+                TSG_HIP(hipEventRecord(cx.ev[9], s));
                 const int rc = dev_spgemm_band(cx, *A, *B, bw, *C, &st, s, cx.ev);
                 cx.put(bw.win);
                 cx.put(bw.width);
                 TSG_TRY(rc);
-            } else {
-                TSG_TRY(dev_spgemm_rows(cx, *A, *B, *C, &st, s, cx.ev));
             }
             TSG_HIP(hipEventRecord(cx.ev[10], s));
             TSG_HIP(hipEventSynchronize(cx.ev[10]));
             auto h1 = std::chrono::steady_clock::now();
             st.numtileA = -1;
             st.numtileB = -1;
+            st.path = band ? TSG_PATH_BAND : TSG_PATH_ROWS;
             st.t_csr2tile_ms = ev_ms(cx.ev[8], cx.ev[9]);   // sortedness (+ band: window statistics; no csr2tile)
             st.t_step1_ms = ev_ms(cx.ev[0], cx.ev[1]);      // entry ranges, staging offsets (+ rows: classes)
             st.t_step2_ms = 0.0;                            // (one walk: structure and values together)
@@ -920,6 +930,7 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
             auto h1 = std::chrono::steady_clock::now();
             st.numtileA = -1;
             st.numtileB = -1;
+            st.path = TSG_PATH_FUSED;
             st.t_csr2tile_ms = ev_ms(cx.ev[8], cx.ev[9]);   // B sortedness check (no csr2tile on this path)
             st.t_step1_ms = ev_ms(cx.ev[0], cx.ev[1]);      // entry ranges, row classes, heavy-row windows, units
             st.t_step2_ms = 0.0;                            // (fused into the unit kernel)

@@ -147,8 +147,12 @@ int dev_spgemm_band(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, Ban
 // rows binned by element products, each row's B rows merged (or, for the
 // longest rows, marked in an LDS column bitmap).
 // ev (optional): 0 start | 1 set up | 4..5 the row kernels | 3 end
+// Unless force, it declines (*declined, nothing computed) products whose class-H
+// rows (> 4,096 products or > 512 runs) hold over a quarter of the work or with
+// a row over kRowsMaxRowProducts products.
+constexpr long long kRowsMaxRowProducts = 65536;
 int dev_spgemm_rows(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, tsg_dev_csr &C, tsg_stats *st,
-                    hipStream_t s, hipEvent_t *ev);
+                    hipStream_t s, hipEvent_t *ev, bool force, bool *declined);
 // exclusive scan (n+1 idiom) whose total is read back
 int scan_exclusive_i32_total(Context &cx, int *a, long n, hipStream_t s, long long *total);
 

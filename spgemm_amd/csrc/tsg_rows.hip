@@ -126,20 +126,37 @@ __device__ __forceinline__ int row_class(const int *rpA, const long long *E, int
 }
 
 // rows -> classes: lists (class c's rows from lists + c*m) and counts cls[0..NCLS);
-// rows without products get nnz 0.  A workgroup per BIN_ROWS rows: its counts
-// first (one atomic per class), then its rows in order into the reserved slots.
+// rows without products get nnz 0; hst[0] = the class-H rows' products, hst[1]
+// = the largest row's products (the routing statistics).  A workgroup per
+// BIN_ROWS rows: its counts first (one atomic per class), then its rows in
+// order into the reserved slots.
 __global__ __launch_bounds__(WG) void k_rows_bin(const int *rpA, int m, const long long *E, int *rnnz, int *lists,
-                                                 int *cls, long long *soff) {
+                                                 int *cls, long long *soff, unsigned long long *hst) {
     __shared__ int wc[NCLS][WAVES];
     __shared__ int gb[NCLS];
+    __shared__ long long red64[WAVES];
     const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
     const int r0 = blockIdx.x * BIN_ROWS, r1 = min(m, r0 + BIN_ROWS);
     int n[NCLS] = {};
+    long long hp = 0, pmax = 0;
     for (int r = r0 + tid; r < r1; r += WG) {
         const int c = row_class(rpA, E, r, soff);  // (+ the row's staging offset)
         if (c < 0) rnnz[r] = 0;
 #pragma unroll
         for (int t = 0; t < NCLS; ++t) n[t] += c == t;
+        const long long P = E[rpA[r + 1]] - soff[r];
+        hp += c == NCLS - 1 ? P : 0;
+        pmax = max(pmax, P);
+    }
+    hp = block_sum(hp, red64);
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) pmax = max(pmax, __shfl_xor(pmax, d, 64));
+    if (lane == 0) red64[wv] = pmax;
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < WAVES; ++w) pmax = max(pmax, red64[w]);
+        if (hp) atomicAdd(&hst[0], (unsigned long long)hp);
+        if (pmax) atomicMax(&hst[1], (unsigned long long)pmax);
     }
 #pragma unroll
     for (int t = 0; t < NCLS; ++t) {
@@ -664,7 +681,8 @@ __global__ __launch_bounds__(WG) void k_rows_compact(int m, int nnz, const int *
 // CSR in -> CSR out (B's rows column-sorted; the caller checked).
 // ev (optional): 0 start | 1 set up | 4..5 the row kernels | 3 end
 int dev_spgemm_rows(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, tsg_dev_csr &C, tsg_stats *st,
-                    hipStream_t s, hipEvent_t *ev) {
+                    hipStream_t s, hipEvent_t *ev, bool force, bool *declined) {
+    *declined = false;
     const int m = A.m;
     C = tsg_dev_csr{};
     C.m = m;
@@ -678,20 +696,35 @@ int dev_spgemm_rows(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, tsg
     TSG_TRY(cx.get(&lists, (size_t)NCLS * (m > 0 ? m : 1)));
     long long *soff = nullptr;
     TSG_TRY(cx.get(&soff, (size_t)m + 1));
-    TSG_TRY(cx.get(&cls, 8));
+    TSG_TRY(cx.get(&cls, 12));  // 6 class counts, then 2 u64 statistics
+    unsigned long long *hst = reinterpret_cast<unsigned long long *>(cls + 8);
     TSG_TRY(cx.get(&C.rowpointer, (size_t)m + 1));
-    TSG_HIP(hipMemsetAsync(cls, 0, 8 * sizeof(int), s));
+    TSG_HIP(hipMemsetAsync(cls, 0, 12 * sizeof(int), s));
     k_rows_entries<<<grid_for((long)A.nnz + 1, WG, 16384), WG, 0, s>>>(A.columnindex, A.nnz, B.rowpointer, ebnd, E);
     TSG_HIP(hipGetLastError());
     TSG_TRY(scan_exclusive_i64(cx, E, (long)A.nnz + 1, s));
-    if (m > 0) k_rows_bin<<<(m + BIN_ROWS - 1) / BIN_ROWS, WG, 0, s>>>(A.rowpointer, m, E, C.rowpointer, lists, cls, soff);
+    if (m > 0) k_rows_bin<<<(m + BIN_ROWS - 1) / BIN_ROWS, WG, 0, s>>>(A.rowpointer, m, E, C.rowpointer, lists, cls, soff, hst);
     TSG_HIP(hipGetLastError());
     TSG_HIP(hipMemcpyAsync(cx.pinned64, E + A.nnz, sizeof(long long), hipMemcpyDeviceToHost, s));
-    TSG_HIP(hipMemcpyAsync(cx.pinned64 + 1, cls, NCLS * sizeof(int), hipMemcpyDeviceToHost, s));
+    TSG_HIP(hipMemcpyAsync(cx.pinned64 + 1, cls, 12 * sizeof(int), hipMemcpyDeviceToHost, s));
     TSG_HIP(hipStreamSynchronize(s));
     const long long products = cx.pinned64[0];
     int ncls[NCLS];
     for (int t = 0; t < NCLS; ++t) ncls[t] = reinterpret_cast<const int *>(cx.pinned64 + 1)[t];
+    const long long hprod = cx.pinned64[5], pmax = cx.pinned64[6];
+    // routing: the path is built for rows of modest length (class H a minority
+    // of the work); hub-dominated products (R-MAT, mawi) go back to the caller
+    if (!force && (hprod * 4 > products || pmax > kRowsMaxRowProducts)) {
+        *declined = true;
+        cx.put(ebnd);
+        cx.put(E);
+        cx.put(lists);
+        cx.put(soff);
+        cx.put(cls);
+        cx.put(C.rowpointer);
+        C = tsg_dev_csr{};
+        return TSG_OK;
+    }
     int *Scol = nullptr;
     double *Sval = nullptr;
     TSG_TRY(cx.get(&Scol, (size_t)products + 1));

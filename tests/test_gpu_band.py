@@ -87,22 +87,22 @@ def test_band_forced_vs_oracle(case, band):
         m, n, rp, ci, vv = _sorted_rows(*synth.random_csr(600, 600, density=0.2, seed=22))
     st = _check(m, n, rp, ci, vv)
     if case in ("narrow", "empty_rows", "dense_block"):
-        assert st["numtileA"] == -1 and st["numblkC"] == -1  # the banded path ran
+        assert st["path"] == T.PATH_BAND and st["numblkC"] == -1  # the banded path ran
 
 
 def test_band_aat_and_real_values(band):
     m, n, rp, ci, _ = _banded(2500, 12, 5)
     vv = np.random.default_rng(6).uniform(-1, 1, len(ci))
     st = _check(m, n, rp, ci, vv, aat=True, real=True)
-    assert st["numblkC"] == -1
+    assert st["path"] == T.PATH_BAND
 
 
 def test_cant_routes_to_band_and_matches_oracle():
     """The cant stand-in (banded FEM-like, ~64 entries per row) takes the banded
-    path by default; webbase-like rows keep the staged pipeline."""
+    path by default; rows spread over all columns take the row-merge path."""
     m, n, rp, ci, vv = synth.GENERATORS["cant"]()
     st = _check(m, n, rp, ci, vv)
-    assert st["numblkC"] == -1 and st["numtileA"] == -1
-    m, n, rp, ci, vv = synth.random_csr(3000, 3000, density=0.02, seed=4)  # spread rows
+    assert st["path"] == T.PATH_BAND and st["numblkC"] == -1
+    m, n, rp, ci, vv = synth.random_csr(3000, 3000, density=0.01, seed=4)  # spread rows
     st = _check(m, n, rp, ci, vv)
-    assert st["numtileA"] > 0
+    assert st["path"] == T.PATH_ROWS

@@ -109,10 +109,10 @@ def test_fused_real_values(fused):
 
 def test_default_routing_short_rows_fused():
     """mc2depi A*A^T (rows of <= 4 entries on both sides) takes the fused path by
-    default; webbase-like long rows take the staged tile pipeline."""
+    default; long rows spread over the columns take the row-merge path."""
     m, n, rp, ci, vv = synth.mc2depi()
     st = _check(m, n, rp, ci, vv, aat=True)
-    assert st["numtileA"] == -1
-    m, n, rp, ci, vv = synth.random_csr(3000, 3000, density=0.02, seed=4)  # ~60-entry rows
+    assert st["path"] == T.PATH_FUSED
+    m, n, rp, ci, vv = synth.random_csr(3000, 3000, density=0.01, seed=4)  # ~30-entry rows
     st = _check(m, n, rp, ci, vv)
-    assert st["numtileA"] > 0
+    assert st["path"] == T.PATH_ROWS

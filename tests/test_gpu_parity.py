@@ -191,11 +191,13 @@ def test_full_size_synthetic_vs_oracle(name, path, monkeypatch):
     assert_csr_equal(Cm.csr(), ref.csr())
     assert st["nnzC"] == ref.s.nnz
     # the staged pipeline's A/B tile counts (wave hash sets + bitmap fallback for
-    # tile rows over 256 entries) equal the oracle csr2tile's numtile (the fused
-    # and banded paths build no A/B tiles and report -1)
-    if st["numtileA"] < 0:
-        assert path is None and name in ("mc2depi", "cant")
+    # tile rows over 256 entries) equal the oracle csr2tile's numtile (the fused,
+    # banded and row-merge paths build no A/B tiles and report -1)
+    if path is None:  # the default routes
+        assert st["path"] == {"cant": T.PATH_BAND, "mc2depi": T.PATH_FUSED, "webbase": T.PATH_ROWS}[name]
+        assert st["numtileA"] == -1
         return
+    assert st["path"] == T.PATH_TILES
     tA = O.OMat.from_csr(m, n, rp, ci, vv)
     O.csr2tile_row_major(tA, 16, 16)
     assert st["numtileA"] == tA.s.numtile

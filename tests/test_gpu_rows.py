@@ -57,7 +57,7 @@ def _check(A_, B_=None, aat=False, real=False, seed=0):
     else:
         np.testing.assert_allclose(got[4], ref[4], rtol=1e-10, atol=0)
     assert st["nnzC"] == len(ref[3])
-    assert st["numblkC"] == -1 and st["numtileA"] == -1  # the row-merge path ran
+    assert st["path"] == T.PATH_ROWS and st["numblkC"] == -1 and st["numtileA"] == -1
     return st
 
 

@@ -54,15 +54,16 @@ print("child ok")
 def test_second_element_walk_and_multiwindow():
     """TSG_ABLATE=768: no unit buffers (512) and no stored bitmasks (256), so
     step 1 emits by a second element walk; one case has 2 column windows."""
-    env = dict(os.environ, TSG_ABLATE="768")
+    env = dict(os.environ, TSG_ABLATE="768", TSG_PATH="tiles")
     code = _CHILD.format(repo=REPO, tests=os.path.join(REPO, "tests"))
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "child ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
 
 
-def test_b_too_wide_for_tile_counts():
+def test_b_too_wide_for_tile_counts(monkeypatch):
     """B with n = 2e8 (12.5 M tile rows x 191 windows > 2^31 count units):
     the element path runs on B's CSR; numtileB is reported as -1."""
+    monkeypatch.setenv("TSG_PATH", "tiles")
     n = 200_000_000
     rng = np.random.default_rng(5)
     # A: 40 rows over the first 2,000 columns; B: rows < 2,000 hold 3 columns
@@ -80,7 +81,7 @@ def test_b_too_wide_for_tile_counts():
     cib = np.concatenate(rows_b).astype(np.int32)
     vvb = (np.arange(len(cib)) % 10 + 1).astype(np.float64)
     st = _check(m, n, rp, ci, vv, n, n, rpb, cib, vvb)
-    assert st["numtileB"] == -1
+    assert st["path"] == T.PATH_TILES and st["numtileB"] == -1
 
 
 @pytest.mark.parametrize("nb", [300_000, 1_200_000])
