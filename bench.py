@@ -168,10 +168,11 @@ def tiled_leg(m, n, rp, ci, vv, mb, nb, rpb, cib, vvb, aat, tm, nnzcub, reps=3):
             "path": "tsg_tilespgemm (reference tiled layout in/out; the ./test CLI path)"}
 
 
-def pmc_traffic(kernel, workload):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary of
-    the same workload (profiles/<round>_pmc.json, written by tools/profile.sh:
-    2*FETCH_SIZE + WRITE_SIZE, separate --pmc passes).  (None, None) when absent."""
+def pmc_traffic(kernels, workload):
+    """HBM bytes per call of the `kernels` (name substrings; their per-dispatch
+    bytes summed) from the newest committed PMC summary of the same workload
+    (profiles/<round>_pmc.json, written by tools/profile.sh: 2*FETCH_SIZE +
+    WRITE_SIZE, separate --pmc passes).  (None, None) when absent."""
     import glob
     def workload_of(f):
         try:
@@ -183,11 +184,13 @@ def pmc_traffic(kernel, workload):
     if not files:
         return None, None
     d = json.load(open(files[-1]))
-    hits = [v for k, v in d.items() if kernel in k and isinstance(v, dict) and v.get("hbm_bytes_per_dispatch")]
-    if not hits:
-        return None, None
-    best = max(hits, key=lambda v: v["dispatches"] or 0)
-    return int(best["hbm_bytes_per_dispatch"]), os.path.relpath(files[-1], REPO)
+    tot = 0
+    for kernel in kernels:
+        hits = [v for k, v in d.items() if kernel in k and isinstance(v, dict) and v.get("hbm_bytes_per_dispatch")]
+        if not hits:
+            return None, None
+        tot += sum(int(v["hbm_bytes_per_dispatch"]) for v in hits)
+    return tot, os.path.relpath(files[-1], REPO)
 
 
 def main():
@@ -354,14 +357,22 @@ def main():
     # context only (never the graded figure): + one fp64 value and one u16 local column
     # per intermediate product of this rank (SURVEY §8d B_stream)
     b_stream = b_alg + 10.0 * float(cum[r_hi] - cum[r_lo])
-    # dominant kernel: the step-3 numeric kernel (reads the CSR operands, writes the
-    # CSR result = B_alg's terms), timed with HIP events around its launch on the
-    # call's stream
+    # dominant kernel (reads the CSR operands, builds the C rows = B_alg's terms),
+    # timed with HIP events on the call's stream: the staged pipeline's step-3
+    # numeric kernel, or the row-merge path's numeric phase (its class kernels
+    # S, M1-M4, H on 4 streams, forked from and joined to the call's stream)
     k3_ms = med["t_step3_kernel_ms"]
     achieved = b_alg / (k3_ms * 1e-3) / 1e9
-    workload = (f"{name} C=A{'*A^T' if aat else '^2'} fp64, {tm}x{tm} tiles, "
-                "csr2tile+steps1-3+tile2csr (device CSR in -> device CSR out)")
-    traffic, traffic_src = pmc_traffic("k_step3", workload)
+    path_id = int(med["path"])
+    path_name = {0: "tiles", 1: "fused", 2: "band", 3: "rows"}.get(path_id, str(path_id))
+    workload = f"{name} C=A{'*A^T' if aat else '^2'} fp64 (device CSR in -> device CSR out), path {path_name}"
+    if path_id == 3:
+        kernel_desc = ("row-merge numeric phase (k_rows_small, k_rows_merge x4 classes, k_rows_bitmap on 4 streams): "
+                       "B_alg of SURVEY §8d / HIP-event phase time")
+        traffic, traffic_src = pmc_traffic(["k_rows_small", "k_rows_merge", "k_rows_bitmap"], workload)
+    else:
+        kernel_desc = "step-3 numeric kernel (fused tile2csr): B_alg of SURVEY §8d / HIP-event kernel time"
+        traffic, traffic_src = pmc_traffic(["k_step3"], workload)
     chk = None
     if args.check and not gather:
         # checksum of this rank's C (every block), recomputed outside the timed region;
@@ -424,16 +435,18 @@ def main():
             "config": {"workload": workload,
                        "m": m * world if weak else m, "m_per_rank": m if weak else None,
                        "nnzA": int(len(ci)) * (world if weak else 1), "nnzCub": nnzcub_total, "nnzC": nnzC,
+                       "path": path_name,
                        "numtileA": int(med["numtileA"]),
                        "numblkC": int(med["numblkC"]),
-                       "numblkC_kind": "element-level C tiles (non-empty 16x16 tiles of C; the reference's "
-                                       "tile-pattern step 1 also lists empty ones, see t_kern_tiled)",
+                       "numblkC_kind": ("element-level C tiles (non-empty 16x16 tiles of C; the reference's "
+                                        "tile-pattern step 1 also lists empty ones, see t_kern_tiled)") if path_id == 0
+                                       else "-1: this path builds no C tiles (the reference-layout tiled C: see tiled)",
                        "row_blocks": len(blocks),
                        "parallelism": par},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "kernel": "step-3 numeric kernel (fused tile2csr): B_alg of SURVEY §8d / HIP-event kernel time",
+                         "kernel": kernel_desc,
                          "algorithmic_bytes": int(b_alg), "kernel_ms": round(k3_ms, 4),
                          "pipeline": {"achieved": round(achieved_pipe, 2),
                                       "frac": round(achieved_pipe / HBM_PEAK_GBS, 5),

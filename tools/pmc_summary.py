@@ -55,6 +55,28 @@ def main():
     if trace:
         for r in csv.DictReader(open(trace[0])):
             dur[short(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    # row-merge path: its class kernels run concurrently (4 streams); the unit the
+    # bench times is the phase from the first class kernel's start to the last's
+    # end in each call (a call = one k_rows_bin)
+    spans, cur = [], None
+    if trace:
+        rows = sorted(csv.DictReader(open(trace[0])), key=lambda r: int(r["Start_Timestamp"]))
+        for r in rows:
+            k = short(r["Kernel_Name"])
+            if k.endswith("k_rows_bin"):
+                if cur:
+                    spans.append(cur[1] - cur[0])
+                cur = None
+            elif any(k.endswith(c) or c + "<" in k for c in ("k_rows_small", "k_rows_merge", "k_rows_bitmap")):
+                s0, e0 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+                cur = [min(cur[0], s0), max(cur[1], e0)] if cur else [s0, e0]
+        if cur:
+            spans.append(cur[1] - cur[0])
+    if spans:
+        warm = sorted(spans[1:] or spans)  # (the first call also loads the kernels' code objects)
+        out["_rows_phase"] = {"calls": len(spans), "median_span_us": round(warm[len(warm) // 2] / 1e3, 2),
+                              "note": "first class-kernel start to last class-kernel end per call (trace), "
+                                      "median over the calls after the first"}
     fetch = counters(os.path.join(src, "pmc_fetch"), "FETCH_SIZE")
     write = counters(os.path.join(src, "pmc_write"), "WRITE_SIZE")
     for k in sorted(set(dur) | set(fetch) | set(write)):
