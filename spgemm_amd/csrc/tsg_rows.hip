@@ -279,44 +279,79 @@ __device__ __forceinline__ void search_ilp(const T *a, int (&b)[U], int (&len)[U
 }
 
 // ---- classes M1..M4: pairwise stable merges of the row's runs in LDS.  NT
-// threads per row, at most CAP products and RUNS runs.  Keys are the columns
-// (u32) with a (run, position) payload.  Thread t owns the positions
-// [t*ipt, t*ipt + ipt) of every pass (ipt odd, so the lanes' LDS accesses
-// spread over the banks): its global loads are issued together (IPM = the
-// largest ipt, unrolled), and each merge round is a merge path -- one co-rank
-// search per pair the chunk touches, then a sequential merge with ties taken
-// from the left group first, so equal columns stay in run order and every sum
-// is taken in one fixed order.
+// threads per row, at most CAP products and RUNS runs.  Thread t owns the
+// positions [t*ipt, t*ipt + ipt) of every pass (ipt odd, so the lanes' LDS
+// accesses spread over the banks): its global loads are issued together (IPM =
+// the largest ipt, unrolled), and each merge round is a merge path -- one
+// co-rank search per pair the chunk touches, then a sequential merge.
+//
+// Keys: when the row's column span fits, one u32 per element packs
+// (column - lo, expansion position) -- unique, so the merged order is one fixed
+// order and nothing else moves; the (run, position-in-run) payloads stay in
+// expansion order.  Wider rows sort u32 columns with a moved payload and take
+// ties from the left group first (equal columns stay in run order).  Either
+// way every sum is taken in one fixed order.
 template <int NT, int CAP, int RUNS>
 __global__ __launch_bounds__(NT) void k_rows_merge(RowsArgs g) {
     constexpr int NW = NT / 64;
     constexpr int IPM = (CAP + NT - 1) / NT | 1;
-    __shared__ u32 kp[2][2][CAP];   // [buffer][keys | payloads]
+    constexpr int IB = CAP == 512 ? 9 : CAP == 1024 ? 10 : CAP == 2048 ? 11 : 12;  // position bits
+    static_assert((1 << IB) == CAP, "CAP: a power of two in [512, 4096]");
+    // kp[0][0] K0 | kp[0][1] X | kp[1][0] K1 | kp[1][1] PY.  Packed: keys ping-pong
+    // K0 <-> K1, PY holds the payloads, and the values go to K0+X or X+K1 (the
+    // free pair next to the final keys).  Unpacked: [buffer][keys | payloads].
+    __shared__ u32 kp[2][2][CAP];
     __shared__ int roff[RUNS + 1];
     __shared__ int rbs[RUNS];       // each run's B start
     __shared__ double rav[RUNS];    // each run's A value
-    __shared__ int red[NW];
+    __shared__ int red[2 * NW];
     RP_INIT
     const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
     const int r = g.list[blockIdx.x];
-    const int a0 = g.rpA[r], k = g.rpA[r + 1] - a0;
+    const int a0 = g.rpA[r], ka = g.rpA[r + 1] - a0;
     const long long base = g.E[a0];
-    const int P = (int)(g.E[a0 + k] - base);
-    for (int j = tid; j <= k; j += NT) {
-        roff[j] = (int)(g.E[a0 + j] - base);
-        if (j < k) {
-            rbs[j] = g.ebnd[a0 + j].x;
-            rav[j] = g.vA[a0 + j];
+    const int P = (int)(g.E[a0 + ka] - base);
+    // the runs with products, in order (entries selecting empty B rows dropped:
+    // fewer runs, fewer rounds)
+    int k = 0;
+    for (int jb = 0; jb < ka; jb += NT) {  // (workgroup-uniform)
+        const int j = jb + tid;
+        long long e0 = 0;
+        int len = 0;
+        if (j < ka) {
+            e0 = g.E[a0 + j];
+            len = (int)(g.E[a0 + j + 1] - e0);
         }
+        const u64 b = __ballot(len > 0);
+        if (lane == 0) red[wv] = __popcll(b);
+        __syncthreads();
+        int off = k, tot = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            off += w < wv ? red[w] : 0;
+            tot += red[w];
+        }
+        if (len > 0) {
+            const int d = off + lanes_below(b);
+            roff[d] = (int)(e0 - base);
+            rbs[d] = g.ebnd[a0 + j].x;
+            rav[d] = g.vA[a0 + j];
+        }
+        k += tot;
+        __syncthreads();
     }
+    if (tid == 0) roff[k] = P;
     __syncthreads();
     RP(0);
     const int ipt = ((P + NT - 1) / NT) | 1;
     const int q0 = min(P, tid * ipt), q1 = min(P, q0 + ipt), nq = q1 - q0;
-    // expansion: position q of run j at roff[j] + t -> key Bcol, payload (j, t)
+    // expansion: position q of run j at roff[j] + t -> column, payload (j, t)
+    int j0 = 0;  // the run holding q0 (pairs keep their position ranges every round)
+    int c[IPM];
+    u32 py[IPM];
     {
         int j = 0;
-        if (nq > 0) {  // the run holding q0: the last run starting at or before it
+        if (nq > 0) {  // the last run starting at or before q0
             int lo = 0, len = k;
             while (len > 0) {
                 const int half = len >> 1;
@@ -328,9 +363,9 @@ __global__ __launch_bounds__(NT) void k_rows_merge(RowsArgs g) {
                 }
             }
             j = lo - 1;
+            j0 = j;
         }
         int pa[IPM];
-        u32 py[IPM];
 #pragma unroll
         for (int u = 0; u < IPM; ++u)
             if (u < nq) {
@@ -339,17 +374,46 @@ __global__ __launch_bounds__(NT) void k_rows_merge(RowsArgs g) {
                 pa[u] = rbs[j] + q - roff[j];
                 py[u] = ((u32)j << 16) | (u32)(q - roff[j]);
             }
-        int c[IPM];
 #pragma unroll
         for (int u = 0; u < IPM; ++u)
             if (u < nq) c[u] = g.Bcol[pa[u]];
-#pragma unroll
-        for (int u = 0; u < IPM; ++u)
-            if (u < nq) {
-                kp[0][0][q0 + u] = (u32)c[u];
-                kp[0][1][q0 + u] = py[u];
-            }
     }
+    // the row's column span [clo, chi]
+    int clo = INT_MAX, chi = -1;
+#pragma unroll
+    for (int u = 0; u < IPM; ++u)
+        if (u < nq) {
+            clo = min(clo, c[u]);
+            chi = max(chi, c[u]);
+        }
+    clo = wave_last(wave_incl_dpp(clo, INT_MAX, OpMin{}));
+    chi = wave_last(wave_incl_dpp(chi, INT_MIN, OpMax{}));
+    if (lane == 0) {
+        red[wv] = clo;
+        red[NW + wv] = chi;
+    }
+    __syncthreads();
+    clo = red[0];
+    chi = red[NW];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {
+        clo = min(clo, red[w]);
+        chi = max(chi, red[NW + w]);
+    }
+    const bool packed = (u32)(chi - clo) < (1u << (32 - IB));  // (workgroup-uniform)
+    u32 *const K0 = kp[0][0], *const X = kp[0][1], *const PY = kp[1][1];
+#pragma unroll
+    for (int u = 0; u < IPM; ++u)
+        if (u < nq) {
+            const int q = q0 + u;
+            if (packed) {
+                K0[q] = ((u32)(c[u] - clo) << IB) | (u32)q;
+                PY[q] = py[u];
+            } else {
+                K0[q] = (u32)c[u];
+                X[q] = py[u];
+            }
+        }
     __syncthreads();
     RP(1);
     // rounds: groups of 2^lw runs merged pairwise
@@ -357,8 +421,9 @@ __global__ __launch_bounds__(NT) void k_rows_merge(RowsArgs g) {
     for (int lw = 0; (1 << lw) < k; ++lw) {
         const u32 *ik = kp[src][0], *ip = kp[src][1];
         u32 *ok = kp[src ^ 1][0], *op = kp[src ^ 1][1];
+        int pr = j0 >> (lw + 1);  // the pair holding q0
         for (int q = q0; q < q1;) {
-            const int pr = (int)(ip[q] >> 16) >> (lw + 1);  // input position q lies in the pair it outputs to
+            while (roff[min((pr + 1) << (lw + 1), k)] <= q) ++pr;  // (pairs ending at or before q)
             const int ps = roff[pr << (lw + 1)];
             const int pm = roff[min((2 * pr + 1) << lw, k)];
             const int pe = roff[min((pr + 1) << (lw + 1), k)];
@@ -369,12 +434,12 @@ __global__ __launch_bounds__(NT) void k_rows_merge(RowsArgs g) {
                 if (ik[ps + i] <= ik[pm + qq - i - 1]) lo = i + 1; else hi = i;
             }
             int i = lo, j = qq - lo;
-            u32 ka = i < la ? ik[ps + i] : ~0u, kb = j < lb ? ik[pm + j] : ~0u;  // (columns < 2^31)
+            u32 ka = i < la ? ik[ps + i] : ~0u, kb = j < lb ? ik[pm + j] : ~0u;  // (keys < 2^32 - 1)
             const int qe = min(q1, pe);
-            for (; q < qe; ++q) {  // one dependent LDS read per output; payloads after the loop
+            for (; q < qe; ++q) {  // one dependent LDS read per output
                 const bool ta = ka <= kb;
                 ok[q] = ta ? ka : kb;
-                op[q] = ta ? ps + i : pm + j;  // (the source position, for now)
+                if (!packed) op[q] = ta ? ps + i : pm + j;  // (the source position, for now)
                 i += ta;
                 j += !ta;
                 const u32 kn = ik[ta ? ps + i : pm + j];  // (an exhausted side reads a neighbour: masked)
@@ -383,15 +448,20 @@ __global__ __launch_bounds__(NT) void k_rows_merge(RowsArgs g) {
                 kb = ta ? kb : (live ? kn : ~0u);
             }
         }
+        if (!packed) {
 #pragma unroll
-        for (int u = 0; u < IPM; ++u)  // the payloads: independent reads
-            if (u < nq) op[q0 + u] = ip[op[q0 + u]];
+            for (int u = 0; u < IPM; ++u)  // the payloads: independent reads
+                if (u < nq) op[q0 + u] = ip[op[q0 + u]];
+        }
         __syncthreads();
         src ^= 1;
     }
     RP(2);
     const u32 *sk = kp[src][0], *sp = kp[src][1];
-    double *vb = reinterpret_cast<double *>(&kp[src ^ 1][0][0]);  // the free buffer: each position's product
+    // each position's product: packed -> into the free pair next to the final
+    // keys; unpacked -> into the free buffer
+    double *vb = reinterpret_cast<double *>(packed ? (src ? K0 : X) : kp[src ^ 1][0]);
+    const u32 cs = packed ? IB : 0;  // key >> cs = the column (- clo when packed)
     int nh = 0;  // heads (first position of each column) in the chunk
     {
         int pa[IPM];
@@ -399,11 +469,12 @@ __global__ __launch_bounds__(NT) void k_rows_merge(RowsArgs g) {
 #pragma unroll
         for (int u = 0; u < IPM; ++u)
             if (u < nq) {
-                const u32 pj = sp[q0 + u];
+                const u32 key = sk[q0 + u];
+                const u32 pj = packed ? PY[key & (CAP - 1)] : sp[q0 + u];
                 const int ru = (int)(pj >> 16);
                 pa[u] = rbs[ru] + (int)(pj & 0xffffu);
                 av[u] = rav[ru];
-                nh += (q0 + u == 0 || sk[q0 + u] != sk[q0 + u - 1]);
+                nh += (q0 + u == 0 || (key >> cs) != (sk[q0 + u - 1] >> cs));
             }
         double x[IPM];
 #pragma unroll
@@ -425,12 +496,13 @@ __global__ __launch_bounds__(NT) void k_rows_merge(RowsArgs g) {
         tot += red[w];
     }
     if (tid == 0) g.rnnz[r] = tot;
+    const int cadd = packed ? clo : 0;
     for (int q = q0; q < q1; ++q) {
-        const u32 col = sk[q];
-        if (q == 0 || sk[q - 1] != col) {
+        const u32 col = sk[q] >> cs;
+        if (q == 0 || (sk[q - 1] >> cs) != col) {
             double sum = vb[q];
-            for (int j = q + 1; j < P && sk[j] == col; ++j) sum += vb[j];  // ascending: deterministic
-            g.Scol[base + o] = (int)col;
+            for (int j = q + 1; j < P && (sk[j] >> cs) == col; ++j) sum += vb[j];  // ascending: deterministic
+            g.Scol[base + o] = (int)col + cadd;
             g.Sval[base + o] = sum;
             ++o;
         }
