@@ -35,14 +35,15 @@ namespace tsg {
 
 namespace {
 
-constexpr int RS_MAX = 64;            // class S: products (and runs) per row
+constexpr int S16_MAX = 16;           // class S16: products (and runs) per row, 4 rows per wave
+constexpr int RS_MAX = 64;            // class S64: products (and runs) per row, a wave
 // merge classes M1..M4: products and runs per row, threads per row -- each
 // sized so its LDS (16 B per product + 16 B per run) keeps several rows per CU
 constexpr int M1_CAP = 512, M1_RUNS = 128, M1_NT = 128;    // 10 KB
 constexpr int M2_CAP = 1024, M2_RUNS = 256, M2_NT = 256;   // 20 KB
 constexpr int M3_CAP = 2048, M3_RUNS = 512, M3_NT = 512;   // 40 KB
 constexpr int M4_CAP = 4096, M4_RUNS = 512, M4_NT = 1024;  // 72 KB
-constexpr int NCLS = 6;               // S, M1..M4, H
+constexpr int NCLS = 7;               // S16, S64, M1..M4, H
 constexpr int BIN_ROWS = 2048;        // rows per workgroup of the binning kernel
 constexpr int RH_NT = 1024;           // class H: workgroup
 constexpr int RH_WORDS = 16384;       // class H: bitmap words (u64) per window: 128 KB of LDS
@@ -117,12 +118,13 @@ __device__ __forceinline__ int row_class(const int *rpA, const long long *E, int
     const long long e0 = E[a0], P = E[a1] - e0;
     if (soff) soff[r] = e0;
     if (P == 0) return -1;
-    if (P <= RS_MAX && k <= RS_MAX) return 0;
-    if (P <= M1_CAP && k <= M1_RUNS) return 1;
-    if (P <= M2_CAP && k <= M2_RUNS) return 2;
-    if (P <= M3_CAP && k <= M3_RUNS) return 3;
-    if (P <= M4_CAP && k <= M4_RUNS) return 4;
-    return 5;
+    if (P <= S16_MAX && k <= S16_MAX) return 0;
+    if (P <= RS_MAX && k <= RS_MAX) return 1;
+    if (P <= M1_CAP && k <= M1_RUNS) return 2;
+    if (P <= M2_CAP && k <= M2_RUNS) return 3;
+    if (P <= M3_CAP && k <= M3_RUNS) return 4;
+    if (P <= M4_CAP && k <= M4_RUNS) return 5;
+    return 6;
 }
 
 // rows -> classes: lists (class c's rows from lists + c*m) and counts cls[0..NCLS);
@@ -198,63 +200,87 @@ __global__ __launch_bounds__(WG) void k_rows_bin(const int *rpA, int m, const lo
     }
 }
 
-// ---- class S: a wave per row, the products one per lane, ranks by counting
+// ---- classes S16 / S64: G lanes per row (64/G rows per wave), the products
+// one per lane, ranks by counting the group's smaller (column, lane) keys
+template <int G>
 __global__ __launch_bounds__(WG) void k_rows_small(RowsArgs g) {
+    constexpr int RPW = 64 / G;
     __shared__ u64 sk[WAVES][64];
     __shared__ double sv[WAVES][64];
-    const int lane = lane_id(), wv = wave_id();
-    const int i = blockIdx.x * WAVES + wv;
-    if (i >= g.nrows) return;  // wave-uniform
-    const int r = g.list[i];
-    const int a0 = g.rpA[r], k = g.rpA[r + 1] - a0;
-    const long long base = g.E[a0];
-    const int P = (int)(g.E[a0 + k] - base);
-    // lane j < k: run j's offset in the row, B start and A value
-    int roff = 0, bs = 0;
-    double av = 0.0;
-    if (lane < k) {
-        roff = (int)(g.E[a0 + lane] - base);
-        bs = g.ebnd[a0 + lane].x;
-        av = g.vA[a0 + lane];
+    const int lane = lane_id(), wv = wave_id(), sl = lane % G, gb = lane - sl;
+    const int i = (blockIdx.x * WAVES + wv) * RPW + lane / G;
+    if ((blockIdx.x * WAVES + wv) * RPW >= g.nrows) return;  // wave-uniform
+    const bool live = i < g.nrows;
+    int r = 0, a0 = 0, k = 0, P = 0;
+    long long base = 0;
+    if (live) {
+        r = g.list[i];
+        a0 = g.rpA[r];
+        k = g.rpA[r + 1] - a0;
+        base = g.E[a0];
+        P = (int)(g.E[a0 + k] - base);
     }
-    // lane e < P: its run = the last run starting at or before e
+    // lane sl < k: run sl's offset in the row, B start and A value
+    int roff = INT_MAX, bs = 0;
+    double av = 0.0;
+    if (sl < k) {
+        roff = (int)(g.E[a0 + sl] - base);
+        bs = g.ebnd[a0 + sl].x;
+        av = g.vA[a0 + sl];
+    }
+    // position sl: its run = the last run starting at or before it
     int run = 0;
-    for (int j = 1; j < k; ++j) run = (__builtin_amdgcn_readlane(roff, j) <= lane) ? j : run;
-    const int rs = __shfl(roff, run, 64), rb = __shfl(bs, run, 64);
-    const double ra = __shfl(av, run, 64);
+    if constexpr (G == 64) {
+        for (int j = 1; j < k; ++j) run = (__builtin_amdgcn_readlane(roff, j) <= sl) ? j : run;
+    } else {
+#pragma unroll
+        for (int j = 1; j < G; ++j) run = __shfl(roff, j, G) <= sl ? j : run;
+    }
+    const int rs = __shfl(roff, run, G), rb = __shfl(bs, run, G);
+    const double ra = __shfl(av, run, G);
     u64 key = ~0ull;
     double x = 0.0;
-    if (lane < P) {
-        const int p = rb + lane - rs;
-        key = ((u64)(u32)g.Bcol[p] << 32) | (u32)lane;
+    if (sl < P) {
+        const int p = rb + sl - rs;
+        key = ((u64)(u32)g.Bcol[p] << 32) | (u32)sl;
         x = ra * g.Bval[p];
     }
+    const u32 khi = (u32)(key >> 32), klo = (u32)key;
     int rank = 0;
-    for (int f = 0; f < P; ++f) {
-        const u64 kf = ((u64)(u32)__builtin_amdgcn_readlane((int)(key >> 32), f) << 32) |
-                       (u32)__builtin_amdgcn_readlane((int)(u32)key, f);
-        rank += kf < key;
+    if constexpr (G == 64) {  // one row per wave: P is wave-uniform, scalar reads of each key
+        for (int f = 0; f < P; ++f) {
+            const u64 kf = ((u64)(u32)__builtin_amdgcn_readlane((int)khi, f) << 32) |
+                           (u32)__builtin_amdgcn_readlane((int)klo, f);
+            rank += kf < key;
+        }
+    } else {
+#pragma unroll
+        for (int f = 0; f < G; ++f) {
+            const u64 kf = ((u64)(u32)__shfl((int)khi, f, G) << 32) | (u32)__shfl((int)klo, f, G);
+            rank += kf < key;  // (lanes past P hold ~0: never below a product)
+        }
     }
-    if (lane < P) {
-        sk[wv][rank] = key;
-        sv[wv][rank] = x;
+    if (sl < P) {
+        sk[wv][gb + rank] = key;
+        sv[wv][gb + rank] = x;
     }
     wave_lds_sync();
     int col = -1;
     bool head = false;
-    if (lane < P) {
-        col = key_col(sk[wv][lane]);
-        head = lane == 0 || key_col(sk[wv][lane - 1]) != col;
+    if (sl < P) {
+        col = key_col(sk[wv][gb + sl]);
+        head = sl == 0 || key_col(sk[wv][gb + sl - 1]) != col;
     }
-    const u64 hb = __ballot(head);
+    const u64 gm = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << gb;
+    const u64 hb = __ballot(head) & gm;
     if (head) {
-        double s = sv[wv][lane];
-        for (int j = lane + 1; j < P && key_col(sk[wv][j]) == col; ++j) s += sv[wv][j];
-        const long long o = base + lanes_below(hb);
+        double s = sv[wv][gb + sl];
+        for (int j = sl + 1; j < P && key_col(sk[wv][gb + j]) == col; ++j) s += sv[wv][gb + j];
+        const long long o = base + (long long)lanes_below(hb);
         g.Scol[o] = col;
         g.Sval[o] = s;
     }
-    if (lane == 0) g.rnnz[r] = __popcll(hb);
+    if (live && sl == 0) g.rnnz[r] = __popcll(hb);
 }
 
 // U independent searches in lockstep (U LDS reads in flight per step): first
@@ -821,13 +847,14 @@ int dev_spgemm_rows(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, tsg
         TSG_HIP(hipGetLastError());
         return TSG_OK;
     };
-    TSG_TRY(launch(5, k_rows_bitmap, ncls[5], RH_NT, s));
+    TSG_TRY(launch(6, k_rows_bitmap, ncls[6], RH_NT, s));
     TSG_TRY(cx.aux_fork(s));
-    TSG_TRY(launch(4, k_rows_merge<M4_NT, M4_CAP, M4_RUNS>, ncls[4], M4_NT, cx.aux[0]));
-    TSG_TRY(launch(3, k_rows_merge<M3_NT, M3_CAP, M3_RUNS>, ncls[3], M3_NT, cx.aux[1]));
-    TSG_TRY(launch(2, k_rows_merge<M2_NT, M2_CAP, M2_RUNS>, ncls[2], M2_NT, cx.aux[2]));
-    TSG_TRY(launch(1, k_rows_merge<M1_NT, M1_CAP, M1_RUNS>, ncls[1], M1_NT, s));
-    TSG_TRY(launch(0, k_rows_small, (ncls[0] + WAVES - 1) / WAVES, WG, s));
+    TSG_TRY(launch(5, k_rows_merge<M4_NT, M4_CAP, M4_RUNS>, ncls[5], M4_NT, cx.aux[0]));
+    TSG_TRY(launch(4, k_rows_merge<M3_NT, M3_CAP, M3_RUNS>, ncls[4], M3_NT, cx.aux[1]));
+    TSG_TRY(launch(3, k_rows_merge<M2_NT, M2_CAP, M2_RUNS>, ncls[3], M2_NT, cx.aux[2]));
+    TSG_TRY(launch(2, k_rows_merge<M1_NT, M1_CAP, M1_RUNS>, ncls[2], M1_NT, s));
+    TSG_TRY(launch(1, k_rows_small<64>, (ncls[1] + WAVES - 1) / WAVES, WG, s));
+    TSG_TRY(launch(0, k_rows_small<16>, (ncls[0] + 4 * WAVES - 1) / (4 * WAVES), WG, s));
     TSG_TRY(cx.aux_join(s));
     if (ev) TSG_HIP(hipEventRecord(ev[5], s));
 #ifdef TSG_ROWS_PROF
@@ -841,7 +868,7 @@ int dev_spgemm_rows(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, tsg
                 for (int k = 0; k < 8; ++k) pr[c * 8 + k] += raw[(c * 256 + b) * 8 + k];
         static const char *nm[3] = {"H", "M2-M4", "M1"};
         for (int c = 0; c < 3; ++c) {
-            const int cnt = c == 0 ? ncls[5] : c == 1 ? ncls[2] + ncls[3] + ncls[4] : ncls[1];
+            const int cnt = c == 0 ? ncls[6] : c == 1 ? ncls[3] + ncls[4] + ncls[5] : ncls[2];
             fprintf(stderr, "rows %s (%d rows) us/row:", nm[c], cnt);
             for (int k = 0; k < 6; ++k) fprintf(stderr, " %.2f", cnt ? pr[c * 8 + k] / 100.0 / cnt : 0.0);
             fprintf(stderr, "\n");

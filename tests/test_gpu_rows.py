@@ -1,5 +1,6 @@
 """The row-merge path (spgemm_amd/csrc/tsg_rows.hip): rows binned by element
-products into six classes -- S (<= 64, ranks by counting in a wave), M1..M4
+products into seven classes -- S16 / S64 (<= 16 / 64 products: ranks by
+counting in 16 or 64 lanes), M1..M4
 (<= 512 / 1,024 / 2,048 / 4,096 products: pairwise merge-path merges of the
 runs in LDS) and H (longer rows or more runs: an LDS column bitmap per window
 of 524,288 columns, f64 atomics for the values).  TSG_PATH=rows forces it.  Pattern
@@ -61,8 +62,10 @@ def _check(A_, B_=None, aat=False, real=False, seed=0):
     return st
 
 
-# (products, runs) caps of the classes S, M1..M4; longer rows are class H (= 5)
-CAPS = [(64, 64), (512, 128), (1024, 256), (2048, 512), (4096, 512)]
+# (products, runs) caps of the classes S16, S64, M1..M4; longer rows are class H
+CAPS = [(16, 16), (64, 64), (512, 128), (1024, 256), (2048, 512), (4096, 512)]
+H = len(CAPS)
+M3, M4 = H - 2, H - 1
 
 
 def _classes(m, n, rp, ci, rpB):
@@ -72,8 +75,8 @@ def _classes(m, n, rp, ci, rpB):
     P = cum[rp[1:]] - cum[rp[:-1]]
     k = np.diff(rp)
     c = np.full(m, -1)
-    c[(P > 0)] = 5
-    for i in range(4, -1, -1):
+    c[(P > 0)] = H
+    for i in range(len(CAPS) - 1, -1, -1):
         c[(P > 0) & (P <= CAPS[i][0]) & (k <= CAPS[i][1])] = i
     return c
 
@@ -83,7 +86,7 @@ def test_rows_full_size_synthetic(name):
     m, n, rp, ci, vv = synth.GENERATORS[name]()
     cls = _classes(m, n, rp, ci, rp)
     if name == "webbase":  # every class is populated
-        assert all((cls == c).any() for c in range(6))
+        assert all((cls == c).any() for c in range(H + 1))
     _check((m, n, rp, ci, vv), aat=name == "mc2depi")
 
 
@@ -103,7 +106,7 @@ def test_rows_random_mixed_classes_real_values():
     B = (Bm[0], Bm[1], Bm[2], np.concatenate([np.sort(Bm[3][Bm[2][i]:Bm[2][i + 1]]) for i in range(n)]).astype(np.int32),
          Bm[4])
     cls = _classes(3000, n, A[2], A[3], B[2])
-    assert all((cls == c).any() for c in range(5))
+    assert all((cls == c).any() for c in range(H))
     _check(A, B, real=True, seed=5)
 
 
@@ -132,7 +135,7 @@ def test_rows_many_runs_go_to_bitmap():
     A = _csr(201, n, rows)
     Bm, Bn, Brp, Bci, Bvv = synth.random_csr(n, n, density=3e-5, seed=6)
     Bci = np.concatenate([np.sort(Bci[Brp[i]:Brp[i + 1]]) for i in range(n)]).astype(np.int32)
-    assert _classes(201, n, A[2], A[3], Brp)[0] == 5
+    assert _classes(201, n, A[2], A[3], Brp)[0] == H
     _check(A, (Bm, Bn, Brp, Bci, Bvv), real=True, seed=8)
 
 
@@ -148,7 +151,7 @@ def test_rows_bitmap_several_windows():
         Brows.append(np.sort(rng.choice(np.arange(lo, lo + 400_000), size=400, replace=False)))
     B = _csr(k, n, Brows)
     A = _csr(3, k, [np.arange(k), np.arange(0, k, 2), np.array([1, 3])])
-    assert _classes(3, k, A[2], A[3], B[2])[0] == 5
+    assert _classes(3, k, A[2], A[3], B[2])[0] == H
     _check(A, B, real=True, seed=2)
 
 
@@ -157,7 +160,7 @@ def test_rows_merge_long_runs_and_collisions():
     rows = [np.arange(max(0, i - 30), min(2000, i + 31)) for i in range(2000)]
     A = _csr(2000, 2000, rows)
     cls = _classes(2000, 2000, A[2], A[3], A[2])
-    assert (cls == 4).any() and (cls == 3).any() and (cls >= 3).all()
+    assert (cls == M4).any() and (cls == M3).any() and (cls >= M3).all()
     _check(A, real=True, seed=4)
 
 
