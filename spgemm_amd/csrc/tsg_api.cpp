@@ -95,6 +95,21 @@ int Context::init(int dev) {
     return TSG_OK;
 }
 
+int stream_wait(hipStream_t s) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e == hipSuccess) return TSG_OK;
+        if (e != hipErrorNotReady) {
+            report_hip_error(e, "hipStreamQuery", __FILE__, __LINE__);
+            return TSG_ERR_HIP;
+        }
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(1000)) break;
+    }
+    TSG_HIP(hipStreamSynchronize(s));
+    return TSG_OK;
+}
+
 int Context::aux_fork(hipStream_t s) {
     if (!aux[0]) {
         for (int i = 0; i < kAux; ++i) TSG_HIP(hipStreamCreateWithFlags(&aux[i], hipStreamNonBlocking));
@@ -856,85 +871,73 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
     // back with the counts' host round trip.  (With unsorted B rows the counts are
     // discarded: the full csr2tile below rebuilds A's tiles.)
     TSG_TRY(dev_rows_sorted_async(cx, *B, cx.pinned + 1, s));
-    // Fused element path (tsg_fused.hip: steps 1-3 + tile2csr in one persistent
-    // kernel over row units) for short-row products -- every C row within
-    // kFusedMaxRowProducts element products (longest A row x longest B row),
-    // B's rows column-sorted -- where its one-kernel pass beats the staged
-    // pipeline (mc2depi A*A^T: 0.40 vs 0.83 ms).  Web graphs and FEM matrices
-    // (long rows) take the staged tile pipeline below, which is faster there.
-    // TSG_PATH=fused / tiles forces either path.
-    // Banded path (tsg_band.hip): when every C row's reachable columns fit one
-    // window of <= 2,048 columns holding at least as many products as columns
-    // (FEM-like operands with dense rows, e.g. cant), one walk accumulates the
-    // row in a dense LDS window.  Checked only for rows of >= 8 entries on
-    // average (a statistics kernel + one host round trip).
-    // Row-merge path (tsg_rows.hip): the remaining sorted-B products, unless its
-    // binning finds them hub-dominated (class-H rows over a quarter of the work,
-    // or a row over kRowsMaxRowProducts products: R-MAT, mawi), which then take
-    // the staged tile pipeline (web graphs: webbase 1.95 vs 2.75 ms).
+    // Routing, B's rows column-sorted:
+    //  * banded path (tsg_band.hip) when A averages >= 8 entries per row and every
+    //    C row's reachable columns fit one window of <= 2,048 columns holding at
+    //    least as many products as columns (FEM-like: cant); its check is a
+    //    statistics kernel + one host round trip;
+    //  * otherwise the row-merge setup (entry table, classes) + one round trip:
+    //    fused path (tsg_fused.hip) when no C row has over kFusedMaxRowProducts
+    //    element products (mc2depi), row-merge path (tsg_rows.hip) unless the
+    //    products are hub-dominated (dev_rows_accept: R-MAT, mawi);
+    //  * the staged tile pipeline below for the rest and for unsorted B rows.
     // TSG_PATH=fused / band / rows / tiles forces a path (band when its check
     // passes).
     const char *path = getenv("TSG_PATH");
     const bool force_fused = path && !strcmp(path, "fused"), force_tiles = path && !strcmp(path, "tiles");
     const bool force_band = path && !strcmp(path, "band"), force_rows = path && !strcmp(path, "rows");
     if (!force_tiles) {
-        TSG_TRY(dev_row_maxlen_async(cx, *A, cx.pinned + 2, s));
-        TSG_TRY(dev_row_maxlen_async(cx, *B, cx.pinned + 3, s));
-        TSG_HIP(hipStreamSynchronize(s));
-        const bool short_rows = (long long)cx.pinned[2] * (long long)cx.pinned[3] <= kFusedMaxRowProducts;
-        const bool bsorted0 = cx.pinned[1] == 0;
         bool band = false;
         BandWin bw;
-        if (bsorted0 && !force_fused && !force_rows &&
-            (force_band || (!short_rows && A->m > 0 && A->nnz >= 8LL * A->m)))
+        // band candidates first (A rows of >= 8 entries on average): the window
+        // check's read-back also brings the sortedness flag
+        if (!force_fused && !force_rows && (force_band || (A->m > 0 && A->nnz >= 8LL * A->m)))
             TSG_TRY(dev_band_check(cx, *A, *B, force_band, &band, &bw, s));
-        bool rows = false;
-        if (!band) TSG_HIP(hipEventRecord(cx.ev[9], s));
-        if (!band && bsorted0 && !force_fused && !force_band && (force_rows || !short_rows)) {
-            bool declined = false;
-            TSG_TRY(dev_spgemm_rows(cx, *A, *B, *C, &st, s, cx.ev, force_rows, &declined));
-            rows = !declined;
+        if (band && cx.pinned[1] != 0) {  // unsorted B rows: the windows mean nothing
+            cx.put(bw.win);
+            cx.put(bw.width);
+            band = false;
         }
-        if (band || rows) {
-            if (band) {
-                TSG_HIP(hipEventRecord(cx.ev[9], s));
-                const int rc = dev_spgemm_band(cx, *A, *B, bw, *C, &st, s, cx.ev);
-                cx.put(bw.win);
-                cx.put(bw.width);
+        long long path_id = -1;
+        TSG_HIP(hipEventRecord(cx.ev[9], s));
+        if (band) {
+            const int rc = dev_spgemm_band(cx, *A, *B, bw, *C, &st, s, cx.ev);
+            cx.put(bw.win);
+            cx.put(bw.width);
+            TSG_TRY(rc);
+            path_id = TSG_PATH_BAND;
+        } else {
+            // the row-merge setup (its entry table is the fused path's too) and the
+            // sortedness flag: one host round trip decides fused / rows / tiles
+            TSG_HIP(hipEventRecord(cx.ev[0], s));
+            RowsPlan plan;
+            TSG_TRY(dev_rows_setup_async(cx, *A, *B, plan, s));
+            TSG_TRY(stream_wait(s));
+            dev_rows_setup_read(cx, plan);
+            const bool bsorted0 = cx.pinned[1] == 0;
+            if (bsorted0 && !force_band && (force_fused || (!force_rows && plan.pmax <= kFusedMaxRowProducts))) {
+                const int rc = dev_spgemm_fused(cx, *A, *B, *C, &st, s, cx.ev, plan.ebnd, plan.E);
+                dev_rows_release(cx, plan);
                 TSG_TRY(rc);
+                path_id = TSG_PATH_FUSED;
+            } else if (bsorted0 && !force_band && (force_rows || dev_rows_accept(plan))) {
+                TSG_TRY(dev_rows_run(cx, *A, *B, plan, *C, &st, s, cx.ev));
+                path_id = TSG_PATH_ROWS;
+            } else {
+                dev_rows_release(cx, plan);
             }
-            TSG_HIP(hipEventRecord(cx.ev[10], s));
-            TSG_HIP(hipEventSynchronize(cx.ev[10]));
-            auto h1 = std::chrono::steady_clock::now();
-            st.numtileA = -1;
-            st.numtileB = -1;
-            st.path = band ? TSG_PATH_BAND : TSG_PATH_ROWS;
-            st.t_csr2tile_ms = ev_ms(cx.ev[8], cx.ev[9]);   // sortedness (+ band: window statistics; no csr2tile)
-            st.t_step1_ms = ev_ms(cx.ev[0], cx.ev[1]);      // entry ranges, staging offsets (+ rows: classes)
-            st.t_step2_ms = 0.0;                            // (one walk: structure and values together)
-            st.t_step3_ms = ev_ms(cx.ev[1], cx.ev[3]);      // the row kernel(s), row pointers, compaction
-            st.t_step3_kernel_ms = ev_ms(cx.ev[4], cx.ev[5]);
-            st.t_tile2csr_ms = 0.0;
-            st.t_kern_ms = ev_ms(cx.ev[0], cx.ev[3]);
-            st.t_e2e_ms = std::chrono::duration<double, std::milli>(h1 - h0).count();
-            st.t_malloc_ms = st.t_e2e_ms - ev_ms(cx.ev[8], cx.ev[10]);
-            if (st.t_malloc_ms < 0) st.t_malloc_ms = 0;
-            if (stats) *stats = st;
-            return TSG_OK;
         }
-        if (bsorted0 && (short_rows || force_fused)) {
-            TSG_HIP(hipEventRecord(cx.ev[9], s));
-            TSG_TRY(dev_spgemm_fused(cx, *A, *B, *C, &st, s, cx.ev));
+        if (path_id >= 0) {
             TSG_HIP(hipEventRecord(cx.ev[10], s));
             TSG_HIP(hipEventSynchronize(cx.ev[10]));
             auto h1 = std::chrono::steady_clock::now();
             st.numtileA = -1;
             st.numtileB = -1;
-            st.path = TSG_PATH_FUSED;
-            st.t_csr2tile_ms = ev_ms(cx.ev[8], cx.ev[9]);   // B sortedness check (no csr2tile on this path)
-            st.t_step1_ms = ev_ms(cx.ev[0], cx.ev[1]);      // entry ranges, row classes, heavy-row windows, units
-            st.t_step2_ms = 0.0;                            // (fused into the unit kernel)
-            st.t_step3_ms = ev_ms(cx.ev[1], cx.ev[3]);      // the unit kernel (steps 1-3 + tile2csr) + allocations
+            st.path = path_id;
+            st.t_csr2tile_ms = ev_ms(cx.ev[8], cx.ev[9]);   // sortedness (+ band: window statistics; no csr2tile)
+            st.t_step1_ms = ev_ms(cx.ev[0], cx.ev[1]);      // entry table, classes / row windows / units
+            st.t_step2_ms = 0.0;                            // (structure and values together)
+            st.t_step3_ms = ev_ms(cx.ev[1], cx.ev[3]);      // the row / unit kernels, row pointers, compaction
             st.t_step3_kernel_ms = ev_ms(cx.ev[4], cx.ev[5]);
             st.t_tile2csr_ms = 0.0;                         // (fused)
             st.t_kern_ms = ev_ms(cx.ev[0], cx.ev[3]);

@@ -230,7 +230,7 @@ int dev_band_check(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, bool
                                                         B.columnindex, win, width, bad);
     TSG_HIP(hipGetLastError());
     TSG_HIP(hipMemcpyAsync(cx.pinned + 8, bad, 6 * sizeof(int), hipMemcpyDeviceToHost, s));
-    TSG_HIP(hipStreamSynchronize(s));
+    TSG_TRY(stream_wait(s));
     cx.put(bad);
     const long long products = *reinterpret_cast<const long long *>(cx.pinned + 10);
     const long long wcols = *reinterpret_cast<const long long *>(cx.pinned + 12);
@@ -292,7 +292,7 @@ int dev_spgemm_band(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, Ban
                                                                C.value);
     TSG_HIP(hipGetLastError());
     if (ev) TSG_HIP(hipEventRecord(ev[3], s));
-    TSG_HIP(hipStreamSynchronize(s));
+    TSG_TRY(stream_wait(s));
     cx.put(ebnd);
     cx.put(Scol);
     cx.put(Sval);

@@ -148,7 +148,7 @@ static int scan_i32_total_impl(Context &cx, int *a, long n, hipStream_t s, long 
     before_read();
     if (part) TSG_HIP(hipMemcpyAsync(cx.pinned64, part + nb, sizeof(long long), hipMemcpyDeviceToHost, s));
     if (extra_d) TSG_HIP(hipMemcpyAsync(cx.pinned64 + 1, extra_d, sizeof(long long), hipMemcpyDeviceToHost, s));
-    if (part || extra_d) TSG_HIP(hipStreamSynchronize(s));
+    if (part || extra_d) TSG_TRY(stream_wait(s));
     if (part) *total = cx.pinned64[0];
     if (extra_d) *extra_h = cx.pinned64[1];
     cx.put(part);
@@ -390,14 +390,14 @@ int launch_nnzcub(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, u64 *
 
 int read_i32(Context &cx, const int *d, int *h, hipStream_t s) {
     TSG_HIP(hipMemcpyAsync(cx.pinned, d, sizeof(int), hipMemcpyDeviceToHost, s));
-    TSG_HIP(hipStreamSynchronize(s));
+    TSG_TRY(stream_wait(s));
     *h = cx.pinned[0];
     return TSG_OK;
 }
 
 int read_i64(Context &cx, const long long *d, long long *h, hipStream_t s) {
     TSG_HIP(hipMemcpyAsync(cx.pinned64, d, sizeof(long long), hipMemcpyDeviceToHost, s));
-    TSG_HIP(hipStreamSynchronize(s));
+    TSG_TRY(stream_wait(s));
     *h = cx.pinned64[0];
     return TSG_OK;
 }
@@ -1341,7 +1341,7 @@ int dev_rows_sorted_async(Context &cx, const tsg_dev_csr &M, int *host_flag, hip
 }
 int dev_rows_sorted(Context &cx, const tsg_dev_csr &M, bool *sorted, hipStream_t s) {
     TSG_TRY(dev_rows_sorted_async(cx, M, cx.pinned + 1, s));
-    TSG_HIP(hipStreamSynchronize(s));
+    TSG_TRY(stream_wait(s));
     *sorted = cx.pinned[1] == 0;
     return TSG_OK;
 }
@@ -2483,7 +2483,7 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     long long ne = 0;
     TSG_HIP(hipMemcpyAsync(cx.pinned, uoff + tilemA, sizeof(int), hipMemcpyDeviceToHost, s));
     if (ebase) TSG_HIP(hipMemcpyAsync(cx.pinned64, ebase + tilemA, sizeof(long long), hipMemcpyDeviceToHost, s));
-    TSG_HIP(hipStreamSynchronize(s));
+    TSG_TRY(stream_wait(s));
     nunits = cx.pinned[0];
     if (ebase) ne = cx.pinned64[0];
     const int gu = grid_for(maxu, 1, TSG_GU_CAP);  // workgroups of steps 2 and 3 (units strided over them)
@@ -2612,7 +2612,7 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     if (g_ablate & 64) {
         unsigned long long pr[16];
         TSG_HIP(hipMemcpyFromSymbolAsync(pr, HIP_SYMBOL(g_prof), sizeof(pr), 0, hipMemcpyDeviceToHost, s));
-        TSG_HIP(hipStreamSynchronize(s));
+        TSG_TRY(stream_wait(s));
         double tot = 0, tot2 = 0;
         for (int k = 0; k < 8; ++k) tot += (double)pr[k];
         for (int k = 8; k < 16; ++k) tot2 += (double)pr[k];
@@ -2638,7 +2638,7 @@ int dev_tilespgemm(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, 
     if (ev) TSG_HIP(hipEventRecord(ev[3], s));
     if (defer_nnz) {  // the pipeline's one read-back after step 3
         TSG_HIP(hipMemcpyAsync(cx.pinned, csr_out->rowpointer + A.m, sizeof(int), hipMemcpyDeviceToHost, s));
-        TSG_HIP(hipStreamSynchronize(s));
+        TSG_TRY(stream_wait(s));
         nnzC = cx.pinned[0];
         C.nnz = nnzC;
         csr_out->nnz = nnzC;

@@ -785,7 +785,7 @@ int dev_row_maxlen_async(Context &cx, const tsg_dev_csr &M, int *host_out, hipSt
 // ev (optional, >= 6 events): 0 start | 1 units built | 4..5 the unit kernel | 3 end
 // ---------------------------------------------------------------------------
 int dev_spgemm_fused(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, tsg_dev_csr &C, tsg_stats *st,
-                     hipStream_t s, hipEvent_t *ev) {
+                     hipStream_t s, hipEvent_t *ev, int2 *ebnd_pre, long long *cum_pre) {
     if (A.n != B.m) return TSG_ERR_INVALID;
     const int m = A.m;
     const long nnzA = A.nnz;
@@ -793,12 +793,18 @@ int dev_spgemm_fused(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, ts
     C = tsg_dev_csr{};
     C.m = m;
     C.n = B.n;
-    if (ev) TSG_HIP(hipEventRecord(ev[0], s));
+    if (ev && !(ebnd_pre && cum_pre)) TSG_HIP(hipEventRecord(ev[0], s));  // (else the caller's, before the shared setup)
     int2 *ebnd = nullptr;
     long long *cum = nullptr;
     int *ucnt = nullptr, *hlist = nullptr, *ctr = nullptr, *wofs = nullptr;
-    TSG_TRY(cx.get(&ebnd, (size_t)nnzA + 1));
-    TSG_TRY(cx.get(&cum, (size_t)nnzA + 1));
+    const bool pre = ebnd_pre && cum_pre;
+    if (pre) {
+        ebnd = ebnd_pre;
+        cum = cum_pre;
+    } else {
+        TSG_TRY(cx.get(&ebnd, (size_t)nnzA + 1));
+        TSG_TRY(cx.get(&cum, (size_t)nnzA + 1));
+    }
     TSG_TRY(cx.get(&ucnt, (size_t)m + 1));
     TSG_TRY(cx.get(&hlist, (size_t)m + 1));
     TSG_TRY(cx.get(&wofs, (size_t)m + 1));
@@ -806,15 +812,17 @@ int dev_spgemm_fused(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, ts
     //            [7] nnz(C) [8..9] products [10..11] C row-segments
     TSG_TRY(cx.get(&ctr, 16));
     TSG_HIP(hipMemsetAsync(ctr, 0, 16 * sizeof(int), s));
-    k_fz_entries<<<grid_for(nnzA + 1, WG, 16384), WG, 0, s>>>(A.columnindex, nnzA, B.rowpointer, ebnd, cum);
-    TSG_HIP(hipGetLastError());
-    TSG_TRY(scan_exclusive_i64(cx, cum, nnzA + 1, s));
+    if (!pre) {
+        k_fz_entries<<<grid_for(nnzA + 1, WG, 16384), WG, 0, s>>>(A.columnindex, nnzA, B.rowpointer, ebnd, cum);
+        TSG_HIP(hipGetLastError());
+        TSG_TRY(scan_exclusive_i64(cx, cum, nnzA + 1, s));
+    }
     k_fz_rows<<<grid_for(((long)m + FZ_ROWS - 1) / FZ_ROWS, WAVES, 4096), WG, 0, s>>>(A.rowpointer, m, cum, nnzA,
                                                                                    ucnt, hlist, ctr);
     TSG_HIP(hipGetLastError());
     // one host round trip: the product total (output bound) and the heavy rows
     TSG_HIP(hipMemcpyAsync(cx.pinned64, ctr, 12 * sizeof(int), hipMemcpyDeviceToHost, s));
-    TSG_HIP(hipStreamSynchronize(s));
+    TSG_TRY(stream_wait(s));
     const int nheavy = reinterpret_cast<const int *>(cx.pinned64)[0];
     const unsigned long long heavyP = reinterpret_cast<const unsigned long long *>(cx.pinned64)[1];
     const long long total = cx.pinned64[4];
@@ -859,7 +867,7 @@ int dev_spgemm_fused(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, ts
     // the one read-back after the kernel: nnz(C), the overflow flag, the segment count
     TSG_HIP(hipMemcpyAsync(cx.pinned64, ctr, 12 * sizeof(int), hipMemcpyDeviceToHost, s));
     if (ev) TSG_HIP(hipEventRecord(ev[3], s));
-    TSG_HIP(hipStreamSynchronize(s));
+    TSG_TRY(stream_wait(s));
 #ifdef TSG_FZ_PROF
     {
         unsigned long long pr[9];
@@ -873,8 +881,10 @@ int dev_spgemm_fused(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, ts
         fprintf(stderr, "  (total %.3g ticks)\n", tot);
     }
 #endif
-    cx.put(ebnd);
-    cx.put(cum);
+    if (!pre) {
+        cx.put(ebnd);
+        cx.put(cum);
+    }
     cx.put(ucnt);
     cx.put(hlist);
     cx.put(wofs);

@@ -31,6 +31,10 @@ namespace tsg {
 
 void report_hip_error(hipError_t e, const char *what, const char *file, int line);
 
+// Wait for the stream's work: poll for up to ~1 ms (a blocking wait costs
+// 20-50 us of wake-up on every mid-pipeline size read-back), then block.
+int stream_wait(hipStream_t s);
+
 // Caching device allocator: power-of-two size classes, blocks return to a free
 // list and are reused by later allocations on the (single) call stream, so the
 // steady-state pipeline performs no hipMalloc.
@@ -123,11 +127,12 @@ int dev_tile2csr(Context &cx, const tsg_dev_tiles &C, tsg_dev_csr &out, hipStrea
 // ev (optional): 0 start | 1 units built | 4, 5 around the unit kernel | 3 end
 // longest row of M, copied (stream-ordered) into *host_out
 int dev_row_maxlen_async(Context &cx, const tsg_dev_csr &M, int *host_out, hipStream_t s);
-// rows of C with at most this many element products (max row length of A x of B)
-// route to the fused path by default
+// rows of C with at most this many element products (the longest C row, from
+// the row-merge setup) route to the fused path by default
 constexpr long long kFusedMaxRowProducts = 256;
+// ebnd / cum (optional): the entry table of a row-merge setup (same layout), reused
 int dev_spgemm_fused(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, tsg_dev_csr &C, tsg_stats *st,
-                     hipStream_t s, hipEvent_t *ev);
+                     hipStream_t s, hipEvent_t *ev, int2 *ebnd_pre = nullptr, long long *cum_pre = nullptr);
 
 // banded path (tsg_band.hip): every C row's reachable columns within one
 // window of <= 2,048 columns, the windows holding at least as many products as
@@ -145,14 +150,30 @@ int dev_spgemm_band(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, Ban
                     tsg_stats *st, hipStream_t s, hipEvent_t *ev);
 // row-merge path (tsg_rows.hip): CSR in -> CSR out, B's rows column-sorted;
 // rows binned by element products, each row's B rows merged (or, for the
-// longest rows, marked in an LDS column bitmap).
-// ev (optional): 0 start | 1 set up | 4..5 the row kernels | 3 end
-// Unless force, it declines (*declined, nothing computed) products whose class-H
-// rows (> 4,096 products or > 512 runs) hold over a quarter of the work or with
-// a row over kRowsMaxRowProducts products.
+// longest rows, marked in an LDS column bitmap).  Two halves around the
+// caller's one host round trip: the setup (entry table = the fused path's
+// too, classes, routing statistics), then the run.
+struct RowsPlan {
+    int2 *ebnd = nullptr;      // per A entry: its B row's [start, end)
+    long long *E = nullptr;    // per A entry: prefix of the element products
+    int *lists = nullptr;      // the classes' rows
+    long long *soff = nullptr; // per row: staging offset
+    int *cls = nullptr;        // class counts + statistics (device)
+    int *rowpointer = nullptr; // C's row pointers (row counts until the scan)
+    int ncls[8] = {};
+    long long products = 0, hprod = 0, pmax = 0;  // all / class-H rows' products, the longest row's
+};
+// Unless forced, the path declines (dev_rows_accept false) products whose
+// class-H rows (> 4,096 products or > 512 runs) hold over a quarter of the work
+// or with a row over kRowsMaxRowProducts products.
 constexpr long long kRowsMaxRowProducts = 65536;
-int dev_spgemm_rows(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, tsg_dev_csr &C, tsg_stats *st,
-                    hipStream_t s, hipEvent_t *ev, bool force, bool *declined);
+int dev_rows_setup_async(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPlan &p, hipStream_t s);
+void dev_rows_setup_read(Context &cx, RowsPlan &p);  // after the stream synchronised
+bool dev_rows_accept(const RowsPlan &p);
+void dev_rows_release(Context &cx, RowsPlan &p);
+// ev (optional): 1 set up | 4..5 the row kernels | 3 end
+int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPlan &p, tsg_dev_csr &C,
+                 tsg_stats *st, hipStream_t s, hipEvent_t *ev);
 // exclusive scan (n+1 idiom) whose total is read back
 int scan_exclusive_i32_total(Context &cx, int *a, long n, hipStream_t s, long long *total);
 

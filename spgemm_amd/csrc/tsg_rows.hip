@@ -734,13 +734,17 @@ __global__ __launch_bounds__(WG) void k_rows_cfirst(int m, const int *Crp, int *
     }
 }
 
-__global__ __launch_bounds__(WG) void k_rows_compact(int m, int nnz, const int *cfirst, const long long *soff,
-                                                     const int *Crp, const int *Scol, const double *Sval, int *Ccol,
-                                                     double *Cval) {
+// (the grid may cover more chunks than nnz(C) has -- sized by the products,
+// so that no host round trip waits for nnz: the surplus workgroups exit)
+__global__ __launch_bounds__(WG) void k_rows_compact(int m, const int *cfirst, const long long *soff, const int *Crp,
+                                                     const int *Scol, const double *Sval, int *Ccol, double *Cval) {
     __shared__ int rowof[CP_CH];
     __shared__ int red[WAVES];
     const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
-    const int c0 = blockIdx.x * CP_CH, n = min(CP_CH, nnz - c0);
+    const int nnz = Crp[m];
+    const int c0 = blockIdx.x * CP_CH;
+    if (c0 >= nnz) return;  // (workgroup-uniform)
+    const int n = min(CP_CH, nnz - c0);
     const int rf = cfirst[blockIdx.x];
     const int rl = c0 + CP_CH < nnz ? cfirst[blockIdx.x + 1] : m - 1;
     for (int i = tid; i < CP_CH; i += WG) rowof[i] = i == 0 ? rf : -1;
@@ -776,53 +780,66 @@ __global__ __launch_bounds__(WG) void k_rows_compact(int m, int nnz, const int *
     }
 }
 
-// CSR in -> CSR out (B's rows column-sorted; the caller checked).
-// ev (optional): 0 start | 1 set up | 4..5 the row kernels | 3 end
-int dev_spgemm_rows(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, tsg_dev_csr &C, tsg_stats *st,
-                    hipStream_t s, hipEvent_t *ev, bool force, bool *declined) {
-    *declined = false;
+// Setup (stream-ordered, no host round trip): the entry table, its scan and the
+// classes; the statistics land in cx.pinned64[0..6] once the stream is synced.
+int dev_rows_setup_async(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPlan &p, hipStream_t s) {
+    static_assert(NCLS <= 8, "class counts in cls[0..8)");
+    const int m = A.m;
+    p = RowsPlan{};
+    TSG_TRY(cx.get(&p.ebnd, (size_t)A.nnz + 1));
+    TSG_TRY(cx.get(&p.E, (size_t)A.nnz + 1));
+    TSG_TRY(cx.get(&p.lists, (size_t)NCLS * (m > 0 ? m : 1)));
+    TSG_TRY(cx.get(&p.soff, (size_t)m + 1));
+    TSG_TRY(cx.get(&p.cls, 12));  // class counts, then 2 u64 statistics at [8..11]
+    TSG_TRY(cx.get(&p.rowpointer, (size_t)m + 1));
+    unsigned long long *hst = reinterpret_cast<unsigned long long *>(p.cls + 8);
+    TSG_HIP(hipMemsetAsync(p.cls, 0, 12 * sizeof(int), s));
+    k_rows_entries<<<grid_for((long)A.nnz + 1, WG, 16384), WG, 0, s>>>(A.columnindex, A.nnz, B.rowpointer, p.ebnd,
+                                                                      p.E);
+    TSG_HIP(hipGetLastError());
+    TSG_TRY(scan_exclusive_i64(cx, p.E, (long)A.nnz + 1, s));
+    if (m > 0)
+        k_rows_bin<<<(m + BIN_ROWS - 1) / BIN_ROWS, WG, 0, s>>>(A.rowpointer, m, p.E, p.rowpointer, p.lists, p.cls,
+                                                                p.soff, hst);
+    TSG_HIP(hipGetLastError());
+    TSG_HIP(hipMemcpyAsync(cx.pinned64, p.E + A.nnz, sizeof(long long), hipMemcpyDeviceToHost, s));
+    TSG_HIP(hipMemcpyAsync(cx.pinned64 + 1, p.cls, 12 * sizeof(int), hipMemcpyDeviceToHost, s));
+    return TSG_OK;
+}
+
+void dev_rows_setup_read(Context &cx, RowsPlan &p) {
+    p.products = cx.pinned64[0];
+    for (int t = 0; t < NCLS; ++t) p.ncls[t] = reinterpret_cast<const int *>(cx.pinned64 + 1)[t];
+    p.hprod = cx.pinned64[5];
+    p.pmax = cx.pinned64[6];
+}
+
+// routing: the path is built for rows of modest length (class H a minority of
+// the work); hub-dominated products (R-MAT, mawi) take the staged pipeline
+bool dev_rows_accept(const RowsPlan &p) { return p.hprod * 4 <= p.products && p.pmax <= kRowsMaxRowProducts; }
+
+void dev_rows_release(Context &cx, RowsPlan &p) {
+    void *ps[] = {p.ebnd, p.E, p.lists, p.soff, p.cls, p.rowpointer};
+    for (void *q : ps) cx.put(q);
+    p = RowsPlan{};
+}
+
+// CSR in -> CSR out from a setup (B's rows column-sorted; the caller checked);
+// consumes the plan.  ev (optional): 1 set up | 4..5 the row kernels | 3 end
+int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPlan &p, tsg_dev_csr &C,
+                 tsg_stats *st, hipStream_t s, hipEvent_t *ev) {
     const int m = A.m;
     C = tsg_dev_csr{};
     C.m = m;
     C.n = B.n;
-    if (ev) TSG_HIP(hipEventRecord(ev[0], s));
-    int2 *ebnd = nullptr;
-    long long *E = nullptr;
-    int *lists = nullptr, *cls = nullptr;
-    TSG_TRY(cx.get(&ebnd, (size_t)A.nnz + 1));
-    TSG_TRY(cx.get(&E, (size_t)A.nnz + 1));
-    TSG_TRY(cx.get(&lists, (size_t)NCLS * (m > 0 ? m : 1)));
-    long long *soff = nullptr;
-    TSG_TRY(cx.get(&soff, (size_t)m + 1));
-    TSG_TRY(cx.get(&cls, 12));  // 6 class counts, then 2 u64 statistics
-    unsigned long long *hst = reinterpret_cast<unsigned long long *>(cls + 8);
-    TSG_TRY(cx.get(&C.rowpointer, (size_t)m + 1));
-    TSG_HIP(hipMemsetAsync(cls, 0, 12 * sizeof(int), s));
-    k_rows_entries<<<grid_for((long)A.nnz + 1, WG, 16384), WG, 0, s>>>(A.columnindex, A.nnz, B.rowpointer, ebnd, E);
-    TSG_HIP(hipGetLastError());
-    TSG_TRY(scan_exclusive_i64(cx, E, (long)A.nnz + 1, s));
-    if (m > 0) k_rows_bin<<<(m + BIN_ROWS - 1) / BIN_ROWS, WG, 0, s>>>(A.rowpointer, m, E, C.rowpointer, lists, cls, soff, hst);
-    TSG_HIP(hipGetLastError());
-    TSG_HIP(hipMemcpyAsync(cx.pinned64, E + A.nnz, sizeof(long long), hipMemcpyDeviceToHost, s));
-    TSG_HIP(hipMemcpyAsync(cx.pinned64 + 1, cls, 12 * sizeof(int), hipMemcpyDeviceToHost, s));
-    TSG_HIP(hipStreamSynchronize(s));
-    const long long products = cx.pinned64[0];
+    C.rowpointer = p.rowpointer;
+    p.rowpointer = nullptr;  // (now C's)
+    int2 *ebnd = p.ebnd;
+    long long *E = p.E, *soff = p.soff;
+    int *lists = p.lists;
+    const long long products = p.products;
     int ncls[NCLS];
-    for (int t = 0; t < NCLS; ++t) ncls[t] = reinterpret_cast<const int *>(cx.pinned64 + 1)[t];
-    const long long hprod = cx.pinned64[5], pmax = cx.pinned64[6];
-    // routing: the path is built for rows of modest length (class H a minority
-    // of the work); hub-dominated products (R-MAT, mawi) go back to the caller
-    if (!force && (hprod * 4 > products || pmax > kRowsMaxRowProducts)) {
-        *declined = true;
-        cx.put(ebnd);
-        cx.put(E);
-        cx.put(lists);
-        cx.put(soff);
-        cx.put(cls);
-        cx.put(C.rowpointer);
-        C = tsg_dev_csr{};
-        return TSG_OK;
-    }
+    for (int t = 0; t < NCLS; ++t) ncls[t] = p.ncls[t];
     int *Scol = nullptr;
     double *Sval = nullptr;
     TSG_TRY(cx.get(&Scol, (size_t)products + 1));
@@ -862,7 +879,7 @@ int dev_spgemm_rows(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, tsg
         static unsigned long long raw[3 * 256 * 8];
         unsigned long long pr[24] = {};
         TSG_HIP(hipMemcpyAsync(raw, dprof, sizeof(raw), hipMemcpyDeviceToHost, s));
-        TSG_HIP(hipStreamSynchronize(s));
+        TSG_TRY(stream_wait(s));
         for (int c = 0; c < 3; ++c)
             for (int b = 0; b < 256; ++b)
                 for (int k = 0; k < 8; ++k) pr[c * 8 + k] += raw[(c * 256 + b) * 8 + k];
@@ -875,31 +892,37 @@ int dev_spgemm_rows(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, tsg
         }
     }
 #endif
+    // row counts -> row pointers -> the compaction, with no host round trip:
+    // nnz(C) <= products, so when the products fit int32 the result arrays are
+    // sized by them and nnz(C) comes back with the call's final synchronisation
     long long nnz = 0;
     TSG_HIP(hipMemsetAsync(C.rowpointer + m, 0, sizeof(int), s));
-    TSG_TRY(scan_exclusive_i32_total(cx, C.rowpointer, (long)m + 1, s, &nnz));
-    if (nnz > 0x7fffffffLL) return TSG_ERR_OVERFLOW;
-    C.nnz = (int)nnz;
-    TSG_TRY(cx.get(&C.columnindex, (size_t)nnz + 1));
-    TSG_TRY(cx.get(&C.value, (size_t)nnz + 1));
-    if (nnz > 0) {
-        const int nch = (int)((nnz + CP_CH - 1) / CP_CH);
-        int *cfirst = nullptr;
+    const bool small = products <= 0x7fffffffLL;
+    if (small) {
+        TSG_TRY(scan_exclusive_i32(cx, C.rowpointer, (long)m + 1, s));
+    } else {  // past int32 products: the checked scan (nnz(C) past int32 fails)
+        TSG_TRY(scan_exclusive_i32_total(cx, C.rowpointer, (long)m + 1, s, &nnz));
+        if (nnz > 0x7fffffffLL) return TSG_ERR_OVERFLOW;
+    }
+    const long long cap = small ? products : nnz;
+    TSG_TRY(cx.get(&C.columnindex, (size_t)cap + 1));
+    TSG_TRY(cx.get(&C.value, (size_t)cap + 1));
+    int *cfirst = nullptr;
+    if (cap > 0) {
+        const int nch = (int)((cap + CP_CH - 1) / CP_CH);
         TSG_TRY(cx.get(&cfirst, (size_t)nch + 1));
         k_rows_cfirst<<<grid_for(m, WG, 8192), WG, 0, s>>>(m, C.rowpointer, cfirst);
         TSG_HIP(hipGetLastError());
-        k_rows_compact<<<nch, WG, 0, s>>>(m, (int)nnz, cfirst, soff, C.rowpointer, Scol, Sval, C.columnindex,
-                                          C.value);
-        cx.put(cfirst);
+        k_rows_compact<<<nch, WG, 0, s>>>(m, cfirst, soff, C.rowpointer, Scol, Sval, C.columnindex, C.value);
     }
     TSG_HIP(hipGetLastError());
+    if (small) TSG_HIP(hipMemcpyAsync(cx.pinned64 + 7, C.rowpointer + m, sizeof(int), hipMemcpyDeviceToHost, s));
     if (ev) TSG_HIP(hipEventRecord(ev[3], s));
-    TSG_HIP(hipStreamSynchronize(s));
-    cx.put(ebnd);
-    cx.put(E);
-    cx.put(lists);
-    cx.put(soff);
-    cx.put(cls);
+    TSG_TRY(stream_wait(s));
+    if (small) nnz = *reinterpret_cast<const int *>(cx.pinned64 + 7);
+    C.nnz = (int)nnz;
+    cx.put(cfirst);
+    dev_rows_release(cx, p);
     cx.put(Scol);
     cx.put(Sval);
     if (st) {
