@@ -367,7 +367,7 @@ def main():
     path_name = {0: "tiles", 1: "fused", 2: "band", 3: "rows"}.get(path_id, str(path_id))
     workload = f"{name} C=A{'*A^T' if aat else '^2'} fp64 (device CSR in -> device CSR out), path {path_name}"
     if path_id == 3:
-        kernel_desc = ("row-merge numeric phase (k_rows_small, k_rows_merge x4 classes, k_rows_bitmap on 4 streams): "
+        kernel_desc = ("row-merge numeric phase (k_rows_bitmap, k_rows_merge x4 classes, k_rows_small x2, in turn): "
                        "B_alg of SURVEY §8d / HIP-event phase time")
         traffic, traffic_src = pmc_traffic(["k_rows_small", "k_rows_merge", "k_rows_bitmap"], workload)
     else:

@@ -110,32 +110,9 @@ int stream_wait(hipStream_t s) {
     return TSG_OK;
 }
 
-int Context::aux_fork(hipStream_t s) {
-    if (!aux[0]) {
-        for (int i = 0; i < kAux; ++i) TSG_HIP(hipStreamCreateWithFlags(&aux[i], hipStreamNonBlocking));
-        for (auto &e : aux_ev) TSG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    }
-    TSG_HIP(hipEventRecord(aux_ev[kAux], s));
-    for (int i = 0; i < kAux; ++i) TSG_HIP(hipStreamWaitEvent(aux[i], aux_ev[kAux], 0));
-    return TSG_OK;
-}
-
-int Context::aux_join(hipStream_t s) {
-    for (int i = 0; i < kAux; ++i) {
-        TSG_HIP(hipEventRecord(aux_ev[i], aux[i]));
-        TSG_HIP(hipStreamWaitEvent(s, aux_ev[i], 0));
-    }
-    return TSG_OK;
-}
-
 void Context::destroy() {
     (void)hipSetDevice(device);
     (void)hipDeviceSynchronize();
-    if (aux[0]) {
-        for (auto &a : aux) (void)hipStreamDestroy(a);
-        for (auto &e : aux_ev) (void)hipEventDestroy(e);
-        for (auto &a : aux) a = nullptr;
-    }
     pool.release_all_live();
     pool.trim();
     if (pinned) (void)hipHostFree(pinned);

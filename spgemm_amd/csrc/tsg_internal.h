@@ -60,13 +60,6 @@ struct Context {
     long long *pinned64 = nullptr;
     hipEvent_t ev[16];
     bool ev_ready = false;
-    // side streams for independent kernels of one call (fork from / join back to
-    // the call's stream; created on first use)
-    static constexpr int kAux = 4;
-    hipStream_t aux[kAux] = {};
-    hipEvent_t aux_ev[kAux + 1] = {};
-    int aux_fork(hipStream_t s);  // the side streams wait for s's work so far
-    int aux_join(hipStream_t s);  // s waits for the side streams' work so far
     std::vector<void *> owned;    // outputs handed to the caller (released on reset)
     int init(int dev);
     void destroy();

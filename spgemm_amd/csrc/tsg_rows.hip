@@ -852,10 +852,11 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
     TSG_HIP(hipMemsetAsync(dprof, 0, sizeof(unsigned long long) * 3 * 256 * 8, s));
 #endif
     RowsArgs g{A.rowpointer, A.value, ebnd, E, B.columnindex, B.value, nullptr, 0, C.rowpointer, Scol, Sval};
-    // class H first, alone: its workgroups take a whole CU's LDS and would
-    // starve behind the short rows' workgroups; then the other classes, each on
-    // a stream of its own so that their tails overlap (4 streams: the hardware
-    // queues a process gets)
+    // the classes in turn on the call's stream, heaviest first: class H alone
+    // (its workgroups take a whole CU's LDS and starved behind the short rows'
+    // workgroups when launched beside them), then M4 .. S16.  (The classes on
+    // four streams, forked and joined, measured the same: the phase is bound by
+    // the resident waves' latency chains, and the join cost ~26 us.)
     auto launch = [&](int c, auto kern, int grid, int nt, hipStream_t st) -> int {
         if (ncls[c] == 0) return TSG_OK;
         g.list = lists + (long)c * m;
@@ -865,14 +866,12 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
         return TSG_OK;
     };
     TSG_TRY(launch(6, k_rows_bitmap, ncls[6], RH_NT, s));
-    TSG_TRY(cx.aux_fork(s));
-    TSG_TRY(launch(5, k_rows_merge<M4_NT, M4_CAP, M4_RUNS>, ncls[5], M4_NT, cx.aux[0]));
-    TSG_TRY(launch(4, k_rows_merge<M3_NT, M3_CAP, M3_RUNS>, ncls[4], M3_NT, cx.aux[1]));
-    TSG_TRY(launch(3, k_rows_merge<M2_NT, M2_CAP, M2_RUNS>, ncls[3], M2_NT, cx.aux[2]));
+    TSG_TRY(launch(5, k_rows_merge<M4_NT, M4_CAP, M4_RUNS>, ncls[5], M4_NT, s));
+    TSG_TRY(launch(4, k_rows_merge<M3_NT, M3_CAP, M3_RUNS>, ncls[4], M3_NT, s));
+    TSG_TRY(launch(3, k_rows_merge<M2_NT, M2_CAP, M2_RUNS>, ncls[3], M2_NT, s));
     TSG_TRY(launch(2, k_rows_merge<M1_NT, M1_CAP, M1_RUNS>, ncls[2], M1_NT, s));
     TSG_TRY(launch(1, k_rows_small<64>, (ncls[1] + WAVES - 1) / WAVES, WG, s));
     TSG_TRY(launch(0, k_rows_small<16>, (ncls[0] + 4 * WAVES - 1) / (4 * WAVES), WG, s));
-    TSG_TRY(cx.aux_join(s));
     if (ev) TSG_HIP(hipEventRecord(ev[5], s));
 #ifdef TSG_ROWS_PROF
     {
