@@ -30,7 +30,7 @@ def _csr(m, n, rows):
     return m, n, rp, ci, vv
 
 
-def _check(A_, B_=None, aat=False, real=False, seed=0):
+def _check(A_, B_=None, aat=False, real=False, seed=0, path=None):
     m, n, rp, ci, vv = A_
     if real:
         vv = np.random.default_rng(seed).uniform(-1, 1, len(ci))
@@ -58,7 +58,10 @@ def _check(A_, B_=None, aat=False, real=False, seed=0):
     else:
         np.testing.assert_allclose(got[4], ref[4], rtol=1e-10, atol=0)
     assert st["nnzC"] == len(ref[3])
-    assert st["path"] == T.PATH_ROWS and st["numblkC"] == -1 and st["numtileA"] == -1
+    if path is None:
+        assert st["path"] == T.PATH_ROWS and st["numblkC"] == -1 and st["numtileA"] == -1
+    else:
+        assert st["path"] == path
     return st
 
 
@@ -169,3 +172,40 @@ def test_rows_aat_lj_prefix():
     r = 20000
     e = int(rp[r])
     _check((r, n, rp[:r + 1].copy(), ci[:e].copy(), vv[:e].copy()), aat=True)
+
+
+def test_default_routing_declines_hub_dominated(monkeypatch):
+    """A product whose longest row passes kRowsMaxRowProducts (65,536) is
+    declined by the row-merge setup and runs on the staged tile pipeline."""
+    monkeypatch.delenv("TSG_PATH", raising=False)
+    n, nb = 300, 100_000
+    rng = np.random.default_rng(21)
+    # row 0 names every B row (300 runs of 300 columns spread over 100,000:
+    # 90,000 products, no band window); 40 short rows
+    rows = [np.arange(n)] + [np.array([i % n, (7 * i) % n]) for i in range(1, 41)]
+    A = _csr(41, n, [np.unique(r) for r in rows])
+    B = _csr(n, nb, [np.sort(rng.choice(nb, size=300, replace=False)) for _ in range(n)])
+    m, _, rp, ci, vv = A
+    Am = T.Matrix.from_csr(41, n, rp, ci, vv)
+    Bm = T.Matrix.from_csr(n, nb, B[2], B[3], B[4])
+    Cm, st = T.spgemm(Am, Bm)
+    ref = O.gustavson(O.OMat.from_csr(41, n, rp, ci, vv), O.OMat.from_csr(n, nb, B[2], B[3], B[4])).csr()
+    got = Cm.csr()
+    np.testing.assert_array_equal(got[2], ref[2])
+    np.testing.assert_array_equal(got[3], ref[3])
+    np.testing.assert_allclose(got[4], ref[4], rtol=1e-10, atol=0)
+    assert st["path"] == T.PATH_TILES
+
+
+def test_default_routing_fused_by_longest_row(monkeypatch):
+    """The fused path is chosen by the longest C row's element products (the
+    setup's statistic), not by longest A row x longest B row: a 100-entry A row
+    over 1-entry B rows, beside a 40-entry B row that no long A row selects."""
+    monkeypatch.delenv("TSG_PATH", raising=False)
+    n = 200
+    brows = [np.array([(3 * j) % n]) for j in range(n)]
+    brows[150] = np.arange(40)  # long B row, selected only by short A rows
+    B = _csr(n, n, [np.unique(r) for r in brows])
+    arows = [np.arange(100)] + [np.array([150, (i * 11) % 100]) for i in range(1, 60)]
+    A = _csr(60, n, [np.unique(r) for r in arows])
+    st = _check(A, B, real=True, seed=13, path=T.PATH_FUSED)
