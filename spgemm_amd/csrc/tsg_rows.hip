@@ -39,11 +39,12 @@ constexpr int S16_MAX = 16;           // class S16: products (and runs) per row,
 constexpr int RS_MAX = 64;            // class S64: products (and runs) per row, a wave
 // merge classes M1..M4: products and runs per row, threads per row -- each
 // sized so its LDS (16 B per product + 16 B per run) keeps several rows per CU
+constexpr int M0_CAP = 256, M0_RUNS = 64, M0_NT = 64;      // 5 KB: one wave per row
 constexpr int M1_CAP = 512, M1_RUNS = 128, M1_NT = 128;    // 10 KB
 constexpr int M2_CAP = 1024, M2_RUNS = 256, M2_NT = 256;   // 20 KB
 constexpr int M3_CAP = 2048, M3_RUNS = 512, M3_NT = 512;   // 40 KB
 constexpr int M4_CAP = 4096, M4_RUNS = 512, M4_NT = 1024;  // 72 KB
-constexpr int NCLS = 7;               // S16, S64, M1..M4, H
+constexpr int NCLS = 8;               // S16, S64, M0..M4, H
 constexpr int BIN_ROWS = 2048;        // rows per workgroup of the binning kernel
 constexpr int RH_NT = 1024;           // class H: workgroup
 constexpr int RH_WORDS = 16384;       // class H: bitmap words (u64) per window: 128 KB of LDS
@@ -120,11 +121,12 @@ __device__ __forceinline__ int row_class(const int *rpA, const long long *E, int
     if (P == 0) return -1;
     if (P <= S16_MAX && k <= S16_MAX) return 0;
     if (P <= RS_MAX && k <= RS_MAX) return 1;
-    if (P <= M1_CAP && k <= M1_RUNS) return 2;
-    if (P <= M2_CAP && k <= M2_RUNS) return 3;
-    if (P <= M3_CAP && k <= M3_RUNS) return 4;
-    if (P <= M4_CAP && k <= M4_RUNS) return 5;
-    return 6;
+    if (P <= M0_CAP && k <= M0_RUNS) return 2;
+    if (P <= M1_CAP && k <= M1_RUNS) return 3;
+    if (P <= M2_CAP && k <= M2_RUNS) return 4;
+    if (P <= M3_CAP && k <= M3_RUNS) return 5;
+    if (P <= M4_CAP && k <= M4_RUNS) return 6;
+    return 7;
 }
 
 // rows -> classes: lists (class c's rows from lists + c*m) and counts cls[0..NCLS);
@@ -321,8 +323,8 @@ template <int NT, int CAP, int RUNS>
 __global__ __launch_bounds__(NT) void k_rows_merge(RowsArgs g) {
     constexpr int NW = NT / 64;
     constexpr int IPM = (CAP + NT - 1) / NT | 1;
-    constexpr int IB = CAP == 512 ? 9 : CAP == 1024 ? 10 : CAP == 2048 ? 11 : 12;  // position bits
-    static_assert((1 << IB) == CAP, "CAP: a power of two in [512, 4096]");
+    constexpr int IB = CAP == 256 ? 8 : CAP == 512 ? 9 : CAP == 1024 ? 10 : CAP == 2048 ? 11 : 12;  // position bits
+    static_assert((1 << IB) == CAP, "CAP: a power of two in [256, 4096]");
     // kp[0][0] K0 | kp[0][1] X | kp[1][0] K1 | kp[1][1] PY.  Packed: keys ping-pong
     // K0 <-> K1, PY holds the payloads, and the values go to K0+X or X+K1 (the
     // free pair next to the final keys).  Unpacked: [buffer][keys | payloads].
@@ -534,7 +536,7 @@ __global__ __launch_bounds__(NT) void k_rows_merge(RowsArgs g) {
         }
     }
     RP(4);
-    RP_DONE(CAP == M1_CAP ? 2 : 1);  // (M1 | M2..M4)
+    RP_DONE(CAP <= M1_CAP ? 2 : 1);  // (M0, M1 | M2..M4)
 }
 
 // ---- class H: a workgroup per row; windows of RH_SPAN columns, each a bitmap
@@ -865,11 +867,12 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
         TSG_HIP(hipGetLastError());
         return TSG_OK;
     };
-    TSG_TRY(launch(6, k_rows_bitmap, ncls[6], RH_NT, s));
-    TSG_TRY(launch(5, k_rows_merge<M4_NT, M4_CAP, M4_RUNS>, ncls[5], M4_NT, s));
-    TSG_TRY(launch(4, k_rows_merge<M3_NT, M3_CAP, M3_RUNS>, ncls[4], M3_NT, s));
-    TSG_TRY(launch(3, k_rows_merge<M2_NT, M2_CAP, M2_RUNS>, ncls[3], M2_NT, s));
-    TSG_TRY(launch(2, k_rows_merge<M1_NT, M1_CAP, M1_RUNS>, ncls[2], M1_NT, s));
+    TSG_TRY(launch(7, k_rows_bitmap, ncls[7], RH_NT, s));
+    TSG_TRY(launch(6, k_rows_merge<M4_NT, M4_CAP, M4_RUNS>, ncls[6], M4_NT, s));
+    TSG_TRY(launch(5, k_rows_merge<M3_NT, M3_CAP, M3_RUNS>, ncls[5], M3_NT, s));
+    TSG_TRY(launch(4, k_rows_merge<M2_NT, M2_CAP, M2_RUNS>, ncls[4], M2_NT, s));
+    TSG_TRY(launch(3, k_rows_merge<M1_NT, M1_CAP, M1_RUNS>, ncls[3], M1_NT, s));
+    TSG_TRY(launch(2, k_rows_merge<M0_NT, M0_CAP, M0_RUNS>, ncls[2], M0_NT, s));
     TSG_TRY(launch(1, k_rows_small<64>, (ncls[1] + WAVES - 1) / WAVES, WG, s));
     TSG_TRY(launch(0, k_rows_small<16>, (ncls[0] + 4 * WAVES - 1) / (4 * WAVES), WG, s));
     if (ev) TSG_HIP(hipEventRecord(ev[5], s));
@@ -882,9 +885,9 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
         for (int c = 0; c < 3; ++c)
             for (int b = 0; b < 256; ++b)
                 for (int k = 0; k < 8; ++k) pr[c * 8 + k] += raw[(c * 256 + b) * 8 + k];
-        static const char *nm[3] = {"H", "M2-M4", "M1"};
+        static const char *nm[3] = {"H", "M2-M4", "M0-M1"};
         for (int c = 0; c < 3; ++c) {
-            const int cnt = c == 0 ? ncls[6] : c == 1 ? ncls[3] + ncls[4] + ncls[5] : ncls[2];
+            const int cnt = c == 0 ? ncls[7] : c == 1 ? ncls[4] + ncls[5] + ncls[6] : ncls[2] + ncls[3];
             fprintf(stderr, "rows %s (%d rows) us/row:", nm[c], cnt);
             for (int k = 0; k < 6; ++k) fprintf(stderr, " %.2f", cnt ? pr[c * 8 + k] / 100.0 / cnt : 0.0);
             fprintf(stderr, "\n");

@@ -1,7 +1,7 @@
 """The row-merge path (spgemm_amd/csrc/tsg_rows.hip): rows binned by element
-products into seven classes -- S16 / S64 (<= 16 / 64 products: ranks by
-counting in 16 or 64 lanes), M1..M4
-(<= 512 / 1,024 / 2,048 / 4,096 products: pairwise merge-path merges of the
+products into eight classes -- S16 / S64 (<= 16 / 64 products: ranks by
+counting in 16 or 64 lanes), M0..M4
+(<= 256 / 512 / 1,024 / 2,048 / 4,096 products: pairwise merge-path merges of the
 runs in LDS) and H (longer rows or more runs: an LDS column bitmap per window
 of 524,288 columns, f64 atomics for the values).  TSG_PATH=rows forces it.  Pattern
 bit-exact, values within 1e-10 relative, against the oracle (the reference's
@@ -66,7 +66,7 @@ def _check(A_, B_=None, aat=False, real=False, seed=0, path=None):
 
 
 # (products, runs) caps of the classes S16, S64, M1..M4; longer rows are class H
-CAPS = [(16, 16), (64, 64), (512, 128), (1024, 256), (2048, 512), (4096, 512)]
+CAPS = [(16, 16), (64, 64), (256, 64), (512, 128), (1024, 256), (2048, 512), (4096, 512)]
 H = len(CAPS)
 M3, M4 = H - 2, H - 1
 
