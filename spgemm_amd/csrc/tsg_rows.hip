@@ -114,10 +114,7 @@ __global__ __launch_bounds__(WG) void k_rows_entries(const int *ciA, long nnzA, 
     }
 }
 
-__device__ __forceinline__ int row_class(const int *rpA, const long long *E, int r, long long *soff = nullptr) {
-    const int a0 = rpA[r], a1 = rpA[r + 1], k = a1 - a0;
-    const long long e0 = E[a0], P = E[a1] - e0;
-    if (soff) soff[r] = e0;
+__device__ __forceinline__ int row_class(long long P, int k) {
     if (P == 0) return -1;
     if (P <= S16_MAX && k <= S16_MAX) return 0;
     if (P <= RS_MAX && k <= RS_MAX) return 1;
@@ -139,16 +136,36 @@ __global__ __launch_bounds__(WG) void k_rows_bin(const int *rpA, int m, const lo
     __shared__ int wc[NCLS][WAVES];
     __shared__ int gb[NCLS];
     __shared__ long long red64[WAVES];
+    __shared__ signed char rc[BIN_ROWS];  // each row's class, for the second sweep
     const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
     const int r0 = blockIdx.x * BIN_ROWS, r1 = min(m, r0 + BIN_ROWS);
     int n[NCLS] = {};
     long long hp = 0, pmax = 0;
-    for (int r = r0 + tid; r < r1; r += WG) {
-        const int c = row_class(rpA, E, r, soff);  // (+ the row's staging offset)
+    constexpr int RPT = BIN_ROWS / WG;  // rows per thread: every load of a sweep issued together
+    int ra0[RPT], ra1[RPT];
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+        const int r = r0 + u * WG + tid;
+        ra0[u] = r < r1 ? rpA[r] : 0;
+        ra1[u] = r < r1 ? rpA[r + 1] : 0;
+    }
+    long long e0[RPT], e1[RPT];
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+        e0[u] = E[ra0[u]];
+        e1[u] = E[ra1[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+        const int r = r0 + u * WG + tid;
+        if (r >= r1) continue;
+        const long long P = e1[u] - e0[u];
+        const int c = row_class(P, ra1[u] - ra0[u]);
+        soff[r] = e0[u];  // the row's staging offset
+        rc[r - r0] = (signed char)c;
         if (c < 0) rnnz[r] = 0;
 #pragma unroll
         for (int t = 0; t < NCLS; ++t) n[t] += c == t;
-        const long long P = E[rpA[r + 1]] - soff[r];
         hp += c == NCLS - 1 ? P : 0;
         pmax = max(pmax, P);
     }
@@ -179,7 +196,7 @@ __global__ __launch_bounds__(WG) void k_rows_bin(const int *rpA, int m, const lo
     for (int t = 0; t < NCLS; ++t) run[t] = gb[t];
     for (int rb = r0; rb < r1; rb += WG) {
         const int r = rb + tid;
-        const int c = r < r1 ? row_class(rpA, E, r) : -1;
+        const int c = r < r1 ? rc[r - r0] : -1;
         u64 bt[NCLS];
 #pragma unroll
         for (int t = 0; t < NCLS; ++t) {
