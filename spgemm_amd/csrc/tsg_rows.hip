@@ -30,6 +30,7 @@
 #include "tsg_dev_common.h"
 
 #include <cstdio>
+#include <cstdlib>
 
 namespace tsg {
 
@@ -219,6 +220,44 @@ __global__ __launch_bounds__(WG) void k_rows_bin(const int *rpA, int m, const lo
     }
 }
 
+// class H's rows longest first (products in buckets of 1,024, a counting sort
+// in one workgroup): the dispatch order is the list order, and a long row
+// started last set the class's tail (row order: ~30 % over the longest-first
+// makespan on webbase).  Past OH_MAX rows the list keeps row order.
+constexpr int OH_NT = 1024, OH_PER = 8, OH_MAX = OH_NT * OH_PER, OH_NB = 64;
+__global__ __launch_bounds__(OH_NT) void k_rows_order_h(const int *rpA, const long long *E, const int *cls,
+                                                        int *list) {
+    __shared__ int cnt[OH_NB];
+    const int tid = threadIdx.x;
+    const int n = cls[NCLS - 1];
+    if (n < 2 || n > OH_MAX) return;  // (workgroup-uniform)
+    if (tid < OH_NB) cnt[tid] = 0;
+    __syncthreads();
+    int r[OH_PER], b[OH_PER];
+#pragma unroll
+    for (int u = 0; u < OH_PER; ++u) {
+        const int i = u * OH_NT + tid;
+        r[u] = i < n ? list[i] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < OH_PER; ++u)
+        if (r[u] >= 0) {
+            const long long P = E[rpA[r[u] + 1]] - E[rpA[r[u]]];
+            b[u] = OH_NB - 1 - (int)min((long long)OH_NB - 1, P >> 10);  // longest first
+            atomicAdd(&cnt[b[u]], 1);
+        }
+    __syncthreads();
+    if (tid < 64) {
+        const int v = cnt[tid];
+        const int inc = wave_incl_scan_dpp(v);
+        cnt[tid] = inc - v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < OH_PER; ++u)
+        if (r[u] >= 0) list[atomicAdd(&cnt[b[u]], 1)] = r[u];
+}
+
 // ---- classes S16 / S64: G lanes per row (64/G rows per wave), the products
 // one per lane, ranks by counting the group's smaller (column, lane) keys
 template <int G>
@@ -323,6 +362,50 @@ __device__ __forceinline__ void search_ilp(const T *a, int (&b)[U], int (&len)[U
     }
 }
 
+// lane l's value of lane l ^ D (D a power of two below 64): DPP quad
+// permutes for 1 and 2, ds_swizzle's xor mode inside 32 lanes, ds_bpermute for 32
+template <int D> __device__ __forceinline__ u32 lane_xor(u32 v) {
+    if constexpr (D == 1) return (u32)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false);  // [1,0,3,2]
+    else if constexpr (D == 2) return (u32)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false);  // [2,3,0,1]
+    else if constexpr (D < 32) return (u32)__builtin_amdgcn_ds_swizzle((int)v, (D << 10) | 0x1f);
+    else return (u32)__shfl_xor((int)v, D, 64);
+}
+
+// one bitonic stage at element distance J inside sequences of K (elements
+// e = 4*lane + u): ascending where e & K == 0
+template <int K, int J> __device__ __forceinline__ void bitonic_stage(u32 (&x)[4], int lane) {
+    if constexpr (J >= 4) {
+        constexpr int D = J / 4;
+        const bool asc = K >= 256 || (lane & (K / 4)) == 0;
+        const bool keep_min = asc == ((lane & D) == 0);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const u32 y = lane_xor<D>(x[u]);
+            x[u] = keep_min ? min(x[u], y) : max(x[u], y);
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if ((u & J) == 0) {
+                const bool asc = K < 4 ? (u & K) == 0 : (K >= 256 || (lane & (K / 4)) == 0);
+                const u32 lo = min(x[u], x[u + J]), hi = max(x[u], x[u + J]);
+                x[u] = asc ? lo : hi;
+                x[u + J] = asc ? hi : lo;
+            }
+    }
+}
+template <int K, int J> __device__ __forceinline__ void bitonic_merge(u32 (&x)[4], int lane) {
+    bitonic_stage<K, J>(x, lane);
+    if constexpr (J > 1) bitonic_merge<K, J / 2>(x, lane);
+}
+template <int K> __device__ __forceinline__ void bitonic_sort(u32 (&x)[4], int lane) {
+    if constexpr (K > 2) bitonic_sort<K / 2>(x, lane);
+    bitonic_merge<K, K / 2>(x, lane);
+}
+// a wave's 256 keys ascending in registers, lane l holding elements 4l..4l+3
+// (36 compare-exchange stages, 21 of them across lanes; no LDS, no barrier)
+__device__ __forceinline__ void wave_sort256(u32 (&x)[4], int lane) { bitonic_sort<256>(x, lane); }
+
 // ---- classes M1..M4: pairwise stable merges of the row's runs in LDS.  NT
 // threads per row, at most CAP products and RUNS runs.  Thread t owns the
 // positions [t*ipt, t*ipt + ipt) of every pass (ipt odd, so the lanes' LDS
@@ -345,8 +428,9 @@ __global__ __launch_bounds__(NT) void k_rows_merge(RowsArgs g) {
     // kp[0][0] K0 | kp[0][1] X | kp[1][0] K1 | kp[1][1] PY.  Packed: keys ping-pong
     // K0 <-> K1, PY holds the payloads, and the values go to K0+X or X+K1 (the
     // free pair next to the final keys).  Unpacked: [buffer][keys | payloads].
-    __shared__ u32 kp[2][2][CAP];
+    __shared__ __align__(16) u32 kp[2][2][CAP];
     __shared__ int roff[RUNS + 1];
+    __shared__ int sbd[CAP / 256 + 1];  // packed: the sorted segments' bounds
     __shared__ int rbs[RUNS];       // each run's B start
     __shared__ double rav[RUNS];    // each run's A value
     __shared__ int red[2 * NW];
@@ -388,46 +472,35 @@ __global__ __launch_bounds__(NT) void k_rows_merge(RowsArgs g) {
     if (tid == 0) roff[k] = P;
     __syncthreads();
     RP(0);
-    const int ipt = ((P + NT - 1) / NT) | 1;
-    const int q0 = min(P, tid * ipt), q1 = min(P, q0 + ipt), nq = q1 - q0;
-    // expansion: position q of run j at roff[j] + t -> column, payload (j, t)
-    int j0 = 0;  // the run holding q0 (pairs keep their position ranges every round)
-    int c[IPM];
-    u32 py[IPM];
+    // expansion: wave w takes positions [256w, 256w + 256), lane l the four at
+    // e0 = 256w + 4l (mostly one run's neighbours); position q of run j at
+    // roff[j] + t -> column, payload (j, t)
+    constexpr int SEG = 256;
+    static_assert(CAP == 4 * NT, "four positions per thread");
+    const int e0 = wv * SEG + 4 * lane, ne = max(0, min(4, P - e0));
+    int c[4];
+    u32 py[4];
     {
         int j = 0;
-        if (nq > 0) {  // the last run starting at or before q0
-            int lo = 0, len = k;
-            while (len > 0) {
-                const int half = len >> 1;
-                if (roff[lo + half] <= q0) {
-                    lo += half + 1;
-                    len -= half + 1;
-                } else {
-                    len = half;
-                }
-            }
-            j = lo - 1;
-            j0 = j;
-        }
-        int pa[IPM];
+        if (ne > 0) j = lower_bound_dev(roff, 0, k + 1, e0 + 1) - 1;  // the last run starting at or before e0
+        int pa[4];
 #pragma unroll
-        for (int u = 0; u < IPM; ++u)
-            if (u < nq) {
-                const int q = q0 + u;
+        for (int u = 0; u < 4; ++u)
+            if (u < ne) {
+                const int q = e0 + u;
                 while (roff[j + 1] <= q) ++j;
                 pa[u] = rbs[j] + q - roff[j];
                 py[u] = ((u32)j << 16) | (u32)(q - roff[j]);
             }
 #pragma unroll
-        for (int u = 0; u < IPM; ++u)
-            if (u < nq) c[u] = g.Bcol[pa[u]];
+        for (int u = 0; u < 4; ++u)
+            if (u < ne) c[u] = g.Bcol[pa[u]];
     }
     // the row's column span [clo, chi]
     int clo = INT_MAX, chi = -1;
 #pragma unroll
-    for (int u = 0; u < IPM; ++u)
-        if (u < nq) {
+    for (int u = 0; u < 4; ++u)
+        if (u < ne) {
             clo = min(clo, c[u]);
             chi = max(chi, c[u]);
         }
@@ -445,33 +518,53 @@ __global__ __launch_bounds__(NT) void k_rows_merge(RowsArgs g) {
         clo = min(clo, red[w]);
         chi = max(chi, red[NW + w]);
     }
-    const bool packed = (u32)(chi - clo) < (1u << (32 - IB));  // (workgroup-uniform)
+    // (strict: the largest packed key stays below the ~0u padding)
+    const bool packed = (u32)(chi - clo) < (1u << (32 - IB)) - 1u;  // (workgroup-uniform)
     u32 *const K0 = kp[0][0], *const X = kp[0][1], *const PY = kp[1][1];
+    if (packed) {
+        // each wave sorts its 256 positions in registers: the merge rounds
+        // start from sorted segments of 256 instead of the B rows' short runs
+        u32 x[4];
 #pragma unroll
-    for (int u = 0; u < IPM; ++u)
-        if (u < nq) {
-            const int q = q0 + u;
-            if (packed) {
-                K0[q] = ((u32)(c[u] - clo) << IB) | (u32)q;
-                PY[q] = py[u];
-            } else {
-                K0[q] = (u32)c[u];
-                X[q] = py[u];
-            }
+        for (int u = 0; u < 4; ++u) {
+            x[u] = u < ne ? ((u32)(c[u] - clo) << IB) | (u32)(e0 + u) : ~0u;
+            if (u < ne) PY[e0 + u] = py[u];
         }
+        if (wv * SEG < P) {  // (wave-uniform)
+            wave_sort256(x, lane);
+            *reinterpret_cast<uint4 *>(K0 + e0) = make_uint4(x[0], x[1], x[2], x[3]);
+        }
+        if (tid <= CAP / SEG) sbd[tid] = min(P, tid * SEG);
+    } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (u < ne) {
+                K0[e0 + u] = (u32)c[u];
+                X[e0 + u] = py[u];
+            }
+    }
     __syncthreads();
     RP(1);
+    // merge-path chunks: thread t owns [t*ipt, t*ipt + ipt) of every round
+    const int ipt = ((P + NT - 1) / NT) | 1;
+    const int q0 = min(P, tid * ipt), q1 = min(P, q0 + ipt), nq = q1 - q0;
+    // the sorted groups the rounds start from: packed -> the waves' segments,
+    // unpacked -> the runs
+    const int *const bd = packed ? sbd : roff;
+    const int nb = packed ? (P + SEG - 1) / SEG : k;
+    int j0 = 0;  // the group holding q0 (pairs keep their position ranges every round)
+    if (nq > 0) j0 = packed ? q0 / SEG : lower_bound_dev(roff, 0, k + 1, q0 + 1) - 1;
     // rounds: groups of 2^lw runs merged pairwise
     int src = 0;
-    for (int lw = 0; (1 << lw) < k; ++lw) {
+    for (int lw = 0; (1 << lw) < nb; ++lw) {
         const u32 *ik = kp[src][0], *ip = kp[src][1];
         u32 *ok = kp[src ^ 1][0], *op = kp[src ^ 1][1];
         int pr = j0 >> (lw + 1);  // the pair holding q0
         for (int q = q0; q < q1;) {
-            while (roff[min((pr + 1) << (lw + 1), k)] <= q) ++pr;  // (pairs ending at or before q)
-            const int ps = roff[pr << (lw + 1)];
-            const int pm = roff[min((2 * pr + 1) << lw, k)];
-            const int pe = roff[min((pr + 1) << (lw + 1), k)];
+            while (bd[min((pr + 1) << (lw + 1), nb)] <= q) ++pr;  // (pairs ending at or before q)
+            const int ps = bd[pr << (lw + 1)];
+            const int pm = bd[min((2 * pr + 1) << lw, nb)];
+            const int pe = bd[min((pr + 1) << (lw + 1), nb)];
             const int la = pm - ps, lb = pe - pm, qq = q - ps;
             int lo = max(0, qq - lb), hi = min(qq, la);
             while (lo < hi) {
@@ -884,6 +977,10 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
         TSG_HIP(hipGetLastError());
         return TSG_OK;
     };
+    if (ncls[7] >= 2 && ncls[7] <= OH_MAX && !getenv("TSG_ROWS_H_ROWORDER")) {
+        k_rows_order_h<<<1, OH_NT, 0, s>>>(A.rowpointer, E, p.cls, lists + (long)(NCLS - 1) * m);
+        TSG_HIP(hipGetLastError());
+    }
     TSG_TRY(launch(7, k_rows_bitmap, ncls[7], RH_NT, s));
     TSG_TRY(launch(6, k_rows_merge<M4_NT, M4_CAP, M4_RUNS>, ncls[6], M4_NT, s));
     TSG_TRY(launch(5, k_rows_merge<M3_NT, M3_CAP, M3_RUNS>, ncls[5], M3_NT, s));
