@@ -269,23 +269,34 @@ __global__ __launch_bounds__(WG) void k_rows_small(RowsArgs g) {
     const int i = (blockIdx.x * WAVES + wv) * RPW + lane / G;
     if ((blockIdx.x * WAVES + wv) * RPW >= g.nrows) return;  // wave-uniform
     const bool live = i < g.nrows;
-    int r = 0, a0 = 0, k = 0, P = 0;
+    int r = 0, a0 = 0, k = 0;
     long long base = 0;
     if (live) {
         r = g.list[i];
         a0 = g.rpA[r];
         k = g.rpA[r + 1] - a0;
-        base = g.E[a0];
-        P = (int)(g.E[a0 + k] - base);
+        base = g.E[a0];  // (the staging offset: not waited for until the output)
     }
-    // lane sl < k: run sl's offset in the row, B start and A value
-    int roff = INT_MAX, bs = 0;
+    // lane sl < k: run sl's B range and A value; the runs' offsets in the row
+    // by a scan of their lengths over the group
+    int2 be = make_int2(0, 0);
     double av = 0.0;
     if (sl < k) {
-        roff = (int)(g.E[a0 + sl] - base);
-        bs = g.ebnd[a0 + sl].x;
+        be = g.ebnd[a0 + sl];
         av = g.vA[a0 + sl];
     }
+    const int len = be.y - be.x, bs = be.x;
+    int inc = len;  // inclusive scan over the G lanes (DPP row shifts stay inside 16-lane rows)
+    inc += dpp_mov<0x111, 0xf>(0, inc);
+    inc += dpp_mov<0x112, 0xf>(0, inc);
+    inc += dpp_mov<0x114, 0xf>(0, inc);
+    inc += dpp_mov<0x118, 0xf>(0, inc);
+    if constexpr (G == 64) {
+        inc += dpp_mov<0x142, 0xa>(0, inc);  // row_bcast:15
+        inc += dpp_mov<0x143, 0xc>(0, inc);  // row_bcast:31
+    }
+    const int roff = sl < k ? inc - len : INT_MAX;
+    const int P = __shfl(inc, G - 1, G);
     // position sl: its run = the last run starting at or before it
     int run = 0;
     if constexpr (G == 64) {
@@ -438,35 +449,43 @@ __global__ __launch_bounds__(NT) void k_rows_merge(RowsArgs g) {
     const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
     const int r = g.list[blockIdx.x];
     const int a0 = g.rpA[r], ka = g.rpA[r + 1] - a0;
-    const long long base = g.E[a0];
-    const int P = (int)(g.E[a0 + ka] - base);
+    const long long base = g.E[a0];  // (the staging offset: not waited for until the output)
     // the runs with products, in order (entries selecting empty B rows dropped:
-    // fewer runs, fewer rounds)
-    int k = 0;
+    // fewer runs, fewer rounds); their offsets by a scan of the B row lengths,
+    // so the table needs only the entries' own loads
+    int k = 0, P = 0;
     for (int jb = 0; jb < ka; jb += NT) {  // (workgroup-uniform)
         const int j = jb + tid;
-        long long e0 = 0;
-        int len = 0;
+        int2 be = make_int2(0, 0);
+        double av = 0.0;
         if (j < ka) {
-            e0 = g.E[a0 + j];
-            len = (int)(g.E[a0 + j + 1] - e0);
+            be = g.ebnd[a0 + j];
+            av = g.vA[a0 + j];
         }
+        const int len = be.y - be.x;
         const u64 b = __ballot(len > 0);
-        if (lane == 0) red[wv] = __popcll(b);
+        const int inc = wave_incl_scan_dpp(len);
+        if (lane == 63) {
+            red[wv] = __popcll(b);
+            red[NW + wv] = inc;
+        }
         __syncthreads();
-        int off = k, tot = 0;
+        int off = k, tot = 0, loff = P, ltot = 0;
 #pragma unroll
         for (int w = 0; w < NW; ++w) {
             off += w < wv ? red[w] : 0;
             tot += red[w];
+            loff += w < wv ? red[NW + w] : 0;
+            ltot += red[NW + w];
         }
         if (len > 0) {
             const int d = off + lanes_below(b);
-            roff[d] = (int)(e0 - base);
-            rbs[d] = g.ebnd[a0 + j].x;
-            rav[d] = g.vA[a0 + j];
+            roff[d] = loff + inc - len;
+            rbs[d] = be.x;
+            rav[d] = av;
         }
         k += tot;
+        P += ltot;
         __syncthreads();
     }
     if (tid == 0) roff[k] = P;
