@@ -149,7 +149,7 @@ int dev_spgemm_band(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, Ban
 struct RowsPlan {
     int2 *ebnd = nullptr;      // per A entry: its B row's [start, end)
     long long *E = nullptr;    // per A entry: prefix of the element products
-    int *lists = nullptr;      // the classes' rows
+    int4 *lists = nullptr;     // the classes' rows: (row, its first A entry, its A entries, -)
     long long *soff = nullptr; // per row: staging offset
     int *cls = nullptr;        // class counts + statistics (device)
     int *rowpointer = nullptr; // C's row pointers (row counts until the scan)

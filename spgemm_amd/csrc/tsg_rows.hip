@@ -94,7 +94,7 @@ struct RowsArgs {
     const long long *E;    // per A entry: prefix of the element products (E[nnzA] = all)
     const int *Bcol;
     const double *Bval;
-    const int *list;       // the class's rows
+    const int4 *list;      // the class's rows: (row, first A entry, A entries, -)
     int nrows;
     int *rnnz;             // nnz of each row (the row pointers after a scan)
     int *Scol;             // staging: row r's nonzeros from E[rpA[r]]
@@ -132,7 +132,7 @@ __device__ __forceinline__ int row_class(long long P, int k) {
 // = the largest row's products (the routing statistics).  A workgroup per
 // BIN_ROWS rows: its counts first (one atomic per class), then its rows in
 // order into the reserved slots.
-__global__ __launch_bounds__(WG) void k_rows_bin(const int *rpA, int m, const long long *E, int *rnnz, int *lists,
+__global__ __launch_bounds__(WG) void k_rows_bin(const int *rpA, int m, const long long *E, int *rnnz, int4 *lists,
                                                  int *cls, long long *soff, unsigned long long *hst) {
     __shared__ int wc[NCLS][WAVES];
     __shared__ int gb[NCLS];
@@ -195,7 +195,10 @@ __global__ __launch_bounds__(WG) void k_rows_bin(const int *rpA, int m, const lo
     int run[NCLS];
 #pragma unroll
     for (int t = 0; t < NCLS; ++t) run[t] = gb[t];
-    for (int rb = r0; rb < r1; rb += WG) {
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+        const int rb = r0 + u * WG;
+        if (rb >= r1) break;  // (workgroup-uniform)
         const int r = rb + tid;
         const int c = r < r1 ? rc[r - r0] : -1;
         u64 bt[NCLS];
@@ -213,7 +216,7 @@ __global__ __launch_bounds__(WG) void k_rows_bin(const int *rpA, int m, const lo
                 pre += w < wv ? v : 0;
                 tot += v;
             }
-            if (c == t) lists[(long)t * m + run[t] + pre + lanes_below(bt[t])] = r;
+            if (c == t) lists[(long)t * m + run[t] + pre + lanes_below(bt[t])] = make_int4(r, ra0[u], ra1[u] - ra0[u], 0);
             run[t] += tot;
         }
         __syncthreads();
@@ -225,24 +228,24 @@ __global__ __launch_bounds__(WG) void k_rows_bin(const int *rpA, int m, const lo
 // started last set the class's tail (row order: ~30 % over the longest-first
 // makespan on webbase).  Past OH_MAX rows the list keeps row order.
 constexpr int OH_NT = 1024, OH_PER = 8, OH_MAX = OH_NT * OH_PER, OH_NB = 64;
-__global__ __launch_bounds__(OH_NT) void k_rows_order_h(const int *rpA, const long long *E, const int *cls,
-                                                        int *list) {
+__global__ __launch_bounds__(OH_NT) void k_rows_order_h(const long long *E, const int *cls, int4 *list) {
     __shared__ int cnt[OH_NB];
     const int tid = threadIdx.x;
     const int n = cls[NCLS - 1];
     if (n < 2 || n > OH_MAX) return;  // (workgroup-uniform)
     if (tid < OH_NB) cnt[tid] = 0;
     __syncthreads();
-    int r[OH_PER], b[OH_PER];
+    int4 r[OH_PER];
+    int b[OH_PER];
 #pragma unroll
     for (int u = 0; u < OH_PER; ++u) {
         const int i = u * OH_NT + tid;
-        r[u] = i < n ? list[i] : -1;
+        r[u] = i < n ? list[i] : make_int4(-1, 0, 0, 0);
     }
 #pragma unroll
     for (int u = 0; u < OH_PER; ++u)
-        if (r[u] >= 0) {
-            const long long P = E[rpA[r[u] + 1]] - E[rpA[r[u]]];
+        if (r[u].x >= 0) {
+            const long long P = E[r[u].y + r[u].z] - E[r[u].y];
             b[u] = OH_NB - 1 - (int)min((long long)OH_NB - 1, P >> 10);  // longest first
             atomicAdd(&cnt[b[u]], 1);
         }
@@ -255,7 +258,7 @@ __global__ __launch_bounds__(OH_NT) void k_rows_order_h(const int *rpA, const lo
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < OH_PER; ++u)
-        if (r[u] >= 0) list[atomicAdd(&cnt[b[u]], 1)] = r[u];
+        if (r[u].x >= 0) list[atomicAdd(&cnt[b[u]], 1)] = r[u];
 }
 
 // ---- classes S16 / S64: G lanes per row (64/G rows per wave), the products
@@ -272,9 +275,10 @@ __global__ __launch_bounds__(WG) void k_rows_small(RowsArgs g) {
     int r = 0, a0 = 0, k = 0;
     long long base = 0;
     if (live) {
-        r = g.list[i];
-        a0 = g.rpA[r];
-        k = g.rpA[r + 1] - a0;
+        const int4 e = g.list[i];
+        r = e.x;
+        a0 = e.y;
+        k = e.z;
         base = g.E[a0];  // (the staging offset: not waited for until the output)
     }
     // lane sl < k: run sl's B range and A value; the runs' offsets in the row
@@ -447,8 +451,8 @@ __global__ __launch_bounds__(NT) void k_rows_merge(RowsArgs g) {
     __shared__ int red[2 * NW];
     RP_INIT
     const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
-    const int r = g.list[blockIdx.x];
-    const int a0 = g.rpA[r], ka = g.rpA[r + 1] - a0;
+    const int4 le = g.list[blockIdx.x];
+    const int r = le.x, a0 = le.y, ka = le.z;
     const long long base = g.E[a0];  // (the staging offset: not waited for until the output)
     // the runs with products, in order (entries selecting empty B rows dropped:
     // fewer runs, fewer rounds); their offsets by a scan of the B row lengths,
@@ -765,8 +769,8 @@ __global__ __launch_bounds__(RH_NT) void k_rows_bitmap(RowsArgs g) {
     constexpr int NW = RH_NT / 64;
     RP_INIT
     const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
-    const int r = g.list[blockIdx.x];
-    const int a0 = g.rpA[r], k = g.rpA[r + 1] - a0;
+    const int4 le = g.list[blockIdx.x];
+    const int r = le.x, a0 = le.y, k = le.z;
     const long long base = g.E[a0];
     // the row's columns [lo, hi]
     int lo = INT_MAX, hi = -1;
@@ -967,7 +971,7 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
     p.rowpointer = nullptr;  // (now C's)
     int2 *ebnd = p.ebnd;
     long long *E = p.E, *soff = p.soff;
-    int *lists = p.lists;
+    int4 *lists = p.lists;
     const long long products = p.products;
     int ncls[NCLS];
     for (int t = 0; t < NCLS; ++t) ncls[t] = p.ncls[t];
@@ -997,7 +1001,7 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
         return TSG_OK;
     };
     if (ncls[7] >= 2 && ncls[7] <= OH_MAX && !getenv("TSG_ROWS_H_ROWORDER")) {
-        k_rows_order_h<<<1, OH_NT, 0, s>>>(A.rowpointer, E, p.cls, lists + (long)(NCLS - 1) * m);
+        k_rows_order_h<<<1, OH_NT, 0, s>>>(E, p.cls, lists + (long)(NCLS - 1) * m);
         TSG_HIP(hipGetLastError());
     }
     TSG_TRY(launch(7, k_rows_bitmap, ncls[7], RH_NT, s));

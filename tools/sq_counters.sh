@@ -15,6 +15,6 @@ for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
            "SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU" \
            "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum"; do
   n=$((n+1))
-  timeout -k 10 300 rocprofv3 --pmc $set --kernel-include-regex "k_step|k_eseg|k_esplit" --output-format csv \
+  timeout -k 10 300 rocprofv3 --pmc $set --kernel-include-regex "${KRE:-k_step|k_eseg|k_esplit}" --output-format csv \
     -d "$OUT/p$n" -o run -- "${BENCH[@]}" > "$OUT/p$n.log" 2>&1
 done

@@ -5,11 +5,11 @@
 set -e
 cd "$(dirname "$0")/.."
 while [ $# -ge 2 ]; do
-  touch spgemm_amd/csrc/tsg_device.hip
+  touch spgemm_amd/csrc/*.hip
   make -C spgemm_amd/csrc -j8 EXTRA="$2" > /dev/null
   cp spgemm_amd/lib/libtsg.so spgemm_amd/lib/libtsg_$1.so
   echo "built libtsg_$1.so ($2)"
   shift 2
 done
-touch spgemm_amd/csrc/tsg_device.hip
+touch spgemm_amd/csrc/*.hip
 make -C spgemm_amd/csrc -j8 > /dev/null
