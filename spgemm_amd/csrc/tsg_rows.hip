@@ -102,8 +102,10 @@ struct RowsArgs {
 };
 
 // per A entry: its B row's range and products (the latter scanned into E)
+// (also zeroes the binning kernel's counters: no separate memset in the stream)
 __global__ __launch_bounds__(WG) void k_rows_entries(const int *ciA, long nnzA, const int *rpB, int2 *ebnd,
-                                                     long long *E) {
+                                                     long long *E, int *cls) {
+    if (blockIdx.x == 0 && threadIdx.x < 14) cls[threadIdx.x] = 0;
     for (long a = (long)blockIdx.x * WG + threadIdx.x; a <= nnzA; a += (long)gridDim.x * WG) {
         if (a == nnzA) {
             E[a] = 0;
@@ -129,17 +131,24 @@ __device__ __forceinline__ int row_class(long long P, int k) {
 
 // rows -> classes: lists (class c's rows from lists + c*m) and counts cls[0..NCLS);
 // rows without products get nnz 0; hst[0] = the class-H rows' products, hst[1]
-// = the largest row's products (the routing statistics).  A workgroup per
+// = the largest row's products (the routing statistics), hst[2] = all products
+// (*Etot, copied so that one read-back brings everything); rnnz[m] = 0 (the
+// row pointers' n+1 slot).  A workgroup per
 // BIN_ROWS rows: its counts first (one atomic per class), then its rows in
 // order into the reserved slots.
-__global__ __launch_bounds__(WG) void k_rows_bin(const int *rpA, int m, const long long *E, int *rnnz, int4 *lists,
-                                                 int *cls, long long *soff, unsigned long long *hst) {
+__global__ __launch_bounds__(WG) void k_rows_bin(const int *rpA, int m, const long long *E, const long long *Etot,
+                                                 int *rnnz, int4 *lists, int *cls, long long *soff,
+                                                 unsigned long long *hst) {
     __shared__ int wc[NCLS][WAVES];
     __shared__ int gb[NCLS];
     __shared__ long long red64[WAVES];
     __shared__ signed char rc[BIN_ROWS];  // each row's class, for the second sweep
     const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
     const int r0 = blockIdx.x * BIN_ROWS, r1 = min(m, r0 + BIN_ROWS);
+    if (blockIdx.x == 0 && tid == 0) {
+        hst[2] = (unsigned long long)*Etot;
+        rnnz[m] = 0;
+    }
     int n[NCLS] = {};
     long long hp = 0, pmax = 0;
     constexpr int RPT = BIN_ROWS / WG;  // rows per thread: every load of a sweep issued together
@@ -916,7 +925,7 @@ __global__ __launch_bounds__(WG) void k_rows_compact(int m, const int *cfirst, c
 }
 
 // Setup (stream-ordered, no host round trip): the entry table, its scan and the
-// classes; the statistics land in cx.pinned64[0..6] once the stream is synced.
+// classes; counts and statistics land in cx.pinned64[0..7) once the stream is synced.
 int dev_rows_setup_async(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPlan &p, hipStream_t s) {
     static_assert(NCLS <= 8, "class counts in cls[0..8)");
     const int m = A.m;
@@ -925,28 +934,26 @@ int dev_rows_setup_async(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B
     TSG_TRY(cx.get(&p.E, (size_t)A.nnz + 1));
     TSG_TRY(cx.get(&p.lists, (size_t)NCLS * (m > 0 ? m : 1)));
     TSG_TRY(cx.get(&p.soff, (size_t)m + 1));
-    TSG_TRY(cx.get(&p.cls, 12));  // class counts, then 2 u64 statistics at [8..11]
+    TSG_TRY(cx.get(&p.cls, 14));  // class counts, then 3 u64 statistics at [8..13]
     TSG_TRY(cx.get(&p.rowpointer, (size_t)m + 1));
     unsigned long long *hst = reinterpret_cast<unsigned long long *>(p.cls + 8);
-    TSG_HIP(hipMemsetAsync(p.cls, 0, 12 * sizeof(int), s));
     k_rows_entries<<<grid_for((long)A.nnz + 1, WG, 16384), WG, 0, s>>>(A.columnindex, A.nnz, B.rowpointer, p.ebnd,
-                                                                      p.E);
+                                                                      p.E, p.cls);
     TSG_HIP(hipGetLastError());
     TSG_TRY(scan_exclusive_i64(cx, p.E, (long)A.nnz + 1, s));
-    if (m > 0)
-        k_rows_bin<<<(m + BIN_ROWS - 1) / BIN_ROWS, WG, 0, s>>>(A.rowpointer, m, p.E, p.rowpointer, p.lists, p.cls,
-                                                                p.soff, hst);
+    // (one workgroup at least: it writes the statistics and rowpointer[m])
+    k_rows_bin<<<max(1, (m + BIN_ROWS - 1) / BIN_ROWS), WG, 0, s>>>(A.rowpointer, m, p.E, p.E + A.nnz, p.rowpointer,
+                                                                    p.lists, p.cls, p.soff, hst);
     TSG_HIP(hipGetLastError());
-    TSG_HIP(hipMemcpyAsync(cx.pinned64, p.E + A.nnz, sizeof(long long), hipMemcpyDeviceToHost, s));
-    TSG_HIP(hipMemcpyAsync(cx.pinned64 + 1, p.cls, 12 * sizeof(int), hipMemcpyDeviceToHost, s));
+    TSG_HIP(hipMemcpyAsync(cx.pinned64, p.cls, 14 * sizeof(int), hipMemcpyDeviceToHost, s));
     return TSG_OK;
 }
 
 void dev_rows_setup_read(Context &cx, RowsPlan &p) {
-    p.products = cx.pinned64[0];
-    for (int t = 0; t < NCLS; ++t) p.ncls[t] = reinterpret_cast<const int *>(cx.pinned64 + 1)[t];
-    p.hprod = cx.pinned64[5];
-    p.pmax = cx.pinned64[6];
+    for (int t = 0; t < NCLS; ++t) p.ncls[t] = reinterpret_cast<const int *>(cx.pinned64)[t];
+    p.hprod = cx.pinned64[4];
+    p.pmax = cx.pinned64[5];
+    p.products = cx.pinned64[6];
 }
 
 // routing: the path is built for rows of modest length (class H a minority of
@@ -1034,8 +1041,7 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
     // row counts -> row pointers -> the compaction, with no host round trip:
     // nnz(C) <= products, so when the products fit int32 the result arrays are
     // sized by them and nnz(C) comes back with the call's final synchronisation
-    long long nnz = 0;
-    TSG_HIP(hipMemsetAsync(C.rowpointer + m, 0, sizeof(int), s));
+    long long nnz = 0;  // (C.rowpointer[m] = 0 from the binning kernel)
     const bool small = products <= 0x7fffffffLL;
     if (small) {
         TSG_TRY(scan_exclusive_i32(cx, C.rowpointer, (long)m + 1, s));
