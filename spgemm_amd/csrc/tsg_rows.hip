@@ -454,7 +454,6 @@ __global__ __launch_bounds__(NT) void k_rows_merge(RowsArgs g) {
     // free pair next to the final keys).  Unpacked: [buffer][keys | payloads].
     __shared__ __align__(16) u32 kp[2][2][CAP];
     __shared__ int roff[RUNS + 1];
-    __shared__ int sbd[CAP / 256 + 1];  // packed: the sorted segments' bounds
     __shared__ int rbs[RUNS];       // each run's B start
     __shared__ double rav[RUNS];    // each run's A value
     __shared__ int red[2 * NW];
@@ -552,21 +551,20 @@ __global__ __launch_bounds__(NT) void k_rows_merge(RowsArgs g) {
     }
     // (strict: the largest packed key stays below the ~0u padding)
     const bool packed = (u32)(chi - clo) < (1u << (32 - IB)) - 1u;  // (workgroup-uniform)
+    int npow = SEG;  // the packed sort's length: P padded to a power of two (with ~0u keys)
+    while (npow < P) npow <<= 1;
     u32 *const K0 = kp[0][0], *const X = kp[0][1], *const PY = kp[1][1];
+    u32 x[4];  // packed: this lane's four keys
     if (packed) {
         // each wave sorts its 256 positions in registers: the merge rounds
         // start from sorted segments of 256 instead of the B rows' short runs
-        u32 x[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             x[u] = u < ne ? ((u32)(c[u] - clo) << IB) | (u32)(e0 + u) : ~0u;
             if (u < ne) PY[e0 + u] = py[u];
         }
-        if (wv * SEG < P) {  // (wave-uniform)
-            wave_sort256(x, lane);
-            *reinterpret_cast<uint4 *>(K0 + e0) = make_uint4(x[0], x[1], x[2], x[3]);
-        }
-        if (tid <= CAP / SEG) sbd[tid] = min(P, tid * SEG);
+        if (wv * SEG < P) wave_sort256(x, lane);  // (wave-uniform)
+        if (wv * SEG < npow) *reinterpret_cast<uint4 *>(K0 + e0) = make_uint4(x[0], x[1], x[2], x[3]);
     } else {
 #pragma unroll
         for (int u = 0; u < 4; ++u)
@@ -577,17 +575,44 @@ __global__ __launch_bounds__(NT) void k_rows_merge(RowsArgs g) {
     }
     __syncthreads();
     RP(1);
+    int src = 0;  // the key buffer holding the (merged) keys: K0 or K1
+    if (packed) {
+        // the waves' sorted segments merged by the rest of a bitonic sort over
+        // npow keys, every sequence ascending: per level K the first stage pairs
+        // each position with its mirror in the K-block (e ^ (K-1)), the stages
+        // at distances K/4 .. 256 pair across waves through LDS (uint4 per
+        // lane, K0/K1 in turn, one barrier each), the last eight stay in
+        // registers.  Independent LDS reads instead of the merge rounds'
+        // dependent ones.
+        const bool act = wv * SEG < npow;  // (wave-uniform)
+        auto cmpx = [&](const uint4 y, bool rev, bool keep_min) {
+            const u32 yy[4] = {rev ? y.w : y.x, rev ? y.z : y.y, rev ? y.y : y.z, rev ? y.x : y.w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) x[u] = keep_min ? min(x[u], yy[u]) : max(x[u], yy[u]);
+        };
+        for (int K = 2 * SEG; K <= npow; K <<= 1) {  // (workgroup-uniform)
+            if (act) cmpx(*reinterpret_cast<const uint4 *>(kp[src][0] + (e0 ^ (K - 4))), true, (e0 & (K >> 1)) == 0);
+            for (int J = K >> 2; J >= SEG; J >>= 1) {
+                src ^= 1;
+                if (act) *reinterpret_cast<uint4 *>(kp[src][0] + e0) = make_uint4(x[0], x[1], x[2], x[3]);
+                __syncthreads();
+                if (act) cmpx(*reinterpret_cast<const uint4 *>(kp[src][0] + (e0 ^ J)), false, (e0 & J) == 0);
+            }
+            if (act) bitonic_merge<256, 128>(x, lane);
+            src ^= 1;
+            if (act) *reinterpret_cast<uint4 *>(kp[src][0] + e0) = make_uint4(x[0], x[1], x[2], x[3]);
+            __syncthreads();
+        }
+    }
     // merge-path chunks: thread t owns [t*ipt, t*ipt + ipt) of every round
     const int ipt = ((P + NT - 1) / NT) | 1;
     const int q0 = min(P, tid * ipt), q1 = min(P, q0 + ipt), nq = q1 - q0;
-    // the sorted groups the rounds start from: packed -> the waves' segments,
-    // unpacked -> the runs
-    const int *const bd = packed ? sbd : roff;
-    const int nb = packed ? (P + SEG - 1) / SEG : k;
+    // unpacked rows: merge rounds from the runs
+    const int *const bd = roff;
+    const int nb = packed ? 1 : k;
     int j0 = 0;  // the group holding q0 (pairs keep their position ranges every round)
-    if (nq > 0) j0 = packed ? q0 / SEG : lower_bound_dev(roff, 0, k + 1, q0 + 1) - 1;
+    if (nq > 0 && !packed) j0 = lower_bound_dev(roff, 0, k + 1, q0 + 1) - 1;
     // rounds: groups of 2^lw runs merged pairwise
-    int src = 0;
     for (int lw = 0; (1 << lw) < nb; ++lw) {
         const u32 *ik = kp[src][0], *ip = kp[src][1];
         u32 *ok = kp[src ^ 1][0], *op = kp[src ^ 1][1];
