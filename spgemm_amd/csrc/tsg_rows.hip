@@ -658,26 +658,52 @@ __global__ __launch_bounds__(NT) void k_rows_merge(RowsArgs g) {
     double *vb = reinterpret_cast<double *>(packed ? (src ? K0 : X) : kp[src ^ 1][0]);
     const u32 cs = packed ? IB : 0;  // key >> cs = the column (- clo when packed)
     int nh = 0;  // heads (first position of each column) in the chunk
-    {
+    // packed rows: the thread's four sorted keys are still in x[] (positions
+    // e0 .. e0 + 3), so only the key before them comes from LDS
+    const int np = packed ? max(0, min(4, P - e0)) : 0;
+    double xv[4];
+    u32 hd = 0;  // packed: head bits of the four positions
+    if (packed) {
+        const u32 prev = e0 > 0 && np > 0 ? sk[e0 - 1] : ~0u;
+        int pa[4];
+        double av[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (u < np) {
+                const u32 pj = PY[x[u] & (CAP - 1)];
+                const int ru = (int)(pj >> 16);
+                pa[u] = rbs[ru] + (int)(pj & 0xffffu);
+                av[u] = rav[ru];
+                const u32 pk = u ? x[u - 1] : prev;
+                hd |= (e0 + u == 0 || (x[u] >> IB) != (pk >> IB)) ? 1u << u : 0u;
+            }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (u < np) xv[u] = av[u] * g.Bval[pa[u]];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (u < np) vb[e0 + u] = xv[u];
+        nh = __popc(hd);
+    } else {
         int pa[IPM];
         double av[IPM];
 #pragma unroll
         for (int u = 0; u < IPM; ++u)
             if (u < nq) {
                 const u32 key = sk[q0 + u];
-                const u32 pj = packed ? PY[key & (CAP - 1)] : sp[q0 + u];
+                const u32 pj = sp[q0 + u];
                 const int ru = (int)(pj >> 16);
                 pa[u] = rbs[ru] + (int)(pj & 0xffffu);
                 av[u] = rav[ru];
                 nh += (q0 + u == 0 || (key >> cs) != (sk[q0 + u - 1] >> cs));
             }
-        double x[IPM];
+        double xx[IPM];
 #pragma unroll
         for (int u = 0; u < IPM; ++u)
-            if (u < nq) x[u] = av[u] * g.Bval[pa[u]];
+            if (u < nq) xx[u] = av[u] * g.Bval[pa[u]];
 #pragma unroll
         for (int u = 0; u < IPM; ++u)
-            if (u < nq) vb[q0 + u] = x[u];
+            if (u < nq) vb[q0 + u] = xx[u];
     }
     // the chunk's first output slot: exclusive scan of the head counts
     const int inc = wave_incl_scan_dpp(nh);
@@ -691,15 +717,35 @@ __global__ __launch_bounds__(NT) void k_rows_merge(RowsArgs g) {
         tot += red[w];
     }
     if (tid == 0) g.rnnz[r] = tot;
-    const int cadd = packed ? clo : 0;
-    for (int q = q0; q < q1; ++q) {
-        const u32 col = sk[q] >> cs;
-        if (q == 0 || (sk[q - 1] >> cs) != col) {
-            double sum = vb[q];
-            for (int j = q + 1; j < P && (sk[j] >> cs) == col; ++j) sum += vb[j];  // ascending: deterministic
-            g.Scol[base + o] = (int)col + cadd;
-            g.Sval[base + o] = sum;
-            ++o;
+    if (packed) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (hd >> u & 1u) {
+                const u32 col = x[u] >> IB;
+                double sum = xv[u];
+                int j = u + 1;
+#pragma unroll
+                for (int v = u + 1; v < 4; ++v)  // (ascending, as below: deterministic)
+                    if (j == v && v < np && (x[v] >> IB) == col) {
+                        sum += xv[v];
+                        ++j;
+                    }
+                if (j == 4)
+                    for (int q = e0 + 4; q < P && (sk[q] >> IB) == col; ++q) sum += vb[q];
+                g.Scol[base + o] = (int)col + clo;
+                g.Sval[base + o] = sum;
+                ++o;
+            }
+    } else {
+        for (int q = q0; q < q1; ++q) {
+            const u32 col = sk[q] >> cs;
+            if (q == 0 || (sk[q - 1] >> cs) != col) {
+                double sum = vb[q];
+                for (int j = q + 1; j < P && (sk[j] >> cs) == col; ++j) sum += vb[j];  // ascending: deterministic
+                g.Scol[base + o] = (int)col;
+                g.Sval[base + o] = sum;
+                ++o;
+            }
         }
     }
     RP(4);
