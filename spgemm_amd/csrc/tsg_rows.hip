@@ -990,8 +990,9 @@ __global__ __launch_bounds__(WG) void k_rows_compact(int m, const int *cfirst, c
     for (int i = tid; i < n; i += WG) {
         const int r = rowof[i];
         const long long src = soff[r] + (c0 + i - Crp[r]);
-        Ccol[c0 + i] = Scol[src];
-        Cval[c0 + i] = Sval[src];
+        // (streamed: staging read once, C not re-read by this call)
+        __builtin_nontemporal_store(__builtin_nontemporal_load(Scol + src), Ccol + c0 + i);
+        __builtin_nontemporal_store(__builtin_nontemporal_load(Sval + src), Cval + c0 + i);
     }
 }
 
