@@ -1304,39 +1304,44 @@ __global__ __launch_bounds__(WG) void k_entry_bounds(const int *ciA, long nnzA, 
 }
 
 // row starts as a bitmap over entry positions (bit p set: some non-empty row starts at p)
-__global__ __launch_bounds__(WG) void k_row_start_bits(const int *rp, int m, u32 *bits, int *flag) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) *flag = 0;  // (k_rows_unsorted3 sets it)
-    for (int r = blockIdx.x * WG + threadIdx.x; r < m; r += gridDim.x * WG) {
+// Row sortedness in one pass, a workgroup per SRT_TILE entries: the rows
+// starting in the tile (a binary search of its bounds in the row pointers)
+// mark their first entries in an LDS bitmap, then a descent ci[p] < ci[p-1]
+// that is not at a row start means some row is not column-sorted -- reported
+// by a system-scope store into the caller's host-mapped flag (no device flag,
+// no memset, no copy back).
+constexpr int SRT_TILE = 4096;
+__global__ __launch_bounds__(WG) void k_rows_sorted_tiles(const int *rp, const int *ci, int m, int nnz, int *hflag) {
+    __shared__ u32 st[SRT_TILE / 32];
+    __shared__ int rr[2];
+    const int tid = threadIdx.x;
+    const int p0 = blockIdx.x * SRT_TILE, p1 = min(nnz, p0 + SRT_TILE);
+    for (int i = tid; i < SRT_TILE / 32; i += WG) st[i] = 0;
+    if (tid < 2) rr[tid] = lower_bound_dev(rp, 0, m + 1, tid ? p1 : p0);  // rows starting in [p0, p1)
+    __syncthreads();
+    for (int r = rr[0] + tid; r < rr[1]; r += WG) {
         const int p = rp[r];
-        if (p < rp[r + 1]) atomicOr(&bits[p >> 5], 1u << (p & 31));
+        if (p < rp[r + 1]) atomicOr(&st[(p - p0) >> 5], 1u << ((p - p0) & 31));
     }
-}
-// a descent ci[p] < ci[p-1] that is not at a row start: rows are not column-sorted
-__global__ __launch_bounds__(WG) void k_rows_unsorted3(const int *rp, const int *ci, int m, const u32 *bits,
-                                                       int *flag) {
-    const int nnz = rp[m];
-    for (int p = blockIdx.x * WG + threadIdx.x + 1; p < nnz; p += gridDim.x * WG)
-        if (ci[p] < ci[p - 1] && !((bits[p >> 5] >> (p & 31)) & 1u)) *flag = 1;
+    __syncthreads();
+    bool bad = false;
+    for (int p = max(1, p0) + tid; p < p1; p += WG)
+        bad |= ci[p] < ci[p - 1] && !((st[(p - p0) >> 5] >> ((p - p0) & 31)) & 1u);
+    if (__ballot(bad) && lane_id() == 0) __hip_atomic_store(hflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Queued only: the flag (1: some row is not column-sorted) lands in *host_flag
-// (pinned) at the caller's next stream synchronisation.
+// (pinned, host-mapped: written by the kernel itself) by the caller's next
+// stream synchronisation.
 int dev_rows_sorted_async(Context &cx, const tsg_dev_csr &M, int *host_flag, hipStream_t s) {
-    int *flag = nullptr;
-    TSG_TRY(cx.get(&flag, 1));
-    u32 *bits = nullptr;
-    if (!(M.m > 0 && M.nnz > 1)) TSG_HIP(hipMemsetAsync(flag, 0, sizeof(int), s));
+    *host_flag = 0;
     if (M.m > 0 && M.nnz > 1) {
-        const size_t nw = ((size_t)M.nnz + 31) / 32;
-        TSG_TRY(cx.get(&bits, nw));
-        TSG_HIP(hipMemsetAsync(bits, 0, nw * sizeof(u32), s));
-        k_row_start_bits<<<grid_for(M.m, WG, 16384), WG, 0, s>>>(M.rowpointer, M.m, bits, flag);
-        k_rows_unsorted3<<<grid_for(M.nnz, WG, 16384), WG, 0, s>>>(M.rowpointer, M.columnindex, M.m, bits, flag);
+        int *dflag = nullptr;
+        TSG_HIP(hipHostGetDevicePointer((void **)&dflag, host_flag, 0));
+        k_rows_sorted_tiles<<<(M.nnz + SRT_TILE - 1) / SRT_TILE, WG, 0, s>>>(M.rowpointer, M.columnindex, M.m, M.nnz,
+                                                                             dflag);
     }
     TSG_HIP(hipGetLastError());
-    TSG_HIP(hipMemcpyAsync(host_flag, flag, sizeof(int), hipMemcpyDeviceToHost, s));
-    cx.put(bits);  // the pool's reuse is stream-ordered
-    cx.put(flag);
     return TSG_OK;
 }
 int dev_rows_sorted(Context &cx, const tsg_dev_csr &M, bool *sorted, hipStream_t s) {
