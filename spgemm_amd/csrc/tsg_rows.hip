@@ -40,10 +40,13 @@ constexpr int S16_MAX = 16;           // class S16: products (and runs) per row,
 constexpr int RS_MAX = 64;            // class S64: products (and runs) per row, a wave
 // merge classes M1..M4: products and runs per row, threads per row -- each
 // sized so its LDS (16 B per product + 16 B per run) keeps several rows per CU
-constexpr int M0_CAP = 256, M0_RUNS = 64, M0_NT = 64;      // 5 KB: one wave per row
-constexpr int M1_CAP = 512, M1_RUNS = 128, M1_NT = 128;    // 10 KB
-constexpr int M2_CAP = 1024, M2_RUNS = 256, M2_NT = 256;   // 20 KB
-constexpr int M3_CAP = 2048, M3_RUNS = 512, M3_NT = 512;   // 40 KB
+// (M0..M3: run tables a few runs short of a power of two, so that 32, 16, 8
+// and 4 workgroups fit a CU's 160 KiB of LDS -- full 64/128/256/512-run tables
+// made each workgroup a few dozen bytes too large for the last one)
+constexpr int M0_CAP = 256, M0_RUNS = 62, M0_NT = 64;      // 5,104 B: one wave per row
+constexpr int M1_CAP = 512, M1_RUNS = 124, M1_NT = 128;    // 10,208 B
+constexpr int M2_CAP = 1024, M2_RUNS = 248, M2_NT = 256;   // 20,400 B
+constexpr int M3_CAP = 2048, M3_RUNS = 504, M3_NT = 512;   // 40,912 B
 constexpr int M4_CAP = 4096, M4_RUNS = 512, M4_NT = 1024;  // 72 KB
 constexpr int NCLS = 8;               // S16, S64, M0..M4, H
 constexpr int BIN_ROWS = 2048;        // rows per workgroup of the binning kernel
