@@ -175,37 +175,47 @@ static int tile_structure(int m, int n, const int *rowptr, const int *col, int r
                           int **tile_col_out, int **tile_row_out) {
     int tilem = (m + rpt - 1) / rpt, tilen = (n + cpt - 1) / cpt;
     int *tile_ptr = (int *)xcalloc((size_t)tilem + 1, sizeof(int));
-    unsigned char *seen = (unsigned char *)xcalloc((size_t)tilen, 1);
-    for (int ti = 0; ti < tilem; ti++) {
-        int r0 = ti * rpt, r1 = (ti + 1) * rpt < m ? (ti + 1) * rpt : m;
-        for (int p = rowptr[r0]; p < rowptr[r1]; p++) {
-            int tc = col[p] / cpt;
-            if (!seen[tc]) { seen[tc] = 1; tile_ptr[ti]++; }
+#pragma omp parallel
+    {
+        unsigned char *seen = (unsigned char *)xcalloc((size_t)tilen, 1);
+#pragma omp for schedule(dynamic, 256)
+        for (int ti = 0; ti < tilem; ti++) {
+            int r0 = ti * rpt, r1 = (ti + 1) * rpt < m ? (ti + 1) * rpt : m;
+            for (int p = rowptr[r0]; p < rowptr[r1]; p++) {
+                int tc = col[p] / cpt;
+                if (!seen[tc]) { seen[tc] = 1; tile_ptr[ti]++; }
+            }
+            for (int p = rowptr[r0]; p < rowptr[r1]; p++) seen[col[p] / cpt] = 0;
         }
-        for (int p = rowptr[r0]; p < rowptr[r1]; p++) seen[col[p] / cpt] = 0;
+        free(seen);
     }
     excl_scan_int(tile_ptr, (long)tilem + 1);
     int numtile = tile_ptr[tilem];
     int *tcol = (int *)xcalloc(numtile, sizeof(int));
     int *trow = (int *)xcalloc(numtile, sizeof(int));
-    for (int ti = 0; ti < tilem; ti++) {
-        int r0 = ti * rpt, r1 = (ti + 1) * rpt < m ? (ti + 1) * rpt : m;
-        for (int p = rowptr[r0]; p < rowptr[r1]; p++) seen[col[p] / cpt] = 1;
-        /* ascending tile columns == the blkj loop of step2_kernel (:92-105) */
-        int w = tile_ptr[ti];
-        for (int p = rowptr[r0]; p < rowptr[r1]; p++) {
-            int tc = col[p] / cpt;
-            if (seen[tc] == 1) { seen[tc] = 2; tcol[w++] = tc; }
+#pragma omp parallel
+    {
+        unsigned char *seen = (unsigned char *)xcalloc((size_t)tilen, 1);
+#pragma omp for schedule(dynamic, 256)
+        for (int ti = 0; ti < tilem; ti++) {
+            int r0 = ti * rpt, r1 = (ti + 1) * rpt < m ? (ti + 1) * rpt : m;
+            for (int p = rowptr[r0]; p < rowptr[r1]; p++) seen[col[p] / cpt] = 1;
+            /* ascending tile columns == the blkj loop of step2_kernel (:92-105) */
+            int w = tile_ptr[ti];
+            for (int p = rowptr[r0]; p < rowptr[r1]; p++) {
+                int tc = col[p] / cpt;
+                if (seen[tc] == 1) { seen[tc] = 2; tcol[w++] = tc; }
+            }
+            /* insertion sort of this tile row's columns (small) */
+            for (int a = tile_ptr[ti] + 1; a < w; a++) {
+                int x = tcol[a], b = a - 1;
+                while (b >= tile_ptr[ti] && tcol[b] > x) { tcol[b + 1] = tcol[b]; b--; }
+                tcol[b + 1] = x;
+            }
+            for (int a = tile_ptr[ti]; a < w; a++) { trow[a] = ti; seen[tcol[a]] = 0; }
         }
-        /* insertion sort of this tile row's columns (small) */
-        for (int a = tile_ptr[ti] + 1; a < w; a++) {
-            int x = tcol[a], b = a - 1;
-            while (b >= tile_ptr[ti] && tcol[b] > x) { tcol[b + 1] = tcol[b]; b--; }
-            tcol[b + 1] = x;
-        }
-        for (int a = tile_ptr[ti]; a < w; a++) { trow[a] = ti; seen[tcol[a]] = 0; }
+        free(seen);
     }
-    free(seen);
     *tilem_out = tilem; *tilen_out = tilen;
     *tile_ptr_out = tile_ptr; *tile_col_out = tcol; *tile_row_out = trow;
     return numtile;
@@ -311,7 +321,8 @@ int tsgo_csr2tile_col_major(tsgo_mat *B, int tm, int tn) {
     B->tile_csr_Col = (uint16_t *)xcalloc(B->nnz, sizeof(uint16_t));
     B->tile_csr_Value = (double *)xcalloc(B->nnz, sizeof(double));
     B->mask = (uint16_t *)xcalloc((size_t)numtile * tn * wpr, sizeof(uint16_t));
-    /* counts per (csc tile, local row) */
+    /* counts per (csc tile, local row); tile columns own disjoint tiles */
+#pragma omp parallel for schedule(dynamic, 64)
     for (int tj = 0; tj < B->tilen; tj++) {
         int t0 = B->csc_tile_ptr[tj], t1 = B->csc_tile_ptr[tj + 1];
         for (int c = tj * tm; c < (tj + 1) * tm && c < n; c++)
@@ -334,6 +345,7 @@ int tsgo_csr2tile_col_major(tsgo_mat *B, int tm, int tn) {
      * iterate local cols ascending and rows ascending inside each column, and
      * insert into the (row) slot -- the per-tile transpose of :455-458 */
     int *rowfill = (int *)xcalloc((size_t)numtile * tn, sizeof(int));
+#pragma omp parallel for schedule(dynamic, 64)
     for (int tj = 0; tj < B->tilen; tj++) {
         int t0 = B->csc_tile_ptr[tj], t1 = B->csc_tile_ptr[tj + 1];
         for (int c = tj * tm; c < (tj + 1) * tm && c < n; c++)
@@ -360,80 +372,116 @@ int tsgo_csr2tile_col_major(tsgo_mat *B, int tm, int tn) {
  * (:394-773); Ptr = exclusive scan of row popcounts, nnz = popcount
  * (:666-709).  Step 3 = values sum_k A(r,c)*B(c,x) at the mask positions,
  * local cols ascending per row (:1612-1952, correct arithmetic).  Tiles of the
- * structure whose product is empty keep nnz 0 and an all-zero Ptr. */
+ * structure whose product is empty keep nnz 0 and an all-zero Ptr.
+ *
+ * Evaluation order (OpenMP over C tile rows, so that full-size stand-ins run
+ * in seconds): the matched (A tile, B tile) pairs of a tile row are visited
+ * A tile by A tile (k ascending), each B tile of B's tile row k mapped to its
+ * C tile -- for any one C tile the pairs still come k ascending, then the A
+ * nonzeros in payload order, then the B row's entries, the order of the
+ * per-tile accumulation above, so every value is the same sum. */
+static int cmp_int_asc(const void *a, const void *b) {
+    int x = *(const int *)a, y = *(const int *)b;
+    return (x > y) - (x < y);
+}
+
 int tsgo_tilespgemm(const tsgo_mat *A, const tsgo_mat *B, tsgo_mat *C, int tm, int tn) {
     memset(C, 0, sizeof(*C));
     if (A->n != B->m) return -1;
     int wpr = tm / MASK_BITS;
     int blkmA = A->tilem, blknB = B->tilen;
     C->m = A->m; C->n = B->n; C->tilem = blkmA; C->tilen = blknB;
-    /* step 1 */
+    /* step 1: C tiles per tile row, then each row's columns ascending */
     C->tile_ptr = (int *)xcalloc((size_t)blkmA + 1, sizeof(int));
-    unsigned char *flag = (unsigned char *)xcalloc((size_t)blknB, 1);
-    long total = 0;
-    for (int i = 0; i < blkmA; i++) {
-        int cnt = 0;
-        for (int a = A->tile_ptr[i]; a < A->tile_ptr[i + 1]; a++) {
-            int k = A->tile_columnidx[a];
-            for (int b = B->tile_ptr[k]; b < B->tile_ptr[k + 1]; b++)
-                if (!flag[B->tile_columnidx[b]]) { flag[B->tile_columnidx[b]] = 1; cnt++; }
+#pragma omp parallel
+    {
+        unsigned char *flag = (unsigned char *)xcalloc((size_t)blknB, 1);
+#pragma omp for schedule(dynamic, 2)
+        for (int i = 0; i < blkmA; i++) {
+            int cnt = 0;
+            for (int a = A->tile_ptr[i]; a < A->tile_ptr[i + 1]; a++) {
+                int k = A->tile_columnidx[a];
+                for (int b = B->tile_ptr[k]; b < B->tile_ptr[k + 1]; b++)
+                    if (!flag[B->tile_columnidx[b]]) { flag[B->tile_columnidx[b]] = 1; cnt++; }
+            }
+            for (int a = A->tile_ptr[i]; a < A->tile_ptr[i + 1]; a++) {
+                int k = A->tile_columnidx[a];
+                for (int b = B->tile_ptr[k]; b < B->tile_ptr[k + 1]; b++) flag[B->tile_columnidx[b]] = 0;
+            }
+            C->tile_ptr[i] = cnt;
         }
-        for (int a = A->tile_ptr[i]; a < A->tile_ptr[i + 1]; a++) {
-            int k = A->tile_columnidx[a];
-            for (int b = B->tile_ptr[k]; b < B->tile_ptr[k + 1]; b++) flag[B->tile_columnidx[b]] = 0;
-        }
-        C->tile_ptr[i] = cnt;
-        total += cnt;
-        if (total > 0x7fffffffL) { free(flag); return -3; }
+        free(flag);
     }
+    long total = 0;
+    for (int i = 0; i < blkmA; i++) total += C->tile_ptr[i];
+    if (total > 0x7fffffffL) return -3;
     excl_scan_int(C->tile_ptr, (long)blkmA + 1);
     int numblkC = C->tile_ptr[blkmA];
     C->numtile = numblkC;
     C->tile_columnidx = (int *)xcalloc(numblkC, sizeof(int));
     C->tile_rowidx = (int *)xcalloc(numblkC, sizeof(int));
-    for (int i = 0; i < blkmA; i++) {
-        for (int a = A->tile_ptr[i]; a < A->tile_ptr[i + 1]; a++) {
-            int k = A->tile_columnidx[a];
-            for (int b = B->tile_ptr[k]; b < B->tile_ptr[k + 1]; b++) flag[B->tile_columnidx[b]] = 1;
+#pragma omp parallel
+    {
+        unsigned char *flag = (unsigned char *)xcalloc((size_t)blknB, 1);
+#pragma omp for schedule(dynamic, 2)
+        for (int i = 0; i < blkmA; i++) {
+            int w = C->tile_ptr[i];
+            for (int a = A->tile_ptr[i]; a < A->tile_ptr[i + 1]; a++) {
+                int k = A->tile_columnidx[a];
+                for (int b = B->tile_ptr[k]; b < B->tile_ptr[k + 1]; b++) {
+                    int j = B->tile_columnidx[b];
+                    if (!flag[j]) { flag[j] = 1; C->tile_columnidx[w++] = j; }
+                }
+            }
+            int t0 = C->tile_ptr[i];
+            qsort(C->tile_columnidx + t0, (size_t)(w - t0), sizeof(int), cmp_int_asc);
+            for (int t = t0; t < w; t++) { C->tile_rowidx[t] = i; flag[C->tile_columnidx[t]] = 0; }
         }
-        int w = C->tile_ptr[i];
-        for (int j = 0; j < blknB && w < C->tile_ptr[i + 1]; j++)
-            if (flag[j]) { flag[j] = 0; C->tile_rowidx[w] = i; C->tile_columnidx[w++] = j; }
+        free(flag);
     }
-    free(flag);
 
-    /* step 2 */
+    /* step 2: masks (maskC[r] |= maskB[c] per matched pair and A nonzero), Ptr, nnz */
     C->tile_nnz = (int *)xcalloc((size_t)numblkC + 1, sizeof(int));
     C->tile_csr_Ptr = (uint16_t *)xcalloc((size_t)numblkC * tm, sizeof(uint16_t));
     C->mask = (uint16_t *)xcalloc((size_t)numblkC * tm * wpr, sizeof(uint16_t));
-    for (int t = 0; t < numblkC; t++) {
-        int i = C->tile_rowidx[t], j = C->tile_columnidx[t];
-        uint16_t *mc = C->mask + (size_t)t * tm * wpr;
-        int b0 = B->csc_tile_ptr[j], b1 = B->csc_tile_ptr[j + 1];
-        for (int a = A->tile_ptr[i]; a < A->tile_ptr[i + 1]; a++) {
-            int k = A->tile_columnidx[a];
-            int b = find_tile(B->csc_tile_rowidx, b0, b1, k);
-            if (b >= b1 || B->csc_tile_rowidx[b] != k) continue;
-            const uint16_t *mb = B->mask + (size_t)b * tn * wpr;
-            for (int q = A->tile_nnz[a]; q < A->tile_nnz[a + 1]; q++) {
-                int r = A->tile_csr_Col[q] / tn, c = A->tile_csr_Col[q] % tn;
-                for (int w = 0; w < wpr; w++) mc[r * wpr + w] |= mb[c * wpr + w];
+#pragma omp parallel
+    {
+        int *map = (int *)malloc(((size_t)blknB + 1) * sizeof(int));
+        for (int j = 0; j < blknB; j++) map[j] = -1;
+#pragma omp for schedule(dynamic, 2)
+        for (int i = 0; i < blkmA; i++) {
+            for (int t = C->tile_ptr[i]; t < C->tile_ptr[i + 1]; t++) map[C->tile_columnidx[t]] = t;
+            for (int a = A->tile_ptr[i]; a < A->tile_ptr[i + 1]; a++) {
+                int k = A->tile_columnidx[a];
+                for (int brm = B->tile_ptr[k]; brm < B->tile_ptr[k + 1]; brm++) {
+                    int j = B->tile_columnidx[brm], t = map[j];
+                    int b0 = B->csc_tile_ptr[j], b1 = B->csc_tile_ptr[j + 1];
+                    int b = find_tile(B->csc_tile_rowidx, b0, b1, k);  /* CSC payload id of tile (k, j) */
+                    uint16_t *mc = C->mask + (size_t)t * tm * wpr;
+                    const uint16_t *mb = B->mask + (size_t)b * tn * wpr;
+                    for (int q = A->tile_nnz[a]; q < A->tile_nnz[a + 1]; q++) {
+                        int r = A->tile_csr_Col[q] / tn, c = A->tile_csr_Col[q] % tn;
+                        for (int w = 0; w < wpr; w++) mc[r * wpr + w] |= mb[c * wpr + w];
+                    }
+                }
+            }
+            for (int t = C->tile_ptr[i]; t < C->tile_ptr[i + 1]; t++) {
+                const uint16_t *mc = C->mask + (size_t)t * tm * wpr;
+                int nz = 0;
+                for (int r = 0; r < tm; r++)
+                    for (int w = 0; w < wpr; w++) nz += __builtin_popcount(mc[r * wpr + w]);
+                if (nz) {
+                    int run = 0;
+                    for (int r = 0; r < tm; r++) {
+                        C->tile_csr_Ptr[(size_t)t * tm + r] = (uint16_t)run;
+                        for (int w = 0; w < wpr; w++) run += __builtin_popcount(mc[r * wpr + w]);
+                    }
+                }
+                C->tile_nnz[t] = nz;
+                map[C->tile_columnidx[t]] = -1;
             }
         }
-        int run = 0;
-        for (int r = 0; r < tm; r++) {
-            C->tile_csr_Ptr[(size_t)t * tm + r] = 0;
-        }
-        int nz = 0;
-        for (int r = 0; r < tm; r++)
-            for (int w = 0; w < wpr; w++) nz += __builtin_popcount(mc[r * wpr + w]);
-        if (nz) {
-            for (int r = 0; r < tm; r++) {
-                C->tile_csr_Ptr[(size_t)t * tm + r] = (uint16_t)run;
-                for (int w = 0; w < wpr; w++) run += __builtin_popcount(mc[r * wpr + w]);
-            }
-        }
-        C->tile_nnz[t] = nz;
+        free(map);
     }
     /* exclusive scan (:2602), nnzC = last (:2604) */
     long long nnzc = 0;
@@ -446,38 +494,54 @@ int tsgo_tilespgemm(const tsgo_mat *A, const tsgo_mat *B, tsgo_mat *C, int tm, i
     C->tile_nnz[numblkC] = (int)nnzc;
     C->nnz = (int)nnzc;
 
-    /* step 3 */
+    /* step 3: local columns from the masks, values accumulated at each
+     * column's rank in its row (the row's Ptr + the mask bits before it) */
     C->tile_csr_Col = (uint16_t *)xcalloc((size_t)nnzc, sizeof(uint16_t));
     C->tile_csr_Value = (double *)xcalloc((size_t)nnzc, sizeof(double));
-    double *acc = (double *)xcalloc((size_t)tm * tm, sizeof(double));
-    for (int t = 0; t < numblkC; t++) {
-        if (C->tile_nnz[t + 1] == C->tile_nnz[t]) continue;
-        int i = C->tile_rowidx[t], j = C->tile_columnidx[t];
-        memset(acc, 0, (size_t)tm * tm * sizeof(double));
-        int b0 = B->csc_tile_ptr[j], b1 = B->csc_tile_ptr[j + 1];
-        for (int a = A->tile_ptr[i]; a < A->tile_ptr[i + 1]; a++) {
-            int k = A->tile_columnidx[a];
-            int b = find_tile(B->csc_tile_rowidx, b0, b1, k);
-            if (b >= b1 || B->csc_tile_rowidx[b] != k) continue;
-            int bnz0 = B->tile_nnz[b], bnz1 = B->tile_nnz[b + 1];
-            const uint16_t *bp = B->tile_csr_Ptr + (size_t)b * tn;
-            for (int q = A->tile_nnz[a]; q < A->tile_nnz[a + 1]; q++) {
-                int r = A->tile_csr_Col[q] / tn, c = A->tile_csr_Col[q] % tn;
-                double va = A->tile_csr_Value[q];
-                int s0 = bnz0 + bp[c], s1 = (c == tn - 1) ? bnz1 : bnz0 + bp[c + 1];
-                for (int s = s0; s < s1; s++) acc[r * tm + B->tile_csr_Col[s]] += va * B->tile_csr_Value[s];
+#pragma omp parallel
+    {
+        int *map = (int *)malloc(((size_t)blknB + 1) * sizeof(int));
+        for (int j = 0; j < blknB; j++) map[j] = -1;
+#pragma omp for schedule(dynamic, 2)
+        for (int i = 0; i < blkmA; i++) {
+            for (int t = C->tile_ptr[i]; t < C->tile_ptr[i + 1]; t++) {
+                map[C->tile_columnidx[t]] = t;
+                const uint16_t *mc = C->mask + (size_t)t * tm * wpr;
+                int w = C->tile_nnz[t];
+                for (int r = 0; r < tm; r++)
+                    for (int x = 0; x < tm; x++)
+                        if ((mc[r * wpr + x / MASK_BITS] >> (MASK_BITS - 1 - x % MASK_BITS)) & 1u)
+                            C->tile_csr_Col[w++] = (uint16_t)x;
             }
-        }
-        const uint16_t *mc = C->mask + (size_t)t * tm * wpr;
-        int w = C->tile_nnz[t];
-        for (int r = 0; r < tm; r++)
-            for (int x = 0; x < tm; x++)
-                if ((mc[r * wpr + x / MASK_BITS] >> (MASK_BITS - 1 - x % MASK_BITS)) & 1u) {
-                    C->tile_csr_Col[w] = (uint16_t)x;
-                    C->tile_csr_Value[w++] = acc[r * tm + x];
+            for (int a = A->tile_ptr[i]; a < A->tile_ptr[i + 1]; a++) {
+                int k = A->tile_columnidx[a];
+                for (int brm = B->tile_ptr[k]; brm < B->tile_ptr[k + 1]; brm++) {
+                    int j = B->tile_columnidx[brm], t = map[j];
+                    int b0 = B->csc_tile_ptr[j], b1 = B->csc_tile_ptr[j + 1];
+                    int b = find_tile(B->csc_tile_rowidx, b0, b1, k);
+                    const uint16_t *mc = C->mask + (size_t)t * tm * wpr;
+                    const uint16_t *bp = B->tile_csr_Ptr + (size_t)b * tn;
+                    int bnz0 = B->tile_nnz[b], bnz1 = B->tile_nnz[b + 1];
+                    double *cv = C->tile_csr_Value + C->tile_nnz[t];
+                    const uint16_t *cp = C->tile_csr_Ptr + (size_t)t * tm;
+                    for (int q = A->tile_nnz[a]; q < A->tile_nnz[a + 1]; q++) {
+                        int r = A->tile_csr_Col[q] / tn, c = A->tile_csr_Col[q] % tn;
+                        double va = A->tile_csr_Value[q];
+                        int s0 = bnz0 + bp[c], s1 = (c == tn - 1) ? bnz1 : bnz0 + bp[c + 1];
+                        for (int s = s0; s < s1; s++) {
+                            int x = B->tile_csr_Col[s], rk = cp[r];
+                            for (int w = 0; w < x / MASK_BITS; w++) rk += __builtin_popcount(mc[r * wpr + w]);
+                            int sh = MASK_BITS - x % MASK_BITS;  /* the bits of columns before x in its word */
+                            rk += __builtin_popcount((unsigned)(mc[r * wpr + x / MASK_BITS] >> sh));
+                            cv[rk] += va * B->tile_csr_Value[s];
+                        }
+                    }
                 }
+            }
+            for (int t = C->tile_ptr[i]; t < C->tile_ptr[i + 1]; t++) map[C->tile_columnidx[t]] = -1;
+        }
+        free(map);
     }
-    free(acc);
     return 0;
 }
 

@@ -400,24 +400,35 @@ template <int D> __device__ __forceinline__ u32 lane_xor(u32 v) {
 
 // one bitonic stage at element distance J inside sequences of K (elements
 // e = 4*lane + u): ascending where e & K == 0
+// (compare-exchanges whose direction varies by lane: one compare, the
+// direction folded into the lane mask, one select -- instead of min, max and a
+// select per element)
 template <int K, int J> __device__ __forceinline__ void bitonic_stage(u32 (&x)[4], int lane) {
     if constexpr (J >= 4) {
         constexpr int D = J / 4;
         const bool asc = K >= 256 || (lane & (K / 4)) == 0;
-        const bool keep_min = asc == ((lane & D) == 0);
+        const bool keep_max = asc != ((lane & D) == 0);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const u32 y = lane_xor<D>(x[u]);
-            x[u] = keep_min ? min(x[u], y) : max(x[u], y);
+            x[u] = ((y < x[u]) != keep_max) ? y : x[u];
         }
     } else {
 #pragma unroll
         for (int u = 0; u < 4; ++u)
             if ((u & J) == 0) {
-                const bool asc = K < 4 ? (u & K) == 0 : (K >= 256 || (lane & (K / 4)) == 0);
-                const u32 lo = min(x[u], x[u + J]), hi = max(x[u], x[u + J]);
-                x[u] = asc ? lo : hi;
-                x[u + J] = asc ? hi : lo;
+                if constexpr (K < 4 || K >= 256) {  // the direction is the same on every lane
+                    const bool asc = K < 4 ? (u & K) == 0 : true;  // (u: unrolled, a constant)
+                    const u32 lo = min(x[u], x[u + J]), hi = max(x[u], x[u + J]);
+                    x[u] = asc ? lo : hi;
+                    x[u + J] = asc ? hi : lo;
+                } else {
+                    const bool desc = (lane & (K / 4)) != 0;
+                    const bool sw = (x[u + J] < x[u]) != desc;
+                    const u32 a = x[u], b = x[u + J];
+                    x[u] = sw ? b : a;
+                    x[u + J] = sw ? a : b;
+                }
             }
     }
 }
@@ -433,28 +444,34 @@ template <int K> __device__ __forceinline__ void bitonic_sort(u32 (&x)[4], int l
 // (36 compare-exchange stages, 21 of them across lanes; no LDS, no barrier)
 __device__ __forceinline__ void wave_sort256(u32 (&x)[4], int lane) { bitonic_sort<256>(x, lane); }
 
-// ---- classes M1..M4: pairwise stable merges of the row's runs in LDS.  NT
-// threads per row, at most CAP products and RUNS runs.  Thread t owns the
-// positions [t*ipt, t*ipt + ipt) of every pass (ipt odd, so the lanes' LDS
-// accesses spread over the banks): its global loads are issued together (IPM =
-// the largest ipt, unrolled), and each merge round is a merge path -- one
-// co-rank search per pair the chunk touches, then a sequential merge.
+// ---- classes M0..M4: a row's runs sorted into one column-ordered sequence in
+// LDS.  NT threads per row, at most CAP products and RUNS A entries (so a
+// thread per entry).
+//
+// The expansion loads each product's B column AND value together (one round
+// trip): the value a*b goes to LDS in expansion order, and after the sort
+// each key's low bits (its expansion position) find it there -- no second
+// dependent gather of B's values after the sort.
 //
 // Keys: when the row's column span fits, one u32 per element packs
-// (column - lo, expansion position) -- unique, so the merged order is one fixed
-// order and nothing else moves; the (run, position-in-run) payloads stay in
-// expansion order.  Wider rows sort u32 columns with a moved payload and take
-// ties from the left group first (equal columns stay in run order).  Either
-// way every sum is taken in one fixed order.
+// (column - lo, expansion position) -- unique, so the sorted order is one fixed
+// order and every sum is taken in it.  Each wave sorts its 256 positions in
+// registers with a bitonic network, then the rest of a bitonic sort over the
+// waves' segments runs through LDS.  Wider rows sort u32 columns with a
+// (run, position) payload by merge-path rounds, ties from the left group first
+// (equal columns stay in run order), and reload their values after.
 template <int NT, int CAP, int RUNS>
-__global__ __launch_bounds__(NT) void k_rows_merge(RowsArgs g) {
+__global__ __launch_bounds__(NT, NT == 1024 ? 8 : 1) void k_rows_merge(RowsArgs g) {
     constexpr int NW = NT / 64;
     constexpr int IPM = (CAP + NT - 1) / NT | 1;
     constexpr int IB = CAP == 256 ? 8 : CAP == 512 ? 9 : CAP == 1024 ? 10 : CAP == 2048 ? 11 : 12;  // position bits
     static_assert((1 << IB) == CAP, "CAP: a power of two in [256, 4096]");
-    // kp[0][0] K0 | kp[0][1] X | kp[1][0] K1 | kp[1][1] PY.  Packed: keys ping-pong
-    // K0 <-> K1, PY holds the payloads, and the values go to K0+X or X+K1 (the
-    // free pair next to the final keys).  Unpacked: [buffer][keys | payloads].
+    constexpr int SEG = 256;
+    static_assert(CAP == 4 * NT, "four positions per thread");
+    static_assert(RUNS <= NT, "a thread per A entry");
+    // packed: keys ping-pong kp[0][0] <-> kp[0][1], the values (expansion
+    // order) in kp[1] as CAP doubles.  Unpacked: [buffer][keys | payloads],
+    // the values gathered at the end into the free buffer.
     __shared__ __align__(16) u32 kp[2][2][CAP];
     __shared__ int roff[RUNS + 1];
     __shared__ int rbs[RUNS];       // each run's B start
@@ -463,295 +480,282 @@ __global__ __launch_bounds__(NT) void k_rows_merge(RowsArgs g) {
     RP_INIT
     const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
     const int4 le = g.list[blockIdx.x];
-    const int r = le.x, a0 = le.y, ka = le.z;
-    const long long base = g.E[a0];  // (the staging offset: not waited for until the output)
-    // the runs with products, in order (entries selecting empty B rows dropped:
-    // fewer runs, fewer rounds); their offsets by a scan of the B row lengths,
-    // so the table needs only the entries' own loads
-    int k = 0, P = 0;
-    for (int jb = 0; jb < ka; jb += NT) {  // (workgroup-uniform)
-        const int j = jb + tid;
-        int2 be = make_int2(0, 0);
-        double av = 0.0;
-        if (j < ka) {
-            be = g.ebnd[a0 + j];
-            av = g.vA[a0 + j];
-        }
-        const int len = be.y - be.x;
-        const u64 b = __ballot(len > 0);
-        const int inc = wave_incl_scan_dpp(len);
-        if (lane == 63) {
-            red[wv] = __popcll(b);
-            red[NW + wv] = inc;
-        }
-        __syncthreads();
-        int off = k, tot = 0, loff = P, ltot = 0;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) {
-            off += w < wv ? red[w] : 0;
-            tot += red[w];
-            loff += w < wv ? red[NW + w] : 0;
-            ltot += red[NW + w];
-        }
-        if (len > 0) {
-            const int d = off + lanes_below(b);
-            roff[d] = loff + inc - len;
-            rbs[d] = be.x;
-            rav[d] = av;
-        }
-        k += tot;
-        P += ltot;
-        __syncthreads();
+    int2 be = make_int2(0, 0);
+    double av = 0.0;
+    if (tid < le.z) {
+        be = g.ebnd[le.y + tid];
+        av = g.vA[le.y + tid];
     }
-    if (tid == 0) roff[k] = P;
-    __syncthreads();
-    RP(0);
-    // expansion: wave w takes positions [256w, 256w + 256), lane l the four at
-    // e0 = 256w + 4l (mostly one run's neighbours); position q of run j at
-    // roff[j] + t -> column, payload (j, t)
-    constexpr int SEG = 256;
-    static_assert(CAP == 4 * NT, "four positions per thread");
-    const int e0 = wv * SEG + 4 * lane, ne = max(0, min(4, P - e0));
-    int c[4];
-    u32 py[4];
+    const long long base = g.E[le.y];  // (the staging offset: not waited for until the output)
+    double *const V = reinterpret_cast<double *>(kp[1][0]);
     {
-        int j = 0;
-        if (ne > 0) j = lower_bound_dev(roff, 0, k + 1, e0 + 1) - 1;  // the last run starting at or before e0
-        int pa[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (u < ne) {
-                const int q = e0 + u;
-                while (roff[j + 1] <= q) ++j;
-                pa[u] = rbs[j] + q - roff[j];
-                py[u] = ((u32)j << 16) | (u32)(q - roff[j]);
+        const int r = le.x;
+        // the runs with products, in order (entries selecting empty B rows
+        // dropped: fewer runs); their offsets by a scan of the B row lengths
+        int k = 0, P = 0;
+        {
+            const int len = be.y - be.x;
+            const u64 b = __ballot(len > 0);
+            const int inc = wave_incl_scan_dpp(len);
+            if (lane == 63) {
+                red[wv] = __popcll(b);
+                red[NW + wv] = inc;
             }
+            __syncthreads();
+            int off = 0, loff = 0;
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (u < ne) c[u] = g.Bcol[pa[u]];
-    }
-    // the row's column span [clo, chi]
-    int clo = INT_MAX, chi = -1;
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-        if (u < ne) {
-            clo = min(clo, c[u]);
-            chi = max(chi, c[u]);
-        }
-    clo = wave_last(wave_incl_dpp(clo, INT_MAX, OpMin{}));
-    chi = wave_last(wave_incl_dpp(chi, INT_MIN, OpMax{}));
-    if (lane == 0) {
-        red[wv] = clo;
-        red[NW + wv] = chi;
-    }
-    __syncthreads();
-    clo = red[0];
-    chi = red[NW];
-#pragma unroll
-    for (int w = 1; w < NW; ++w) {
-        clo = min(clo, red[w]);
-        chi = max(chi, red[NW + w]);
-    }
-    // (strict: the largest packed key stays below the ~0u padding)
-    const bool packed = (u32)(chi - clo) < (1u << (32 - IB)) - 1u;  // (workgroup-uniform)
-    int npow = SEG;  // the packed sort's length: P padded to a power of two (with ~0u keys)
-    while (npow < P) npow <<= 1;
-    u32 *const K0 = kp[0][0], *const X = kp[0][1], *const PY = kp[1][1];
-    u32 x[4];  // packed: this lane's four keys
-    if (packed) {
-        // each wave sorts its 256 positions in registers: the merge rounds
-        // start from sorted segments of 256 instead of the B rows' short runs
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            x[u] = u < ne ? ((u32)(c[u] - clo) << IB) | (u32)(e0 + u) : ~0u;
-            if (u < ne) PY[e0 + u] = py[u];
-        }
-        if (wv * SEG < P) wave_sort256(x, lane);  // (wave-uniform)
-        if (wv * SEG < npow) *reinterpret_cast<uint4 *>(K0 + e0) = make_uint4(x[0], x[1], x[2], x[3]);
-    } else {
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (u < ne) {
-                K0[e0 + u] = (u32)c[u];
-                X[e0 + u] = py[u];
+            for (int w = 0; w < NW; ++w) {
+                off += w < wv ? red[w] : 0;
+                k += red[w];
+                loff += w < wv ? red[NW + w] : 0;
+                P += red[NW + w];
             }
-    }
-    __syncthreads();
-    RP(1);
-    int src = 0;  // the key buffer holding the (merged) keys: K0 or K1
-    if (packed) {
-        // the waves' sorted segments merged by the rest of a bitonic sort over
-        // npow keys, every sequence ascending: per level K the first stage pairs
-        // each position with its mirror in the K-block (e ^ (K-1)), the stages
-        // at distances K/4 .. 256 pair across waves through LDS (uint4 per
-        // lane, K0/K1 in turn, one barrier each), the last eight stay in
-        // registers.  Independent LDS reads instead of the merge rounds'
-        // dependent ones.
-        const bool act = wv * SEG < npow;  // (wave-uniform)
-        auto cmpx = [&](const uint4 y, bool rev, bool keep_min) {
-            const u32 yy[4] = {rev ? y.w : y.x, rev ? y.z : y.y, rev ? y.y : y.z, rev ? y.x : y.w};
-#pragma unroll
-            for (int u = 0; u < 4; ++u) x[u] = keep_min ? min(x[u], yy[u]) : max(x[u], yy[u]);
-        };
-        for (int K = 2 * SEG; K <= npow; K <<= 1) {  // (workgroup-uniform)
-            if (act) cmpx(*reinterpret_cast<const uint4 *>(kp[src][0] + (e0 ^ (K - 4))), true, (e0 & (K >> 1)) == 0);
-            for (int J = K >> 2; J >= SEG; J >>= 1) {
-                src ^= 1;
-                if (act) *reinterpret_cast<uint4 *>(kp[src][0] + e0) = make_uint4(x[0], x[1], x[2], x[3]);
-                __syncthreads();
-                if (act) cmpx(*reinterpret_cast<const uint4 *>(kp[src][0] + (e0 ^ J)), false, (e0 & J) == 0);
+            if (len > 0) {
+                const int d = off + lanes_below(b);
+                roff[d] = loff + inc - len;
+                rbs[d] = be.x;
+                rav[d] = av;
             }
-            if (act) bitonic_merge<256, 128>(x, lane);
-            src ^= 1;
-            if (act) *reinterpret_cast<uint4 *>(kp[src][0] + e0) = make_uint4(x[0], x[1], x[2], x[3]);
+            if (tid == 0) roff[k] = P;
             __syncthreads();
         }
-    }
-    // merge-path chunks: thread t owns [t*ipt, t*ipt + ipt) of every round
-    const int ipt = ((P + NT - 1) / NT) | 1;
-    const int q0 = min(P, tid * ipt), q1 = min(P, q0 + ipt), nq = q1 - q0;
-    // unpacked rows: merge rounds from the runs
-    const int *const bd = roff;
-    const int nb = packed ? 1 : k;
-    int j0 = 0;  // the group holding q0 (pairs keep their position ranges every round)
-    if (nq > 0 && !packed) j0 = lower_bound_dev(roff, 0, k + 1, q0 + 1) - 1;
-    // rounds: groups of 2^lw runs merged pairwise
-    for (int lw = 0; (1 << lw) < nb; ++lw) {
-        const u32 *ik = kp[src][0], *ip = kp[src][1];
-        u32 *ok = kp[src ^ 1][0], *op = kp[src ^ 1][1];
-        int pr = j0 >> (lw + 1);  // the pair holding q0
-        for (int q = q0; q < q1;) {
-            while (bd[min((pr + 1) << (lw + 1), nb)] <= q) ++pr;  // (pairs ending at or before q)
-            const int ps = bd[pr << (lw + 1)];
-            const int pm = bd[min((2 * pr + 1) << lw, nb)];
-            const int pe = bd[min((pr + 1) << (lw + 1), nb)];
-            const int la = pm - ps, lb = pe - pm, qq = q - ps;
-            int lo = max(0, qq - lb), hi = min(qq, la);
-            while (lo < hi) {
-                const int i = (lo + hi) >> 1;
-                if (ik[ps + i] <= ik[pm + qq - i - 1]) lo = i + 1; else hi = i;
-            }
-            int i = lo, j = qq - lo;
-            u32 ka = i < la ? ik[ps + i] : ~0u, kb = j < lb ? ik[pm + j] : ~0u;  // (keys < 2^32 - 1)
-            const int qe = min(q1, pe);
-            for (; q < qe; ++q) {  // one dependent LDS read per output
-                const bool ta = ka <= kb;
-                ok[q] = ta ? ka : kb;
-                if (!packed) op[q] = ta ? ps + i : pm + j;  // (the source position, for now)
-                i += ta;
-                j += !ta;
-                const u32 kn = ik[ta ? ps + i : pm + j];  // (an exhausted side reads a neighbour: masked)
-                const bool live = ta ? i < la : j < lb;
-                ka = ta ? (live ? kn : ~0u) : ka;
-                kb = ta ? kb : (live ? kn : ~0u);
-            }
-        }
-        if (!packed) {
+        RP(0);
+        // expansion: wave w takes positions [256w, 256w + 256), lane l the four at
+        // e0 = 256w + 4l (mostly one run's neighbours); position q of run j at
+        // roff[j] + t -> column, value, payload (j, t)
+        const int e0 = wv * SEG + 4 * lane, ne = max(0, min(4, P - e0));
+        int c[4] = {0, 0, 0, 0};
+        u32 py[4] = {0, 0, 0, 0};
+        double xv[4] = {0.0, 0.0, 0.0, 0.0};
+        {
+            int j = 0;
+            if (ne > 0) j = lower_bound_dev(roff, 0, k + 1, e0 + 1) - 1;  // the last run starting at or before e0
+            int pa[4] = {0, 0, 0, 0};
+            double ra[4] = {0.0, 0.0, 0.0, 0.0}, bv[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int u = 0; u < IPM; ++u)  // the payloads: independent reads
-                if (u < nq) op[q0 + u] = ip[op[q0 + u]];
+            for (int u = 0; u < 4; ++u)
+                if (u < ne) {
+                    const int q = e0 + u;
+                    while (roff[j + 1] <= q) ++j;
+                    pa[u] = rbs[j] + q - roff[j];
+                    py[u] = ((u32)j << 16) | (u32)(q - roff[j]);
+                    ra[u] = rav[j];
+                }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (u < ne) {
+                    c[u] = g.Bcol[pa[u]];
+                    bv[u] = g.Bval[pa[u]];
+                }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) xv[u] = u < ne ? ra[u] * bv[u] : 0.0;
+        }
+        // the row's column span [clo, chi]
+        int clo = INT_MAX, chi = -1;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (u < ne) {
+                clo = min(clo, c[u]);
+                chi = max(chi, c[u]);
+            }
+        clo = wave_last(wave_incl_dpp(clo, INT_MAX, OpMin{}));
+        chi = wave_last(wave_incl_dpp(chi, INT_MIN, OpMax{}));
+        if (lane == 0) {
+            red[wv] = clo;
+            red[NW + wv] = chi;
         }
         __syncthreads();
-        src ^= 1;
-    }
-    RP(2);
-    const u32 *sk = kp[src][0], *sp = kp[src][1];
-    // each position's product: packed -> into the free pair next to the final
-    // keys; unpacked -> into the free buffer
-    double *vb = reinterpret_cast<double *>(packed ? (src ? K0 : X) : kp[src ^ 1][0]);
-    const u32 cs = packed ? IB : 0;  // key >> cs = the column (- clo when packed)
-    int nh = 0;  // heads (first position of each column) in the chunk
-    // packed rows: the thread's four sorted keys are still in x[] (positions
-    // e0 .. e0 + 3), so only the key before them comes from LDS
-    const int np = packed ? max(0, min(4, P - e0)) : 0;
-    double xv[4];
-    u32 hd = 0;  // packed: head bits of the four positions
-    if (packed) {
-        const u32 prev = e0 > 0 && np > 0 ? sk[e0 - 1] : ~0u;
-        int pa[4];
-        double av[4];
+        clo = red[0];
+        chi = red[NW];
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (u < np) {
-                const u32 pj = PY[x[u] & (CAP - 1)];
-                const int ru = (int)(pj >> 16);
-                pa[u] = rbs[ru] + (int)(pj & 0xffffu);
-                av[u] = rav[ru];
-                const u32 pk = u ? x[u - 1] : prev;
-                hd |= (e0 + u == 0 || (x[u] >> IB) != (pk >> IB)) ? 1u << u : 0u;
+        for (int w = 1; w < NW; ++w) {
+            clo = min(clo, red[w]);
+            chi = max(chi, red[NW + w]);
+        }
+        // (strict: the largest packed key stays below the ~0u padding)
+        const bool packed = (u32)(chi - clo) < (1u << (32 - IB)) - 1u;  // (workgroup-uniform)
+        int npow = SEG;  // the packed sort's length: P padded to a power of two (with ~0u keys)
+        while (npow < P) npow <<= 1;
+        u32 x[4] = {~0u, ~0u, ~0u, ~0u};  // packed: this lane's four keys
+        if (packed) {
+            // each wave sorts its 256 positions in registers: the LDS stages
+            // start from sorted segments of 256
+#pragma unroll
+            for (int u = 0; u < 4; ++u) x[u] = u < ne ? ((u32)(c[u] - clo) << IB) | (u32)(e0 + u) : ~0u;
+            if (ne > 0) {
+                reinterpret_cast<double4 *>(V)[e0 >> 2] = make_double4(xv[0], xv[1], xv[2], xv[3]);
             }
+            if (wv * SEG < P) wave_sort256(x, lane);  // (wave-uniform)
+            if (wv * SEG < npow) *reinterpret_cast<uint4 *>(kp[0][0] + e0) = make_uint4(x[0], x[1], x[2], x[3]);
+        } else {
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (u < np) xv[u] = av[u] * g.Bval[pa[u]];
+            for (int u = 0; u < 4; ++u)
+                if (u < ne) {
+                    kp[0][0][e0 + u] = (u32)c[u];
+                    kp[0][1][e0 + u] = py[u];
+                }
+        }
+        __syncthreads();
+        RP(1);
+        int src = 0;  // packed: the key buffer holding the (merged) keys
+        if (packed) {
+            // the waves' sorted segments merged by the rest of a bitonic sort over
+            // npow keys, every sequence ascending: per level K the first stage pairs
+            // each position with its mirror in the K-block (e ^ (K-1)), the stages
+            // at distances K/4 .. 256 pair across waves through LDS (uint4 per
+            // lane, the two key buffers in turn, one barrier each), the last eight
+            // stay in registers.
+            const bool act = wv * SEG < npow;  // (wave-uniform)
+            auto cmpx = [&](const uint4 y, bool rev, bool keep_min) {
+                const u32 yy[4] = {rev ? y.w : y.x, rev ? y.z : y.y, rev ? y.y : y.z, rev ? y.x : y.w};
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (u < np) vb[e0 + u] = xv[u];
-        nh = __popc(hd);
-    } else {
-        int pa[IPM];
-        double av[IPM];
-#pragma unroll
-        for (int u = 0; u < IPM; ++u)
-            if (u < nq) {
-                const u32 key = sk[q0 + u];
-                const u32 pj = sp[q0 + u];
-                const int ru = (int)(pj >> 16);
-                pa[u] = rbs[ru] + (int)(pj & 0xffffu);
-                av[u] = rav[ru];
-                nh += (q0 + u == 0 || (key >> cs) != (sk[q0 + u - 1] >> cs));
-            }
-        double xx[IPM];
-#pragma unroll
-        for (int u = 0; u < IPM; ++u)
-            if (u < nq) xx[u] = av[u] * g.Bval[pa[u]];
-#pragma unroll
-        for (int u = 0; u < IPM; ++u)
-            if (u < nq) vb[q0 + u] = xx[u];
-    }
-    // the chunk's first output slot: exclusive scan of the head counts
-    const int inc = wave_incl_scan_dpp(nh);
-    if (lane == 63) red[wv] = inc;
-    __syncthreads();
-    RP(3);
-    int o = inc - nh, tot = 0;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) {
-        o += w < wv ? red[w] : 0;
-        tot += red[w];
-    }
-    if (tid == 0) g.rnnz[r] = tot;
-    if (packed) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (hd >> u & 1u) {
-                const u32 col = x[u] >> IB;
-                double sum = xv[u];
-                int j = u + 1;
-#pragma unroll
-                for (int v = u + 1; v < 4; ++v)  // (ascending, as below: deterministic)
-                    if (j == v && v < np && (x[v] >> IB) == col) {
-                        sum += xv[v];
-                        ++j;
-                    }
-                if (j == 4)
-                    for (int q = e0 + 4; q < P && (sk[q] >> IB) == col; ++q) sum += vb[q];
-                g.Scol[base + o] = (int)col + clo;
-                g.Sval[base + o] = sum;
-                ++o;
-            }
-    } else {
-        for (int q = q0; q < q1; ++q) {
-            const u32 col = sk[q] >> cs;
-            if (q == 0 || (sk[q - 1] >> cs) != col) {
-                double sum = vb[q];
-                for (int j = q + 1; j < P && (sk[j] >> cs) == col; ++j) sum += vb[j];  // ascending: deterministic
-                g.Scol[base + o] = (int)col;
-                g.Sval[base + o] = sum;
-                ++o;
+                for (int u = 0; u < 4; ++u) x[u] = keep_min ? min(x[u], yy[u]) : max(x[u], yy[u]);
+            };
+            for (int K = 2 * SEG; K <= npow; K <<= 1) {  // (workgroup-uniform)
+                if (act) cmpx(*reinterpret_cast<const uint4 *>(kp[0][src] + (e0 ^ (K - 4))), true, (e0 & (K >> 1)) == 0);
+                for (int J = K >> 2; J >= SEG; J >>= 1) {
+                    src ^= 1;
+                    if (act) *reinterpret_cast<uint4 *>(kp[0][src] + e0) = make_uint4(x[0], x[1], x[2], x[3]);
+                    __syncthreads();
+                    if (act) cmpx(*reinterpret_cast<const uint4 *>(kp[0][src] + (e0 ^ J)), false, (e0 & J) == 0);
+                }
+                if (act) bitonic_merge<256, 128>(x, lane);
+                src ^= 1;
+                if (act) *reinterpret_cast<uint4 *>(kp[0][src] + e0) = make_uint4(x[0], x[1], x[2], x[3]);
+                __syncthreads();
             }
         }
+        // unpacked rows: merge-path rounds from the runs; thread t owns
+        // [t*ipt, t*ipt + ipt) of every round
+        const int ipt = ((P + NT - 1) / NT) | 1;
+        const int q0 = min(P, tid * ipt), q1 = min(P, q0 + ipt), nq = q1 - q0;
+        if (!packed) {
+            const int *const bd = roff;
+            const int nb = k;
+            int j0 = 0;  // the group holding q0 (pairs keep their position ranges every round)
+            if (nq > 0) j0 = lower_bound_dev(roff, 0, k + 1, q0 + 1) - 1;
+            for (int lw = 0; (1 << lw) < nb; ++lw) {  // groups of 2^lw runs merged pairwise
+                const u32 *ik = kp[src][0], *ip = kp[src][1];
+                u32 *ok = kp[src ^ 1][0], *op = kp[src ^ 1][1];
+                int pr = j0 >> (lw + 1);  // the pair holding q0
+                for (int q = q0; q < q1;) {
+                    while (bd[min((pr + 1) << (lw + 1), nb)] <= q) ++pr;  // (pairs ending at or before q)
+                    const int ps = bd[pr << (lw + 1)];
+                    const int pm = bd[min((2 * pr + 1) << lw, nb)];
+                    const int pe = bd[min((pr + 1) << (lw + 1), nb)];
+                    const int la = pm - ps, lb = pe - pm, qq = q - ps;
+                    int lo = max(0, qq - lb), hi = min(qq, la);
+                    while (lo < hi) {
+                        const int t = (lo + hi) >> 1;
+                        if (ik[ps + t] <= ik[pm + qq - t - 1]) lo = t + 1; else hi = t;
+                    }
+                    int ia = lo, ib = qq - lo;
+                    u32 ka = ia < la ? ik[ps + ia] : ~0u, kbv = ib < lb ? ik[pm + ib] : ~0u;  // (keys < 2^32 - 1)
+                    const int qe = min(q1, pe);
+                    for (; q < qe; ++q) {  // one dependent LDS read per output
+                        const bool ta = ka <= kbv;
+                        ok[q] = ta ? ka : kbv;
+                        op[q] = ta ? ps + ia : pm + ib;  // (the source position, for now)
+                        ia += ta;
+                        ib += !ta;
+                        const u32 kn = ik[ta ? ps + ia : pm + ib];  // (an exhausted side reads a neighbour: masked)
+                        const bool live = ta ? ia < la : ib < lb;
+                        ka = ta ? (live ? kn : ~0u) : ka;
+                        kbv = ta ? kbv : (live ? kn : ~0u);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < IPM; ++u)  // the payloads: independent reads
+                    if (u < nq) op[q0 + u] = ip[op[q0 + u]];
+                __syncthreads();
+                src ^= 1;
+            }
+        }
+        RP(2);
+        // heads (first position of each column) and the values in sorted order
+        int nh = 0;
+        const int np = packed ? max(0, min(4, P - e0)) : 0;
+        double xs[4] = {0.0, 0.0, 0.0, 0.0};
+        u32 hd = 0;  // packed: head bits of the four positions
+        const u32 *const sk = packed ? kp[0][src] : kp[src][0];
+        double *const vb = reinterpret_cast<double *>(kp[src ^ 1][0]);  // unpacked: the free buffer
+        if (packed) {
+            const u32 prev = e0 > 0 && np > 0 ? sk[e0 - 1] : ~0u;
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (u < np) {
+                    xs[u] = V[x[u] & (CAP - 1)];
+                    const u32 pk = u ? x[u - 1] : prev;
+                    hd |= (e0 + u == 0 || (x[u] >> IB) != (pk >> IB)) ? 1u << u : 0u;
+                }
+            nh = __popc(hd);
+        } else {
+            const u32 *sp = kp[src][1];
+            int pa[IPM] = {};
+            double ra[IPM] = {};
+#pragma unroll
+            for (int u = 0; u < IPM; ++u)
+                if (u < nq) {
+                    const u32 key = sk[q0 + u];
+                    const u32 pj = sp[q0 + u];
+                    const int ru = (int)(pj >> 16);
+                    pa[u] = rbs[ru] + (int)(pj & 0xffffu);
+                    ra[u] = rav[ru];
+                    nh += (q0 + u == 0 || key != sk[q0 + u - 1]);
+                }
+            double xx[IPM] = {};
+#pragma unroll
+            for (int u = 0; u < IPM; ++u)
+                if (u < nq) xx[u] = ra[u] * g.Bval[pa[u]];
+#pragma unroll
+            for (int u = 0; u < IPM; ++u)
+                if (u < nq) vb[q0 + u] = xx[u];
+        }
+        // the chunk's first output slot: exclusive scan of the head counts
+        const int inc = wave_incl_scan_dpp(nh);
+        if (lane == 63) red[wv] = inc;
+        __syncthreads();
+        RP(3);
+        int o = inc - nh, tot = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            o += w < wv ? red[w] : 0;
+            tot += red[w];
+        }
+        if (tid == 0) g.rnnz[r] = tot;
+        if (packed) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (hd >> u & 1u) {
+                    const u32 col = x[u] >> IB;
+                    double sum = xs[u];
+                    int j = u + 1;
+#pragma unroll
+                    for (int v = u + 1; v < 4; ++v)  // (ascending, as below: deterministic)
+                        if (j == v && v < np && (x[v] >> IB) == col) {
+                            sum += xs[v];
+                            ++j;
+                        }
+                    if (j == 4)
+                        for (int q = e0 + 4; q < P && (sk[q] >> IB) == col; ++q) sum += V[sk[q] & (CAP - 1)];
+                    g.Scol[base + o] = (int)col + clo;
+                    g.Sval[base + o] = sum;
+                    ++o;
+                }
+        } else {
+            for (int q = q0; q < q1; ++q) {
+                const u32 col = sk[q];
+                if (q == 0 || sk[q - 1] != col) {
+                    double sum = vb[q];
+                    for (int j = q + 1; j < P && sk[j] == col; ++j) sum += vb[j];  // ascending: deterministic
+                    g.Scol[base + o] = (int)col;
+                    g.Sval[base + o] = sum;
+                    ++o;
+                }
+            }
+        }
+        RP(4);
     }
-    RP(4);
     RP_DONE(CAP <= M1_CAP ? 2 : 1);  // (M0, M1 | M2..M4)
 }
 
@@ -1082,16 +1086,25 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
         TSG_HIP(hipGetLastError());
         return TSG_OK;
     };
+    auto launch_m = [&](int c, auto kern, int grid, int nt, hipStream_t st) -> int {
+        if (ncls[c] == 0) return TSG_OK;
+        g.list = lists + (long)c * m;
+        g.nrows = ncls[c];
+        kern<<<grid, nt, 0, st>>>(g);
+        TSG_HIP(hipGetLastError());
+        return TSG_OK;
+    };
+    // the merge classes are persistent: one resident wave of workgroups
     if (ncls[7] >= 2 && ncls[7] <= OH_MAX && !getenv("TSG_ROWS_H_ROWORDER")) {
         k_rows_order_h<<<1, OH_NT, 0, s>>>(E, p.cls, lists + (long)(NCLS - 1) * m);
         TSG_HIP(hipGetLastError());
     }
     TSG_TRY(launch(7, k_rows_bitmap, ncls[7], RH_NT, s));
-    TSG_TRY(launch(6, k_rows_merge<M4_NT, M4_CAP, M4_RUNS>, ncls[6], M4_NT, s));
-    TSG_TRY(launch(5, k_rows_merge<M3_NT, M3_CAP, M3_RUNS>, ncls[5], M3_NT, s));
-    TSG_TRY(launch(4, k_rows_merge<M2_NT, M2_CAP, M2_RUNS>, ncls[4], M2_NT, s));
-    TSG_TRY(launch(3, k_rows_merge<M1_NT, M1_CAP, M1_RUNS>, ncls[3], M1_NT, s));
-    TSG_TRY(launch(2, k_rows_merge<M0_NT, M0_CAP, M0_RUNS>, ncls[2], M0_NT, s));
+    TSG_TRY(launch_m(6, k_rows_merge<M4_NT, M4_CAP, M4_RUNS>, ncls[6], M4_NT, s));
+    TSG_TRY(launch_m(5, k_rows_merge<M3_NT, M3_CAP, M3_RUNS>, ncls[5], M3_NT, s));
+    TSG_TRY(launch_m(4, k_rows_merge<M2_NT, M2_CAP, M2_RUNS>, ncls[4], M2_NT, s));
+    TSG_TRY(launch_m(3, k_rows_merge<M1_NT, M1_CAP, M1_RUNS>, ncls[3], M1_NT, s));
+    TSG_TRY(launch_m(2, k_rows_merge<M0_NT, M0_CAP, M0_RUNS>, ncls[2], M0_NT, s));
     TSG_TRY(launch(1, k_rows_small<64>, (ncls[1] + WAVES - 1) / WAVES, WG, s));
     TSG_TRY(launch(0, k_rows_small<16>, (ncls[0] + 4 * WAVES - 1) / (4 * WAVES), WG, s));
     if (ev) TSG_HIP(hipEventRecord(ev[5], s));
