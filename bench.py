@@ -89,53 +89,82 @@ def _cpu_model():
     return "unknown"
 
 
-def _timed_prefix(fn, m, budget_s, max_rows=None):
-    """Run fn(rows) on a growing row prefix until it takes ~budget_s; (rows, seconds).
-    max_rows caps the prefix (a sample whose C must fit int32 row pointers)."""
-    cap = m if max_rows is None else max(1, min(m, max_rows))
-    rows = min(cap, 2000)
+def _strided_rows(m, rp, ci, vv, stride):
+    """Rows 0, stride, 2*stride, ... of a CSR as a standalone CSR (a row sample
+    that keeps the per-row cost distribution of the whole matrix)."""
+    rows = np.arange(0, m, max(1, int(stride)), dtype=np.int64)
+    rp64 = rp.astype(np.int64)
+    lens = rp64[rows + 1] - rp64[rows]
+    rps = np.concatenate([[0], np.cumsum(lens)])
+    idx = np.repeat(rp64[rows] - rps[:-1], lens) + np.arange(int(rps[-1]), dtype=np.int64)
+    return len(rows), rps.astype(np.int32), ci[idx], vv[idx]
+
+
+def _timed_sample(fn, m, rp, ci, vv, rpb, budget_s):
+    """fn(A sample) timed on the whole A when a probe predicts it fits budget_s,
+    else on a strided row sample sized to it ("time a strided
+    row sample and extrapolate"); (stride, products of the sample, seconds)."""
+    blen = np.diff(rpb.astype(np.int64))
+    probe = max(1, m // 2000)
+    sub = _strided_rows(m, rp, ci, vv, probe)
     t0 = time.perf_counter()
-    fn(rows)
+    fn(*sub)
     t = time.perf_counter() - t0
-    rows2 = int(min(cap, max(rows, rows * budget_s / max(t, 1e-6))))
-    t0 = time.perf_counter()
-    fn(rows2)
-    return rows2, time.perf_counter() - t0
+    stride = probe
+    while True:  # (small samples overestimate: fixed per-call costs) -- refine once or twice
+        est_full = t * stride
+        nxt = 1 if est_full <= budget_s else int(np.ceil(est_full / budget_s))
+        if nxt >= stride and stride != probe:
+            break
+        stride = min(nxt, stride)
+        sub = _strided_rows(m, rp, ci, vv, stride) if stride > 1 else (m, rp, ci, vv)
+        t0 = time.perf_counter()
+        fn(*sub)
+        t = time.perf_counter() - t0
+        if stride == 1:
+            break
+    return stride, int(blen[sub[2]].sum()), t
 
 
 def cpu_baseline(m, n, rp, ci, vv, mb, nb, rpb, cib, vvb, budget_s):
     """The reference's CPU SPA (spgemm_serialref_spa_new.h, clean-room oracle
-    restatement, both passes; symbolic only) on a bounded row prefix of the same
-    workload, plus the oracle's numeric Gustavson timed beside it."""
+    restatement, both passes; symbolic only) on the same workload -- whole when it
+    fits the budget, else a strided row sample marked "extrapolated" -- plus the
+    oracle's numeric Gustavson timed beside it."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import _oracle as O
-    A = O.OMat.from_csr(m, n, rp, ci, vv)
     B = O.OMat.from_csr(mb, nb, rpb, cib, vvb)
-    # the SPA sample holds its symbolic C (int32 row pointers, 4 B per column):
-    # rows whose intermediate products stay <= 2e8 (an upper bound of their nnz(C))
-    blen = np.diff(rpb.astype(np.int64))
-    cum = np.concatenate([[0], np.cumsum(blen[ci])])[rp]
-    max_rows = int(np.searchsorted(cum, 2e8, side="right") - 1)
-    rows, t = _timed_prefix(lambda r: O.spa(A, B, 0, r), m, budget_s, max_rows)
-    cub = nnzcub_rows(rp, ci, rpb, 0, rows)
-    nrows, nt = _timed_prefix(lambda r: O.gustavson_rows(A, B, 0, r), m, budget_s / 2)
-    ncub = nnzcub_rows(rp, ci, rpb, 0, nrows)
+
+    def spa(mm, r, c, v):
+        A = O.OMat.from_csr(mm, n, r, c, v)
+        O.spa(A, B, 0, mm)
+
+    def gus(mm, r, c, v):
+        A = O.OMat.from_csr(mm, n, r, c, v)
+        O.gustavson_rows(A, B, 0, mm)
+
+    stride, cub, t = _timed_sample(spa, m, rp, ci, vv, rpb, budget_s)
+    nstride, ncub, nt = _timed_sample(gus, m, rp, ci, vv, rpb, budget_s / 2)
     thr = O.num_threads()
     nproc = os.cpu_count()
     affinity = _AFFINITY
-    # cores actually available to the threads: the OpenMP team, capped by the
-    # process's CPU affinity mask (a lease may expose fewer CPUs than nproc)
+    # threads actually used: the OpenMP team (OMP_NUM_THREADS, which the GPU pool
+    # sets to the box's CPU share per GPU), capped by the process's affinity mask
     cores = min(thr, affinity) if affinity else thr
+
+    def what(st):
+        return ("all rows" if st == 1 else
+                f"extrapolated from a strided sample: every {st}-th row ({100.0 / st:.2g} % of the rows)")
     return {"value": round(2.0 * cub / t / 1e9, 4), "unit": "GFLOPS", "cores": cores, "omp_threads": thr,
             "nproc": nproc, "affinity_cpus": affinity,
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
-            "kind": "port",
-            "sample": f"spgemm_spa restatement (count+fill passes, symbolic), rows [0,{rows}) of {m} "
-                      f"({cub} of the intermediate products), {t:.1f} s; {thr} OpenMP threads on {cores} "
-                      f"usable CPU(s) of {nproc} (affinity mask; OMP_PROC_BIND="
+            "kind": "port", "extrapolated": stride > 1,
+            "sample": f"spgemm_spa restatement (count+fill passes, symbolic), {what(stride)} of {m} "
+                      f"({cub} intermediate products), {t:.1f} s; {thr} OpenMP threads on {cores} "
+                      f"usable CPU(s) of {nproc} (affinity mask {affinity}; OMP_PROC_BIND="
                       f"{os.environ.get('OMP_PROC_BIND', 'unset')}) on {_cpu_model()}",
-            "numeric": {"value": round(2.0 * ncub / nt / 1e9, 4), "unit": "GFLOPS",
-                        "sample": f"oracle Gustavson (dense-row accumulator, fp64 values), rows [0,{nrows}), "
+            "numeric": {"value": round(2.0 * ncub / nt / 1e9, 4), "unit": "GFLOPS", "extrapolated": nstride > 1,
+                        "sample": f"oracle Gustavson (dense-row accumulator, fp64 values), {what(nstride)}, "
                                   f"{nt:.1f} s"}}
 
 
@@ -210,6 +239,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", action="store_true",
                     help="add a checksum of the (gathered) C of the last step to the JSON line")
+    ap.add_argument("--dump", default=None,
+                    help="rank 0 saves the (gathered) C of the last step as an .npz (rowptr, col, val), "
+                         "outside the timed region (array-level parity tests)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N>1 (nccl = RCCL over xGMI; gloo = host-staged "
                          "rehearsal of the multi-rank path, e.g. several ranks on one GPU)")
@@ -342,6 +374,17 @@ def main():
         nnzC = int(nz.item())
     else:
         nnzC = nnz_rank
+    work_share = None
+    if dist:
+        # each rank's share of the intermediate products (its rows' work) and the
+        # max/mean imbalance of the partition
+        w = torch.tensor([float(cum[r_hi] - cum[r_lo])], dtype=torch.float64, device=red_dev)
+        allw = [torch.zeros_like(w) for _ in range(world)]
+        dist.all_gather(allw, w)
+        ws = [float(x.item()) for x in allw]
+        mean = sum(ws) / world
+        work_share = {"products": [int(x) for x in ws],
+                      "max_over_mean": round(max(ws) / mean, 4) if mean > 0 else None}
     ms_per_step = elapsed * 1e3 / args.steps
     gflops = 2.0 * nnzcub_total * args.steps / elapsed / 1e9
 
@@ -408,6 +451,14 @@ def main():
         else:
             chk = acc
             chk[1] += off
+    if args.dump and world == 1 and not blocked:
+        ctx.reset()
+        cb, _ = ctx.spgemm(dA_blocks[0][2], dB, tm, tm)
+        g_rp, g_ci, g_vv = ctx.to_host(cb)[2:]
+        np.savez(args.dump, rowptr=g_rp, col=g_ci, val=g_vv)
+    elif args.dump and gather and rank == 0:
+        g_rp, g_ci, g_vv = (x.cpu().numpy() for x in gathered[0])
+        np.savez(args.dump, rowptr=g_rp, col=g_ci, val=g_vv)
     tiled = None
     want_tiled = args.tiled if args.tiled is not None else (world == 1 and nnzcub_full <= 4e8)
     if want_tiled and rank == 0 and world == 1:
@@ -458,6 +509,7 @@ def main():
                                                         "t_kern_ms", "t_e2e_ms")},
             "stage_ms_min": {k: round(v, 4) for k, v in mins.items()},
             "gather_ms": round(float(np.median(gather_ms[-args.steps:])), 4) if gather_ms else None,
+            "work_share": work_share,
             "gflops_kern": round(2.0 * nnzcub_total / (med["t_kern_ms"] * 1e-3) / 1e9, 3) if world == 1 else None,
             "tiled": tiled,
             "cpu_baseline": cpu,

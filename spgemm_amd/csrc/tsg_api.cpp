@@ -89,7 +89,7 @@ int Context::init(int dev) {
     device = dev;
     TSG_HIP(hipSetDevice(dev));
     TSG_HIP(hipHostMalloc((void **)&pinned, 64, hipHostMallocDefault));
-    TSG_HIP(hipHostMalloc((void **)&pinned64, 64, hipHostMallocDefault));
+    TSG_HIP(hipHostMalloc((void **)&pinned64, 256, hipHostMallocDefault));
     for (auto &e : ev) TSG_HIP(hipEventCreate(&e));
     ev_ready = true;
     return TSG_OK;

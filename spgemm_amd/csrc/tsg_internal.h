@@ -155,11 +155,15 @@ struct RowsPlan {
     int *rowpointer = nullptr; // C's row pointers (row counts until the scan)
     int ncls[8] = {};
     long long products = 0, hprod = 0, pmax = 0;  // all / class-H rows' products, the longest row's
+    long long drprod = 0, hubrest = 0;  // hub rows' products: one run dominant (DR kernels) / not
 };
-// Unless forced, the path declines (dev_rows_accept false) products whose
-// class-H rows (> 4,096 products or > 512 runs) hold over a quarter of the work
-// or with a row over kRowsMaxRowProducts products.
-constexpr long long kRowsMaxRowProducts = 65536;
+// Class-H rows past kRowsHubProducts products are hub rows: one run holding all
+// but 4,096 of them -> the dominant-run kernels (k_rows_dr_*), else the windowed
+// kernel (k_rows_hwin); the shorter ones take the one-window bitmap kernel
+// (k_rows_bitmap).  Unless forced, the path declines (dev_rows_accept false)
+// products with hub rows of the second kind, or whose bitmap-kernel rows hold
+// over a quarter of the work.
+constexpr long long kRowsHubProducts = 65536;
 int dev_rows_setup_async(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPlan &p, hipStream_t s);
 void dev_rows_setup_read(Context &cx, RowsPlan &p);  // after the stream synchronised
 bool dev_rows_accept(const RowsPlan &p);

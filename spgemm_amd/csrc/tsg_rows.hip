@@ -49,6 +49,8 @@ constexpr int M2_CAP = 1024, M2_RUNS = 248, M2_NT = 256;   // 20,400 B
 constexpr int M3_CAP = 2048, M3_RUNS = 504, M3_NT = 512;   // 40,912 B
 constexpr int M4_CAP = 4096, M4_RUNS = 512, M4_NT = 1024;  // 72 KB
 constexpr int NCLS = 8;               // S16, S64, M0..M4, H
+constexpr int DR_SMAX = 4096;         // hub rows: products outside the dominant run (the DR kernels)
+constexpr int DR_CH = 65536;          // DR fill: dominant-run elements per workgroup
 constexpr int BIN_ROWS = 2048;        // rows per workgroup of the binning kernel
 constexpr int RH_NT = 1024;           // class H: workgroup
 constexpr int RH_WORDS = 16384;       // class H: bitmap words (u64) per window: 128 KB of LDS
@@ -108,7 +110,7 @@ struct RowsArgs {
 // (also zeroes the binning kernel's counters: no separate memset in the stream)
 __global__ __launch_bounds__(WG) void k_rows_entries(const int *ciA, long nnzA, const int *rpB, int2 *ebnd,
                                                      long long *E, int *cls) {
-    if (blockIdx.x == 0 && threadIdx.x < 14) cls[threadIdx.x] = 0;
+    if (blockIdx.x == 0 && threadIdx.x < 24) cls[threadIdx.x] = 0;  // (class counts, statistics, cursors)
     for (long a = (long)blockIdx.x * WG + threadIdx.x; a <= nnzA; a += (long)gridDim.x * WG) {
         if (a == nnzA) {
             E[a] = 0;
@@ -134,7 +136,9 @@ __device__ __forceinline__ int row_class(long long P, int k) {
 
 // rows -> classes: lists (class c's rows from lists + c*m) and counts cls[0..NCLS);
 // rows without products get nnz 0; hst[0] = the class-H rows' products, hst[1]
-// = the largest row's products (the routing statistics), hst[2] = all products
+// = the largest row's products (the routing statistics), hst[2] = all products,
+// hst[3] / hst[4] = the products of hub rows (past kRowsHubProducts) that one
+// run dominates (all but DR_SMAX products in it) / that none does
 // (*Etot, copied so that one read-back brings everything); rnnz[m] = 0 (the
 // row pointers' n+1 slot).  A workgroup per
 // BIN_ROWS rows: its counts first (one atomic per class), then its rows in
@@ -153,7 +157,7 @@ __global__ __launch_bounds__(WG) void k_rows_bin(const int *rpA, int m, const lo
         rnnz[m] = 0;
     }
     int n[NCLS] = {};
-    long long hp = 0, pmax = 0;
+    long long hp = 0, pmax = 0, drp = 0, hubr = 0;
     constexpr int RPT = BIN_ROWS / WG;  // rows per thread: every load of a sweep issued together
     int ra0[RPT], ra1[RPT];
 #pragma unroll
@@ -181,8 +185,15 @@ __global__ __launch_bounds__(WG) void k_rows_bin(const int *rpA, int m, const lo
         for (int t = 0; t < NCLS; ++t) n[t] += c == t;
         hp += c == NCLS - 1 ? P : 0;
         pmax = max(pmax, P);
+        if (P > kRowsHubProducts) {  // a hub row: dominated by one run (-> the DR kernels) or not
+            long long lmax = 0;
+            for (int a = ra0[u]; a < ra1[u]; ++a) lmax = max(lmax, E[a + 1] - E[a]);
+            if (P - lmax <= DR_SMAX) drp += P; else hubr += P;
+        }
     }
     hp = block_sum(hp, red64);
+    drp = block_sum(drp, red64);
+    hubr = block_sum(hubr, red64);
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) pmax = max(pmax, __shfl_xor(pmax, d, 64));
     if (lane == 0) red64[wv] = pmax;
@@ -191,6 +202,8 @@ __global__ __launch_bounds__(WG) void k_rows_bin(const int *rpA, int m, const lo
         for (int w = 1; w < WAVES; ++w) pmax = max(pmax, red64[w]);
         if (hp) atomicAdd(&hst[0], (unsigned long long)hp);
         if (pmax) atomicMax(&hst[1], (unsigned long long)pmax);
+        if (drp) atomicAdd(&hst[3], (unsigned long long)drp);
+        if (hubr) atomicAdd(&hst[4], (unsigned long long)hubr);
     }
 #pragma unroll
     for (int t = 0; t < NCLS; ++t) {
@@ -848,6 +861,11 @@ __device__ __forceinline__ int bm_rank(const u64 *bm, const u16 *g4, const int *
 }
 
 __global__ __launch_bounds__(RH_NT) void k_rows_bitmap(RowsArgs g) {
+    // (rows past kRowsHubProducts are k_rows_hwin's)
+    {
+        const int4 le0 = g.list[blockIdx.x];
+        if (g.E[le0.y + le0.z] - g.E[le0.y] > kRowsHubProducts) return;  // (workgroup-uniform)
+    }
     __shared__ __align__(16) u64 bm[RH_WORDS];
     __shared__ u16 g4[RH_NGRP];       // each 4-word group's bits before it in its block
     __shared__ int blk[RH_NBLK];      // each block's bits before it in the window
@@ -942,6 +960,565 @@ __global__ __launch_bounds__(RH_NT) void k_rows_bitmap(RowsArgs g) {
     RP_DONE(0);
 }
 
+// ---- class H, windowed: a workgroup per row, any length (web-graph heavy
+// rows, R-MAT and mawi hub rows alike).
+//   1. one walk over the row's products (runs in batches of HW_RUNS, flattened
+//      over the threads): each product's (column, a*b) stored in expansion
+//      order into the row's own staging slots (coalesced; the products bound
+//      the row's nonzeros, so the slots exist);
+//   2. the row's column span cut into buckets of 2^bs columns (at most
+//      HW_MAXB): a counting pass and a scatter pass over those slots (both
+//      streaming) gather each bucket's products into the row's region of a
+//      bucket area -- skipped when the span fits one window;
+//   3. each bucket in column order, as windows of 2^HW_WB columns: a bitmap of
+//      the window in LDS (its products' bits ORed in), ranks by popcount
+//      prefixes, the values added at their ranks in LDS (ds_add_f64), and the
+//      window's nonzeros emitted in column order at the row's running output
+//      offset -- no per-product global atomic, no second gather of B.
+// A window with more than HW_VCAP nonzeros takes its values in rank chunks of
+// HW_VCAP (one more streaming pass over the window's products per chunk).  The
+// bucket pass is skipped only for a row of one window and at most HW_VCAP
+// products, which then reads its slots and writes its output in place.
+constexpr int HW_NT = 1024;
+constexpr int HW_RUNS = 512;                    // runs per walk batch
+constexpr int HW_WB = 18;                       // window: 2^18 columns
+constexpr int HW_WORDS = (1 << HW_WB) / 64;     // 4,096 bitmap words: 32 KB
+constexpr int HW_BLK = 512;                     // words per rank block
+constexpr int HW_NBLK = HW_WORDS / HW_BLK;      // 8
+constexpr int HW_NGRP = HW_WORDS / 4;
+constexpr int HW_VCAP = 4096;                   // window nonzeros with LDS values: 32 KB
+constexpr int HW_MAXB = 256;                    // buckets per row
+
+__device__ __forceinline__ int hw_rank(const u64 *bm, const u16 *g4, const int *blk, int c) {
+    const int w = c >> 6, gi = w >> 2, sub = w & 3;
+    const ulonglong2 lo = reinterpret_cast<const ulonglong2 *>(bm)[gi * 2];
+    const ulonglong2 hi = reinterpret_cast<const ulonglong2 *>(bm)[gi * 2 + 1];
+    const u64 word = sub == 0 ? lo.x : sub == 1 ? lo.y : sub == 2 ? hi.x : hi.y;
+    int rk = blk[w / HW_BLK] + g4[gi] + __popcll(word & ((1ull << (c & 63)) - 1ull));
+    rk += sub > 0 ? __popcll(lo.x) : 0;
+    rk += sub > 1 ? __popcll(lo.y) : 0;
+    rk += sub > 2 ? __popcll(hi.x) : 0;
+    return rk;
+}
+
+// the longest run of a row (entries a0 .. a0+k, products from the prefix E)
+// and its entry (the first such), over the workgroup; red: 2 * (blockDim / 64) ints
+__device__ __forceinline__ long long row_longest_run(const long long *E, int a0, int k, int *jl, int *red) {
+    const int nw = blockDim.x >> 6, lane = lane_id(), wv = wave_id();
+    long long best = -1;
+    int bj = INT_MAX;
+    for (int j = threadIdx.x; j < k; j += blockDim.x) {
+        const long long len = E[a0 + j + 1] - E[a0 + j];
+        if (len > best) {
+            best = len;
+            bj = j;
+        }
+    }
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+        const long long ob = __shfl_xor(best, d, 64);
+        const int oj = __shfl_xor(bj, d, 64);
+        if (ob > best || (ob == best && oj < bj)) {
+            best = ob;
+            bj = oj;
+        }
+    }
+    __syncthreads();  // (red may hold an earlier phase's values)
+    if (lane == 0) {
+        red[2 * wv] = (int)min(best, (long long)INT_MAX);  // (a run is one B row: < 2^31)
+        red[2 * wv + 1] = bj;
+    }
+    __syncthreads();
+    best = -1;
+    bj = INT_MAX;
+    for (int w = 0; w < nw; ++w) {
+        const long long ob = red[2 * w];
+        const int oj = red[2 * w + 1];
+        if (ob > best || (ob == best && oj < bj)) {
+            best = ob;
+            bj = oj;
+        }
+    }
+    __syncthreads();
+    *jl = bj;
+    return best;
+}
+
+struct HwTab {
+    int pre[HW_RUNS];     // products before each run of the batch
+    int bs[HW_RUNS];      // B start
+    double av[HW_RUNS];   // A value
+    int red[HW_NT / 64];
+    int tot;
+};
+
+__global__ __launch_bounds__(HW_NT, 8) void k_rows_hwin(RowsArgs g, int *Tcol, double *Tval,
+                                                     unsigned long long *tnext) {
+    constexpr int NW = HW_NT / 64;
+    __shared__ __align__(16) u64 bm[HW_WORDS];
+    __shared__ u16 g4[HW_NGRP];
+    __shared__ int blk[HW_NBLK];
+    __shared__ __align__(16) double vals[HW_VCAP];
+    __shared__ HwTab tb;
+    __shared__ int bcnt[HW_MAXB + 1];   // per bucket: products, then (scanned) first slot
+    __shared__ int bcur[HW_MAXB];       // scatter cursors
+    __shared__ int red[2 * NW];
+    __shared__ long long s_toff;
+    RP_INIT
+    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    const int4 le = g.list[blockIdx.x];
+    const int r = le.x, a0 = le.y, k = le.z;
+    const long long base = g.E[a0];
+    const int P = (int)(g.E[a0 + k] - base);
+    if (P <= kRowsHubProducts) return;  // (k_rows_bitmap's row; workgroup-uniform)
+    {
+        int jl;
+        const long long lmax = row_longest_run(g.E, a0, k, &jl, red);
+        if (P - lmax <= DR_SMAX) return;  // (the DR kernels' row)
+    }
+    int *const Acol = g.Scol + base;  // the row's staging slots: expansion-order products, then its output
+    double *const Aval = g.Sval + base;
+    // the row's columns [lo, hi] (each run's first and last)
+    int lo = INT_MAX, hi = -1;
+    for (int j = tid; j < k; j += HW_NT) {
+        const int2 be = g.ebnd[a0 + j];
+        if (be.y > be.x) {
+            lo = min(lo, g.Bcol[be.x]);
+            hi = max(hi, g.Bcol[be.y - 1]);
+        }
+    }
+    lo = wave_last(wave_incl_dpp(lo, INT_MAX, OpMin{}));
+    hi = wave_last(wave_incl_dpp(hi, INT_MIN, OpMax{}));
+    if (lane == 0) {
+        red[wv] = lo;
+        red[NW + wv] = hi;
+    }
+    __syncthreads();
+    lo = red[0];
+    hi = red[NW];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {
+        lo = min(lo, red[w]);
+        hi = max(hi, red[NW + w]);
+    }
+    // 1. the walk: every product's (column, a*b) into the row's slots, in expansion order
+    {
+        constexpr int U = 4;
+        int qb = 0;  // products of the earlier batches
+        for (int b0 = 0; b0 < k; b0 += HW_RUNS) {  // (workgroup-uniform)
+            __syncthreads();  // (the previous batch's table reads done)
+            {
+                const int j = b0 + tid;
+                int2 be = make_int2(0, 0);
+                double av = 0.0;
+                if (tid < HW_RUNS && j < k) {
+                    be = g.ebnd[a0 + j];
+                    av = g.vA[a0 + j];
+                }
+                const int len = be.y - be.x;
+                const int inc = wave_incl_scan_dpp(len);
+                if (lane == 63) tb.red[wv] = inc;
+                __syncthreads();
+                int woff = 0, tot = 0;
+#pragma unroll
+                for (int w = 0; w < NW; ++w) {
+                    const int v = tb.red[w];
+                    woff += w < wv ? v : 0;
+                    tot += v;
+                }
+                if (tid < HW_RUNS) {
+                    tb.pre[tid] = woff + inc - len;
+                    tb.bs[tid] = be.x;
+                    tb.av[tid] = av;
+                }
+                if (tid == 0) tb.tot = tot;
+                __syncthreads();
+            }
+            const int nb = min(HW_RUNS, k - b0), tot = tb.tot;
+            for (int q0 = 0; q0 < tot; q0 += U * HW_NT) {
+                int b[U], len2[U], q[U];
+                int c[U] = {0, 0, 0, 0};
+                double x[U] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    q[u] = q0 + u * HW_NT + tid;
+                    b[u] = 0;
+                    len2[u] = q[u] < tot ? nb : 0;
+                }
+                const bool ub[U] = {true, true, true, true};
+                search_ilp(tb.pre, b, len2, q, ub);  // b - 1 = the run holding product q
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (q[u] < tot) {
+                        const int pp = tb.bs[b[u] - 1] + q[u] - tb.pre[b[u] - 1];
+                        c[u] = g.Bcol[pp];
+                        x[u] = tb.av[b[u] - 1] * g.Bval[pp];
+                    }
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (q[u] < tot) {
+                        Acol[qb + q[u]] = c[u];
+                        Aval[qb + q[u]] = x[u];
+                    }
+            }
+            qb += tot;
+        }
+    }
+    __syncthreads();  // (the slots written: read back by this workgroup only)
+    RP(0);
+    // 2. buckets of 2^bsh columns (bsh >= HW_WB, at most HW_MAXB of them)
+    const long long span = (long long)hi - lo + 1;
+    int bsh = HW_WB;
+    while (bsh < 31 && (span + (1ll << bsh) - 1) >> bsh > HW_MAXB) ++bsh;
+    const int nbk = P > 0 ? (int)((span + (1ll << bsh) - 1) >> bsh) : 0;
+    const int *Bkc = Acol;     // the bucketed products (in place: the slots themselves)
+    const double *Bkv = Aval;
+    if (nbk > 1 || P > HW_VCAP) {
+        for (int i = tid; i <= HW_MAXB; i += HW_NT) bcnt[i] = 0;
+        if (tid == 0) s_toff = (long long)atomicAdd(tnext, (unsigned long long)P);
+        __syncthreads();
+        for (int q = tid; q < P; q += HW_NT) atomicAdd(&bcnt[(Acol[q] - lo) >> bsh], 1);
+        __syncthreads();
+        if (wv == 0) {  // exclusive scan of the (<= 256) bucket counts, four per lane
+            int v[4], sum = 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                v[u] = 4 * lane + u < nbk ? bcnt[4 * lane + u] : 0;
+                sum += v[u];
+            }
+            const int inc = wave_incl_scan_dpp(sum);
+            int run = inc - sum;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (4 * lane + u < nbk) {
+                    bcnt[4 * lane + u] = run;
+                    bcur[4 * lane + u] = run;
+                }
+                run += v[u];
+            }
+            if (lane == 63) bcnt[nbk] = inc;
+        }
+        __syncthreads();
+        const long long toff = s_toff;
+        for (int q = tid; q < P; q += HW_NT) {
+            const int c = Acol[q];
+            const int d = atomicAdd(&bcur[(c - lo) >> bsh], 1);
+            Tcol[toff + d] = c;
+            Tval[toff + d] = Aval[q];
+        }
+        __syncthreads();  // (the bucket area read back by this workgroup only)
+        Bkc = Tcol + toff;
+        Bkv = Tval + toff;
+    } else if (tid == 0) {
+        bcnt[0] = 0;
+        bcnt[1] = P;
+    }
+    __syncthreads();
+    RP(1);
+    // 3. the buckets in column order, each as windows of 2^HW_WB columns
+    long long out = 0;  // the row's nonzeros so far
+    for (int bk = 0; bk < nbk; ++bk) {  // (workgroup-uniform)
+        const int s0 = bcnt[bk], s1 = bcnt[bk + 1];
+        if (s1 == s0) continue;
+        const long long blo = (long long)lo + ((long long)bk << bsh);
+        const long long bhi = min((long long)hi, blo + (1ll << bsh) - 1);
+        for (long long wlo = blo; wlo <= bhi; wlo += 1ll << HW_WB) {  // (workgroup-uniform)
+            const int nwd = (int)((min(bhi, wlo + (1ll << HW_WB) - 1) - wlo + 64) >> 6);
+            for (int i = tid; i < nwd; i += HW_NT) bm[i] = 0ull;
+            __syncthreads();
+            for (int q = s0 + tid; q < s1; q += HW_NT) {
+                const long long c = (long long)Bkc[q] - wlo;
+                if (c >= 0 && c < (1ll << HW_WB)) atomicOr(&bm[c >> 6], 1ull << (c & 63));
+            }
+            __syncthreads();
+            // ranks: a wave per 512-word block (a lane: two 4-word groups), then the blocks
+            for (int bb = wv; bb < HW_NBLK; bb += NW) {
+                const int w0 = bb * HW_BLK + lane * 8;
+                int t0 = 0, t1 = 0;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    t0 += w0 + u < nwd ? __popcll(bm[w0 + u]) : 0;
+                    t1 += w0 + 4 + u < nwd ? __popcll(bm[w0 + 4 + u]) : 0;
+                }
+                const int inc = wave_incl_scan_dpp(t0 + t1);
+                g4[w0 / 4] = (u16)(inc - t0 - t1);
+                g4[w0 / 4 + 1] = (u16)(inc - t1);
+                if (lane == 63) blk[bb] = inc;
+            }
+            __syncthreads();
+            if (wv == 0) {
+                const int v = lane < HW_NBLK ? blk[lane] : 0;
+                const int inc = wave_incl_scan_dpp(v);
+                if (lane < HW_NBLK) blk[lane] = inc - v;
+                if (lane == 63) red[0] = inc;
+            }
+            __syncthreads();
+            const int wn = red[0];  // the window's nonzeros
+            int *const Ocol = g.Scol + base + out;
+            double *const Oval = g.Sval + base + out;
+            for (int r0 = 0; r0 < wn; r0 += HW_VCAP) {  // (workgroup-uniform; one chunk unless wn > HW_VCAP)
+                const int r1 = min(wn, r0 + HW_VCAP);
+                for (int i = tid; i < r1 - r0; i += HW_NT) vals[i] = 0.0;
+                __syncthreads();
+                for (int q = s0 + tid; q < s1; q += HW_NT) {
+                    const long long c = (long long)Bkc[q] - wlo;
+                    if (c >= 0 && c < (1ll << HW_WB)) {
+                        const int rk = hw_rank(bm, g4, blk, (int)c) - r0;
+                        if ((unsigned)rk < (unsigned)HW_VCAP) atomicAdd(&vals[rk], Bkv[q]);
+                    }
+                }
+                __syncthreads();
+                // emit: a thread per bitmap word, its columns at their ranks
+                for (int w = tid; w < nwd; w += HW_NT) {
+                    u64 word = bm[w];
+                    int rk = blk[w / HW_BLK] + g4[w >> 2];
+                    for (int t = w & ~3; t < w; ++t) rk += __popcll(bm[t]);
+                    while (word && rk < r1) {
+                        const int bit = __builtin_ctzll(word);
+                        word &= word - 1ull;
+                        if (rk >= r0) {
+                            Ocol[rk] = (int)(wlo + w * 64 + bit);
+                            Oval[rk] = vals[rk - r0];
+                        }
+                        ++rk;
+                    }
+                }
+                __syncthreads();  // (the chunk's values read before the next chunk's zeroing)
+            }
+            out += wn;
+            __syncthreads();  // (the window's LDS reads done before the next window's zeroing)
+        }
+    }
+    RP(2);
+    if (tid == 0) g.rnnz[r] = (int)out;
+    RP_DONE(0);
+}
+
+// ---- hub rows dominated by one run (mawi: a hub neighbour's C row is the
+// hub's whole B row plus a few entries): the row is the dominant run L with
+// the other runs' products S (at most DR_SMAX) inserted.
+//   k_rows_dr_prep, a workgroup per row: S expanded, sorted by (column,
+//     position) in LDS and summed per column; each column's insertion point p
+//     in L (binary search of the B row) and whether L holds the column (then
+//     its sum joins that element); the row's nnz = |L| + the inserted columns;
+//     the row's chunks of DR_CH elements of L enqueued.
+//   k_rows_dr_fill, a workgroup per chunk: L streamed (coalesced) to the
+//     row's staging slots at i + (inserted columns before it), the inserted
+//     columns of its range beside them.  For L's element i the S columns
+//     before it are those with p <= i that L does not hold; an S column goes
+//     to p + (inserted columns before it).
+struct DrRow {
+    long long base;  // staging offset
+    int r, bs, L, nu;
+    double aL;
+};
+struct DrEnt {     // one S column (sorted by column): insertion point, kind, column, sum
+    int p;           // first element of L at or past the column
+    int nd;          // inserted (not in L) columns before this one in S
+    int col;
+    int dup;         // 1: L holds the column
+    double val;
+};
+constexpr int DR_NT = 1024;
+
+__global__ __launch_bounds__(DR_NT) void k_rows_dr_prep(RowsArgs g, DrRow *rows, DrEnt *ents, int2 *chunks,
+                                                        int *nchunk, int *ndr) {
+    constexpr int NW = DR_NT / 64;
+    __shared__ unsigned long long sk[DR_SMAX];  // (column << 12 | S position), sorted
+    __shared__ double sv[DR_SMAX];              // S values by S position
+    __shared__ int red[2 * NW + 2];
+    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    const int4 le = g.list[blockIdx.x];
+    const int r = le.x, a0 = le.y, k = le.z;
+    const long long base = g.E[a0];
+    const long long P = g.E[a0 + k] - base;
+    if (P <= kRowsHubProducts) return;  // (workgroup-uniform)
+    int jl;
+    const long long L = row_longest_run(g.E, a0, k, &jl, red);
+    const int nS = (int)(P - L);
+    if (nS > DR_SMAX) return;  // (k_rows_hwin's row)
+    __shared__ int s_h;
+    if (tid == 0) s_h = atomicAdd(ndr, 1);  // this row's slot among the DR rows
+    const long long eL = g.E[a0 + jl] - base;  // L's first product in the row's product order
+    const int2 bL = g.ebnd[a0 + jl];
+    // S: the row's products outside L, in product order; position q -> the row's
+    // product q' (q past L's start skips L), its entry by a binary search of E
+    int npow = 1;
+    while (npow < nS) npow <<= 1;
+    for (int q = tid; q < npow; q += DR_NT) {
+        if (q >= nS) {
+            sk[q] = ~0ull;
+            continue;
+        }
+        const long long qq = base + (q < eL ? q : q + L);
+        int lo = a0, hi = a0 + k;  // the last entry a with E[a] <= qq
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (g.E[mid] <= qq) lo = mid; else hi = mid;
+        }
+        const int pb = g.ebnd[lo].x + (int)(qq - g.E[lo]);
+        const int c = g.Bcol[pb];
+        sv[q] = g.vA[lo] * g.Bval[pb];
+        sk[q] = ((unsigned long long)(unsigned)c << 12) | (unsigned)q;
+    }
+    __syncthreads();
+    // bitonic sort of npow keys in LDS
+    for (int K = 2; K <= npow; K <<= 1)
+        for (int J = K >> 1; J > 0; J >>= 1) {
+            for (int i = tid; i < npow; i += DR_NT) {
+                const int ij = i ^ J;
+                if (ij > i) {
+                    const unsigned long long a = sk[i], b = sk[ij];
+                    const bool asc = (i & K) == 0;
+                    if ((a > b) == asc) {
+                        sk[i] = b;
+                        sk[ij] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    // per column (heads in sorted order): its sum in sorted order, insertion
+    // point in L, whether L holds it
+    int nh = 0;
+    int hq[DR_SMAX / DR_NT];
+#pragma unroll
+    for (int u = 0; u < DR_SMAX / DR_NT; ++u) {
+        const int t = tid * (DR_SMAX / DR_NT) + u;
+        hq[u] = t < nS && (t == 0 || (sk[t] >> 12) != (sk[t - 1] >> 12));
+        nh += hq[u];
+    }
+    const int inc = wave_incl_scan_dpp(nh);
+    if (lane == 63) red[wv] = inc;
+    __syncthreads();
+    int o = inc - nh, nu = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        o += w < wv ? red[w] : 0;
+        nu += red[w];
+    }
+    const int h = s_h;  // (written before the barriers above)
+    DrEnt *const E8 = ents + (long)h * DR_SMAX;
+    const int oslot = o;  // this thread's first entry
+    int ndp = 0;          // this thread's columns not in L
+    int mydup[DR_SMAX / DR_NT];
+#pragma unroll
+    for (int u = 0; u < DR_SMAX / DR_NT; ++u) {
+        const int t = tid * (DR_SMAX / DR_NT) + u;
+        mydup[u] = 0;
+        if (!hq[u]) continue;
+        const int c = (int)(sk[t] >> 12);
+        double sum = sv[sk[t] & 4095u];
+        for (int j = t + 1; j < nS && (int)(sk[j] >> 12) == c; ++j) sum += sv[sk[j] & 4095u];  // (ascending)
+        int lo = 0, hi = (int)L;  // first element of L at or past c
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (g.Bcol[bL.x + mid] < c) lo = mid + 1; else hi = mid;
+        }
+        mydup[u] = lo < L && g.Bcol[bL.x + lo] == c;
+        ndp += !mydup[u];
+        DrEnt e;
+        e.p = lo;
+        e.col = c;
+        e.dup = mydup[u];
+        e.val = sum;
+        e.nd = 0;
+        E8[o++] = e;
+    }
+    // inserted columns before each entry: exclusive scan of the not-in-L flags in S order
+    __syncthreads();  // (red reused)
+    const int inc2 = wave_incl_scan_dpp(ndp);
+    if (lane == 63) red[wv] = inc2;
+    __syncthreads();
+    int nd = inc2 - ndp, ndt = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        nd += w < wv ? red[w] : 0;
+        ndt += red[w];
+    }
+    int os = oslot;
+#pragma unroll
+    for (int u = 0; u < DR_SMAX / DR_NT; ++u) {
+        if (!hq[u]) continue;
+        E8[os].nd = nd;
+        nd += !mydup[u];
+        ++os;
+    }
+    if (tid == 0) {
+        DrRow d;
+        d.base = base;
+        d.r = r;
+        d.bs = bL.x;
+        d.L = (int)L;
+        d.nu = nu;
+        d.aL = g.vA[a0 + jl];
+        rows[h] = d;
+        g.rnnz[r] = (int)L + ndt;
+        const int nch = (int)((L + DR_CH - 1) / DR_CH);
+        const int c0 = atomicAdd(nchunk, nch);
+        for (int c = 0; c < nch; ++c) chunks[c0 + c] = make_int2(h, c * DR_CH);
+    }
+}
+
+__global__ __launch_bounds__(DR_NT) void k_rows_dr_fill(RowsArgs g, const DrRow *rows, const DrEnt *ents,
+                                                        const int2 *chunks, const int *nchunk) {
+    __shared__ int sp[DR_SMAX];   // the chunk's S entries: insertion points
+    __shared__ int snd[DR_SMAX];  // inserted columns before each
+    __shared__ unsigned char sdup[DR_SMAX];
+    __shared__ double sval[DR_SMAX];
+    __shared__ int s_lo, s_hi;
+    const int tid = threadIdx.x;
+    if ((int)blockIdx.x >= *nchunk) return;  // (workgroup-uniform)
+    const int2 ch = chunks[blockIdx.x];
+    const DrRow d = rows[ch.x];
+    const DrEnt *const E8 = ents + (long)ch.x * DR_SMAX;
+    const int i0 = ch.y, i1 = min(d.L, i0 + DR_CH);
+    const bool last = i1 == d.L;
+    // the S entries with insertion point in [i0, i1) (the last chunk: [i0, L])
+    if (tid < 2) {
+        const int key = tid == 0 ? i0 : (last ? d.L + 1 : i1);
+        int lo = 0, hi = d.nu;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (E8[mid].p < key) lo = mid + 1; else hi = mid;
+        }
+        if (tid == 0) s_lo = lo; else s_hi = lo;
+    }
+    __syncthreads();
+    const int elo = s_lo, ne = s_hi - s_lo;
+    const int nd0 = elo < d.nu ? E8[elo].nd : (d.nu ? E8[d.nu - 1].nd + !E8[d.nu - 1].dup : 0);
+    for (int t = tid; t < ne; t += DR_NT) {
+        const DrEnt e = E8[elo + t];
+        sp[t] = e.p;
+        snd[t] = e.nd;
+        sdup[t] = e.dup;
+        sval[t] = e.val;
+    }
+    __syncthreads();
+    int *const Ocol = g.Scol + d.base;
+    double *const Oval = g.Sval + d.base;
+    for (int i = i0 + tid; i < i1; i += DR_NT) {
+        const int c = g.Bcol[d.bs + i];
+        double v = d.aL * g.Bval[d.bs + i];
+        // entries with p <= i: the count t; the inserted ones before i = nd of entry t
+        int lo = 0, hi = ne;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (sp[mid] <= i) lo = mid + 1; else hi = mid;
+        }
+        const int ins = lo < ne ? snd[lo] : (ne ? snd[ne - 1] + !sdup[ne - 1] : nd0);
+        if (lo > 0 && sp[lo - 1] == i && sdup[lo - 1]) v += sval[lo - 1];
+        Ocol[i + ins] = c;
+        Oval[i + ins] = v;
+    }
+    for (int t = tid; t < ne; t += DR_NT)
+        if (!sdup[t]) {
+            const DrEnt e = E8[elo + t];
+            Ocol[e.p + e.nd] = e.col;
+            Oval[e.p + e.nd] = e.val;
+        }
+}
+
 // every row's run from the staging area (at soff[r]) to its CSR place, by
 // chunks of CP_CH output positions (a workgroup each, consecutive lanes on
 // consecutive positions): the chunk's rows from cfirst (the row holding each
@@ -1013,7 +1590,7 @@ int dev_rows_setup_async(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B
     TSG_TRY(cx.get(&p.E, (size_t)A.nnz + 1));
     TSG_TRY(cx.get(&p.lists, (size_t)NCLS * (m > 0 ? m : 1)));
     TSG_TRY(cx.get(&p.soff, (size_t)m + 1));
-    TSG_TRY(cx.get(&p.cls, 14));  // class counts, then 3 u64 statistics at [8..13]
+    TSG_TRY(cx.get(&p.cls, 24));  // class counts, 5 u64 statistics at [8..18), hub rows' cursors at [18..24)
     TSG_TRY(cx.get(&p.rowpointer, (size_t)m + 1));
     unsigned long long *hst = reinterpret_cast<unsigned long long *>(p.cls + 8);
     k_rows_entries<<<grid_for((long)A.nnz + 1, WG, 16384), WG, 0, s>>>(A.columnindex, A.nnz, B.rowpointer, p.ebnd,
@@ -1024,7 +1601,7 @@ int dev_rows_setup_async(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B
     k_rows_bin<<<max(1, (m + BIN_ROWS - 1) / BIN_ROWS), WG, 0, s>>>(A.rowpointer, m, p.E, p.E + A.nnz, p.rowpointer,
                                                                     p.lists, p.cls, p.soff, hst);
     TSG_HIP(hipGetLastError());
-    TSG_HIP(hipMemcpyAsync(cx.pinned64, p.cls, 14 * sizeof(int), hipMemcpyDeviceToHost, s));
+    TSG_HIP(hipMemcpyAsync(cx.pinned64, p.cls, 18 * sizeof(int), hipMemcpyDeviceToHost, s));
     return TSG_OK;
 }
 
@@ -1033,11 +1610,16 @@ void dev_rows_setup_read(Context &cx, RowsPlan &p) {
     p.hprod = cx.pinned64[4];
     p.pmax = cx.pinned64[5];
     p.products = cx.pinned64[6];
+    p.drprod = cx.pinned64[7];
+    p.hubrest = cx.pinned64[8];
 }
 
-// routing: the path is built for rows of modest length (class H a minority of
-// the work); hub-dominated products (R-MAT, mawi) take the staged pipeline
-bool dev_rows_accept(const RowsPlan &p) { return p.hprod * 4 <= p.products && p.pmax <= kRowsMaxRowProducts; }
+// routing: the path is built for rows of modest length (class H's bitmap rows a
+// minority of the work) and for hub rows that one run dominates (the DR
+// kernels); hub rows without a dominant run (R-MAT) take the staged pipeline
+bool dev_rows_accept(const RowsPlan &p) {
+    return (p.hprod - p.drprod) * 4 <= p.products && p.hubrest == 0;
+}
 
 void dev_rows_release(Context &cx, RowsPlan &p) {
     void *ps[] = {p.ebnd, p.E, p.lists, p.soff, p.cls, p.rowpointer};
@@ -1099,7 +1681,35 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
         k_rows_order_h<<<1, OH_NT, 0, s>>>(E, p.cls, lists + (long)(NCLS - 1) * m);
         TSG_HIP(hipGetLastError());
     }
-    TSG_TRY(launch(7, k_rows_bitmap, ncls[7], RH_NT, s));
+    int *Tcol = nullptr;
+    double *Tval = nullptr;
+    DrRow *drows = nullptr;
+    DrEnt *dents = nullptr;
+    int2 *dchunks = nullptr;
+    if (ncls[7] > 0) {
+        // class H: each kernel takes its rows of the class (hub rows the windowed
+        // one) and its other workgroups return at once
+        g.list = lists + (long)7 * m;
+        g.nrows = ncls[7];
+        if (p.hubrest > 0) {  // hub rows without a dominant run: their bucket area
+            TSG_TRY(cx.get(&Tcol, (size_t)p.hubrest + 1));
+            TSG_TRY(cx.get(&Tval, (size_t)p.hubrest + 1));
+            k_rows_hwin<<<ncls[7], HW_NT, 0, s>>>(g, Tcol, Tval, reinterpret_cast<unsigned long long *>(p.cls + 18));
+            TSG_HIP(hipGetLastError());
+        }
+        k_rows_bitmap<<<ncls[7], RH_NT, 0, s>>>(g);
+        TSG_HIP(hipGetLastError());
+        if (p.drprod > 0) {  // hub rows with a dominant run
+            const long long ndr = p.drprod / kRowsHubProducts + 1, nch = p.drprod / DR_CH + ndr;
+            TSG_TRY(cx.get(&drows, (size_t)ndr));
+            TSG_TRY(cx.get(&dents, (size_t)ndr * DR_SMAX));
+            TSG_TRY(cx.get(&dchunks, (size_t)nch));
+            k_rows_dr_prep<<<ncls[7], DR_NT, 0, s>>>(g, drows, dents, dchunks, p.cls + 20, p.cls + 21);
+            TSG_HIP(hipGetLastError());
+            k_rows_dr_fill<<<(unsigned)nch, DR_NT, 0, s>>>(g, drows, dents, dchunks, p.cls + 20);
+            TSG_HIP(hipGetLastError());
+        }
+    }
     TSG_TRY(launch_m(6, k_rows_merge<M4_NT, M4_CAP, M4_RUNS>, ncls[6], M4_NT, s));
     TSG_TRY(launch_m(5, k_rows_merge<M3_NT, M3_CAP, M3_RUNS>, ncls[5], M3_NT, s));
     TSG_TRY(launch_m(4, k_rows_merge<M2_NT, M2_CAP, M2_RUNS>, ncls[4], M2_NT, s));
@@ -1149,15 +1759,20 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
         k_rows_compact<<<nch, WG, 0, s>>>(m, cfirst, soff, C.rowpointer, Scol, Sval, C.columnindex, C.value);
     }
     TSG_HIP(hipGetLastError());
-    if (small) TSG_HIP(hipMemcpyAsync(cx.pinned64 + 7, C.rowpointer + m, sizeof(int), hipMemcpyDeviceToHost, s));
+    if (small) TSG_HIP(hipMemcpyAsync(cx.pinned64 + 15, C.rowpointer + m, sizeof(int), hipMemcpyDeviceToHost, s));
     if (ev) TSG_HIP(hipEventRecord(ev[3], s));
     TSG_TRY(stream_wait(s));
-    if (small) nnz = *reinterpret_cast<const int *>(cx.pinned64 + 7);
+    if (small) nnz = *reinterpret_cast<const int *>(cx.pinned64 + 15);
     C.nnz = (int)nnz;
     cx.put(cfirst);
     dev_rows_release(cx, p);
     cx.put(Scol);
     cx.put(Sval);
+    cx.put(Tcol);
+    cx.put(Tval);
+    cx.put(drows);
+    cx.put(dents);
+    cx.put(dchunks);
     if (st) {
         st->nnzC = C.nnz;
         st->tile_products = products;

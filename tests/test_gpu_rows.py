@@ -1,9 +1,13 @@
 """The row-merge path (spgemm_amd/csrc/tsg_rows.hip): rows binned by element
-products into eight classes -- S16 / S64 (<= 16 / 64 products: ranks by
-counting in 16 or 64 lanes), M0..M4
-(<= 256 / 512 / 1,024 / 2,048 / 4,096 products: pairwise merge-path merges of the
-runs in LDS) and H (longer rows or more runs: an LDS column bitmap per window
-of 524,288 columns, f64 atomics for the values).  TSG_PATH=rows forces it.  Pattern
+products (and A entries) into eight classes -- S16 / S64 (<= 16 / 64
+products: ranks by counting in 16 or 64 lanes), M0..M4 (<= 256 / 512 /
+1,024 / 2,048 / 4,096 products and <= 62 / 124 / 248 / 504 / 512 entries:
+bitonic sorts of packed (column, position) keys in registers and LDS, or
+merge-path rounds when the row's column span is too wide for packed keys) and
+H (longer rows or more entries: an LDS column bitmap per window of 1,048,576
+columns, f64 atomics for the values; hub rows past 65,536 products: the
+windowed kernel -- products bucketed by column, LDS bitmaps of 262,144
+columns, values added in LDS).  TSG_PATH=rows forces the path.  Pattern
 bit-exact, values within 1e-10 relative, against the oracle (the reference's
 semantics: steps 1-3 + tile2csr, tilespgemm-cuda.h:279-2218)."""
 import numpy as np
@@ -65,8 +69,9 @@ def _check(A_, B_=None, aat=False, real=False, seed=0, path=None):
     return st
 
 
-# (products, runs) caps of the classes S16, S64, M1..M4; longer rows are class H
-CAPS = [(16, 16), (64, 64), (256, 64), (512, 128), (1024, 256), (2048, 512), (4096, 512)]
+# (products, A entries) caps of the classes S16, S64, M0..M4 (tsg_rows.hip
+# row_class); longer rows are class H
+CAPS = [(16, 16), (64, 64), (256, 62), (512, 124), (1024, 248), (2048, 504), (4096, 512)]
 H = len(CAPS)
 M3, M4 = H - 2, H - 1
 
@@ -143,14 +148,14 @@ def test_rows_many_runs_go_to_bitmap():
 
 
 def test_rows_bitmap_several_windows():
-    # class H rows over 2,000,000 columns: four windows of 524,288 columns,
-    # including empty windows in between
-    n = 2_000_000
+    # class H rows over 3,000,000 columns: three windows of 1,048,576 columns,
+    # including an empty window in between
+    n = 3_000_000
     rng = np.random.default_rng(7)
     k = 20
     Brows = []
     for j in range(k):
-        lo = 0 if j % 2 == 0 else 1_600_000
+        lo = 0 if j % 2 == 0 else 2_500_000
         Brows.append(np.sort(rng.choice(np.arange(lo, lo + 400_000), size=400, replace=False)))
     B = _csr(k, n, Brows)
     A = _csr(3, k, [np.arange(k), np.arange(0, k, 2), np.array([1, 3])])
@@ -209,3 +214,82 @@ def test_default_routing_fused_by_longest_row(monkeypatch):
     arows = [np.arange(100)] + [np.array([150, (i * 11) % 100]) for i in range(1, 60)]
     A = _csr(60, n, [np.unique(r) for r in arows])
     st = _check(A, B, real=True, seed=13, path=T.PATH_FUSED)
+
+
+def test_rows_class_boundaries_by_entries():
+    """Rows at each merge class's entry cap and one past it (62/63, 124/125,
+    248/249, 504/505, 512/513 A entries of two products each): the class
+    changes at the cap exactly (the LDS run tables are sized by it)."""
+    n = 20000
+    rng = np.random.default_rng(31)
+    rows = []
+    for cap in (62, 124, 248, 504, 512):
+        for k in (cap, cap + 1):
+            rows.append(np.sort(rng.choice(n, size=k, replace=False)))
+    A = _csr(len(rows), n, rows)
+    B = _csr(n, 50000, [np.sort(np.array([(7 * j) % 50000, (7 * j + 3) % 50000])) for j in range(n)])
+    cls = _classes(len(rows), n, A[2], A[3], B[2])
+    assert list(cls[0::2]) == [2, 3, 4, 5, 6] and list(cls[1::2]) == [3, 4, 5, 6, H]
+    _check(A, B, real=True, seed=17)
+
+
+@pytest.mark.parametrize("cls_products", [800, 1600, 3500])
+def test_rows_unpacked_wide_span(cls_products):
+    """M2 / M3 / M4 rows whose column span (20,000,000 columns) is too wide for
+    packed u32 keys: the merge-path branch with moved (run, position) payloads
+    and values gathered after the merge.  Runs sit at both ends of the range and
+    collide (equal columns in several runs)."""
+    n = 20_000_000
+    rng = np.random.default_rng(cls_products)
+    nb = 40
+    Brows = []
+    for j in range(nb):
+        lo = 0 if j % 2 == 0 else n - 200_000
+        Brows.append(np.sort(rng.choice(np.arange(lo, lo + 200_000, 50), size=cls_products // 20,
+                                        replace=False)))
+    B = _csr(nb, n, Brows)
+    A = _csr(4, nb, [np.arange(0, 20), np.arange(20, 40), np.arange(0, 40, 3), np.array([1, 2, 5])])
+    cls = _classes(4, nb, A[2], A[3], B[2])
+    assert cls.max() >= 4 and cls.max() < H
+    _check(A, B, real=True, seed=cls_products)
+
+
+def test_rows_hub_rows_windowed_and_dominant_run():
+    """Hub rows (past 65,536 products): without a dominant run the windowed
+    class-H kernel (products bucketed by column, per-window LDS bitmaps, LDS
+    values) -- many runs over 1,500,000 columns with heavy collisions (several
+    buckets, windows with more nonzeros than one LDS value chunk), two long
+    colliding runs; with one (all but <= 4,096 products in one run) the DR
+    kernels -- one long run with a few short ones (the mawi pattern) and a row
+    of one run -- beside ordinary rows."""
+    rng = np.random.default_rng(41)
+    n = 1_500_000
+    nb = 3000
+    Brows = [np.sort(rng.choice(n, size=int(rng.integers(20, 120)), replace=False)) for _ in range(nb - 3)]
+    Brows.append(np.sort(rng.choice(n, size=200_000, replace=False)))  # a hub's long row
+    Brows.append(np.sort(rng.choice(np.arange(1000, 1000 + 150_000), size=90_000, replace=False)))  # narrow
+    Brows.append(np.arange(0, n, 7)[:80_000])
+    B = _csr(nb, n, Brows)
+    arows = [np.sort(rng.choice(nb - 3, size=1500, replace=False)),   # ~100k products, many runs
+             np.array([5, 17, nb - 3]),                                # long run + short ones
+             np.array([nb - 2, nb - 1]),                               # two long runs, colliding
+             np.array([nb - 2])]                                       # one run, one window
+    arows += [np.sort(rng.choice(nb - 3, size=5, replace=False)) for _ in range(50)]
+    A = _csr(len(arows), nb, arows)
+    blen = np.diff(B[2].astype(np.int64))
+    P = np.array([blen[r].sum() for r in arows])
+    assert (P[:4] > 65536).all()
+    _check(A, B, real=True, seed=43)
+
+
+def test_rows_mawi_prefix_hub_rows():
+    """The mawi stand-in at 1e-2 scale (hub degree 1e5): a row prefix holding
+    hub-neighbour rows (each C row receives the hub's whole row) through the
+    row-merge path, against the oracle."""
+    m, n, rp, ci, vv = synth.mawi(scale=0.01)
+    blen = np.diff(rp.astype(np.int64))
+    cum = np.concatenate([[0], np.cumsum(blen[ci])])[rp]
+    r = int(np.searchsorted(cum, 3e7, side="right") - 1)
+    P = np.diff(cum[:r + 1])
+    assert P.max() > 65536
+    _check((r, n, rp[:r + 1].copy(), ci[:rp[r]].copy(), vv[:rp[r]].copy()), (m, n, rp, ci, vv), real=True, seed=47)
