@@ -213,13 +213,12 @@ def pmc_traffic(kernels, workload):
     if not files:
         return None, None
     d = json.load(open(files[-1]))
-    tot = 0
-    for kernel in kernels:
+    tot, found = 0, False
+    for kernel in kernels:  # (the kernels of the unit that ran for this workload)
         hits = [v for k, v in d.items() if kernel in k and isinstance(v, dict) and v.get("hbm_bytes_per_dispatch")]
-        if not hits:
-            return None, None
+        found |= bool(hits)
         tot += sum(int(v["hbm_bytes_per_dispatch"]) for v in hits)
-    return tot, os.path.relpath(files[-1], REPO)
+    return (tot, os.path.relpath(files[-1], REPO)) if found else (None, None)
 
 
 def main():
@@ -235,6 +234,9 @@ def main():
     ap.add_argument("--rows", type=int, default=None,
                     help="A = its first ROWS rows (B whole); default: all rows, or for configs whose "
                          "full product exceeds int32 nnz(C) (lj) the largest prefix with nnzCub <= 1.5e9")
+    ap.add_argument("--row-start", type=int, default=0,
+                    help="with --rows R: A = rows [ROW_START, ROW_START + R) (e.g. the LiveJournal "
+                         "stand-in's heaviest row block; B whole)")
     ap.add_argument("--cpu-budget-s", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", action="store_true",
@@ -296,7 +298,14 @@ def main():
         # row prefix within one int32 C, as SURVEY §8d prescribes for infeasible sizes
         rows = int(np.searchsorted(cum, args.block_products, side="right") - 1) // tm * tm
         log(f"full product infeasible (nnzCub {int(cum[-1])}); using rows [0,{rows})")
-    if rows is not None and rows < m:
+    if rows is not None and args.row_start > 0:
+        r0 = min(args.row_start, m)
+        r1 = min(m, r0 + rows)
+        rows_, rp_, ci_, vv_ = tdist.slice_rows(m, rp, ci, vv, r0, r1)
+        m, rp, ci, vv = rows_, rp_, ci_.copy(), vv_.copy()
+        cum = cum[r0:r1 + 1] - cum[r0]
+        name = f"{name} rows[{r0},{r1}) of {full_m}"
+    elif rows is not None and rows < m:
         m, rp, ci, vv = rows, rp[:rows + 1].copy(), ci[:rp[rows]].copy(), vv[:rp[rows]].copy()
         cum = cum[:rows + 1]
         name = f"{name} rows[0,{rows}) of {full_m}"
@@ -410,9 +419,11 @@ def main():
     path_name = {0: "tiles", 1: "fused", 2: "band", 3: "rows"}.get(path_id, str(path_id))
     workload = f"{name} C=A{'*A^T' if aat else '^2'} fp64 (device CSR in -> device CSR out), path {path_name}"
     if path_id == 3:
-        kernel_desc = ("row-merge numeric phase (k_rows_bitmap, k_rows_merge x4 classes, k_rows_small x2, in turn): "
-                       "B_alg of SURVEY §8d / HIP-event phase time")
-        traffic, traffic_src = pmc_traffic(["k_rows_small", "k_rows_merge", "k_rows_bitmap"], workload)
+        kernel_desc = ("row-merge numeric phase (class H: k_rows_bitmap / hub rows k_rows_hwin, k_rows_dr_*; "
+                       "k_rows_merge x5 classes, k_rows_small x2; in turn): B_alg of SURVEY §8d / HIP-event phase "
+                       "time")
+        traffic, traffic_src = pmc_traffic(["k_rows_small", "k_rows_merge", "k_rows_bitmap", "k_rows_hwin",
+                                            "k_rows_dr_"], workload)
     else:
         kernel_desc = "step-3 numeric kernel (fused tile2csr): B_alg of SURVEY §8d / HIP-event kernel time"
         traffic, traffic_src = pmc_traffic(["k_step3"], workload)

@@ -861,8 +861,7 @@ __device__ __forceinline__ int bm_rank(const u64 *bm, const u16 *g4, const int *
 }
 
 __global__ __launch_bounds__(RH_NT) void k_rows_bitmap(RowsArgs g) {
-    // (rows past kRowsHubProducts are k_rows_hwin's)
-    {
+    {  // (hub rows, past kRowsHubProducts: k_rows_hwin's or the DR kernels')
         const int4 le0 = g.list[blockIdx.x];
         if (g.E[le0.y + le0.z] - g.E[le0.y] > kRowsHubProducts) return;  // (workgroup-uniform)
     }
@@ -940,9 +939,14 @@ __global__ __launch_bounds__(RH_NT) void k_rows_bitmap(RowsArgs g) {
         RP(3);
         // the window's values zeroed (coalesced); the walk below stores each column
         // at its rank (a column's products store the same value) and adds the values
+        // with workgroup-scope atomics.  Ordering: __syncthreads' workgroup release
+        // compiles to a bare s_barrier here (no vmcnt wait: the ISA showed the
+        // zeroing stores still in flight at the barrier), so each wave drains its
+        // own stores first -- every zero has completed before any atomic issues.
+        // (An agent-scope fence instead wrote the L2 back, ~85 us per window.)
         for (int i = tid; i < wn; i += RH_NT) g.Sval[base + out + i] = 0.0;
-        __syncthreads();  // (workgroup scope: the zeros and the atomics meet in this XCD's L2; an
-                          // agent-scope fence here wrote the L2 back, ~85 us per window)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
         RP(4);
         rows_walk<true>(g, a0, k, wt, [&](int col, double x) {
             const long long c = (long long)col - wlo;
@@ -1164,7 +1168,8 @@ __global__ __launch_bounds__(HW_NT, 8) void k_rows_hwin(RowsArgs g, int *Tcol, d
             qb += tot;
         }
     }
-    __syncthreads();  // (the slots written: read back by this workgroup only)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (each wave's stores complete before the barrier:
+    __syncthreads();                                   //  the slots are read back by other waves)
     RP(0);
     // 2. buckets of 2^bsh columns (bsh >= HW_WB, at most HW_MAXB of them)
     const long long span = (long long)hi - lo + 1;
@@ -1206,7 +1211,8 @@ __global__ __launch_bounds__(HW_NT, 8) void k_rows_hwin(RowsArgs g, int *Tcol, d
             Tcol[toff + d] = c;
             Tval[toff + d] = Aval[q];
         }
-        __syncthreads();  // (the bucket area read back by this workgroup only)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // (the bucket area read back by the other waves)
         Bkc = Tcol + toff;
         Bkv = Tval + toff;
     } else if (tid == 0) {
@@ -1697,8 +1703,10 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
             k_rows_hwin<<<ncls[7], HW_NT, 0, s>>>(g, Tcol, Tval, reinterpret_cast<unsigned long long *>(p.cls + 18));
             TSG_HIP(hipGetLastError());
         }
-        k_rows_bitmap<<<ncls[7], RH_NT, 0, s>>>(g);
-        TSG_HIP(hipGetLastError());
+        if (p.hprod > p.drprod + p.hubrest) {  // rows of the one-window bitmap kernel
+            k_rows_bitmap<<<ncls[7], RH_NT, 0, s>>>(g);
+            TSG_HIP(hipGetLastError());
+        }
         if (p.drprod > 0) {  // hub rows with a dominant run
             const long long ndr = p.drprod / kRowsHubProducts + 1, nch = p.drprod / DR_CH + ndr;
             TSG_TRY(cx.get(&drows, (size_t)ndr));

@@ -53,6 +53,7 @@ def test_two_ranks_gather_equals_single_rank(name, aat):
     assert two["scaling"] == "strong"
     assert two["check"] == one["check"]
     assert two["config"]["nnzC"] == one["config"]["nnzC"]
+    assert two["work_share"]["max_over_mean"] >= 1.0
 
 
 @pytest.mark.parametrize("name,aat", [("x_powerlaw_400", 1)])
@@ -80,22 +81,32 @@ def _mawi_rows(scale, products):
     return (m, n, rp, ci, vv), rows
 
 
-def test_mawi_eight_ranks_gather_vs_oracle():
+def test_mawi_eight_ranks_gather_vs_oracle(tmp_path):
     """BASELINE config 5 rehearsed on one GPU: the mawi stand-in at 1e-2 scale
     (2.26 M nodes, hub degree 1e5), a row prefix of ~2e8 intermediate products
     (the full A^2 is ~1e10 products, past int32 nnz(C)), partitioned 8 ways by
     work, each rank's block through the HIP pipeline, the C blocks gathered to
-    rank 0 (gloo here; RCCL on an 8-GPU node).  The gathered C's checksum must
-    equal the oracle's full product of the same rows."""
+    rank 0 (gloo here; RCCL on an 8-GPU node).  The gathered C -- row pointers,
+    columns and values, array by array (bench.py --dump) -- must equal the
+    oracle's product of the same rows, and the line reports each rank's share
+    of the work."""
     import numpy as np
     import _oracle as O
     (m, n, rp, ci, vv), rows = _mawi_rows(0.01, 2e8)
-    eight = _bench(8, None, 0, extra=("--matrix", "mawi", "--scale", "0.01", "--rows", str(rows)))
+    dump = str(tmp_path / "c8.npz")
+    eight = _bench(8, None, 0, extra=("--matrix", "mawi", "--scale", "0.01", "--rows", str(rows), "--dump", dump))
     assert eight["n_gpus"] == 8 and eight["scaling"] == "strong"
     assert eight["config"]["parallelism"] == "row-block8 + RCCL gather"
+    ws = eight["work_share"]
+    assert len(ws["products"]) == 8 and sum(ws["products"]) == eight["config"]["nnzCub"]
+    assert ws["max_over_mean"] >= 1.0
     oA = O.OMat.from_csr(rows, n, rp[:rows + 1].copy(), ci[:rp[rows]].copy(), vv[:rp[rows]].copy())
     oB = O.OMat.from_csr(m, n, rp, ci, vv)
     _, _, erp, eci, evv = O.gustavson(oA, oB).csr()
+    got = np.load(dump)
+    np.testing.assert_array_equal(got["rowptr"], erp)
+    np.testing.assert_array_equal(got["col"], eci)
+    np.testing.assert_allclose(got["val"], evv, rtol=1e-10, atol=0)
     want = {"nnz": int(len(eci)), "rowptr_sum": int(erp.astype(np.int64).sum()),
             "col_sum": int(eci.astype(np.int64).sum()), "val_sum": float(evv.sum())}
     assert eight["check"] == want

@@ -11,7 +11,7 @@ shift || true
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
-BENCH=(python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --tiled 0 "$@")
+BENCH=(python3 "$ROOT/bench.py" --steps ${PSTEPS:-5} --warmup 2 --no-cpu-baseline --tiled 0 "$@")
 cd /tmp
 export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run -- "${BENCH[@]}" \
