@@ -105,6 +105,7 @@ int stream_wait(hipStream_t s) {
             return TSG_ERR_HIP;
         }
         if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(1000)) break;
+        std::this_thread::yield();  // (concurrent callers on other threads keep their cores)
     }
     TSG_HIP(hipStreamSynchronize(s));
     return TSG_OK;
@@ -854,9 +855,11 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
     //    least as many products as columns (FEM-like: cant); its check is a
     //    statistics kernel + one host round trip;
     //  * otherwise the row-merge setup (entry table, classes) + one round trip:
-    //    fused path (tsg_fused.hip) when no C row has over kFusedMaxRowProducts
-    //    element products (mc2depi), row-merge path (tsg_rows.hip) unless the
-    //    products are hub-dominated (dev_rows_accept: R-MAT, mawi);
+    //    the row-merge path (tsg_rows.hip) unless hub rows without a dominant
+    //    run carry the product (dev_rows_accept: R-MAT).  (The fused path,
+    //    tsg_fused.hip, is no longer a default: since the merge classes' value
+    //    preload the row-merge path is faster on short rows too -- mc2depi
+    //    A*A^T 0.25 vs 0.35 ms; TSG_PATH=fused still runs it.)
     //  * the staged tile pipeline below for the rest and for unsorted B rows.
     // TSG_PATH=fused / band / rows / tiles forces a path (band when its check
     // passes).
@@ -892,7 +895,8 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
             TSG_TRY(stream_wait(s));
             dev_rows_setup_read(cx, plan);
             const bool bsorted0 = cx.pinned[1] == 0;
-            if (bsorted0 && !force_band && (force_fused || (!force_rows && plan.pmax <= kFusedMaxRowProducts))) {
+            const bool fused_fits = (long long)B->n < kFusedMaxCols;  // (else the fused path is UNSUPPORTED)
+            if (bsorted0 && !force_band && fused_fits && force_fused) {
                 const int rc = dev_spgemm_fused(cx, *A, *B, *C, &st, s, cx.ev, plan.ebnd, plan.E);
                 dev_rows_release(cx, plan);
                 TSG_TRY(rc);

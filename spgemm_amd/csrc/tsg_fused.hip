@@ -244,11 +244,14 @@ __device__ long long fz_resolve(unsigned long long *status, int u, long long n, 
         const int j = j0 - lane;
         if (!first) st = j >= 0 ? fz_ld(&status[j]) : FZ_INC;
         first = false;
-        int spins = 0;
+        // a predecessor that has not published yet: wait (ticket order guarantees
+        // it is running); one that never publishes within 2 s of wall clock --
+        // not a slow one, a fault -- fails the call instead of hanging it
+        const unsigned long long w0 = wall_clock64();
         while ((st >> 62) == 0) {
             __builtin_amdgcn_s_sleep(1);
             st = fz_ld(&status[j]);
-            if (++spins > (1 << 24)) {  // a predecessor that never publishes: fail, never hang
+            if ((st >> 62) == 0 && wall_clock64() - w0 > 200000000ull) {  // (100 MHz wall clock: 2 s)
                 atomicExch(fail, 2);
                 st = FZ_INC;
             }
@@ -789,7 +792,7 @@ int dev_spgemm_fused(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, ts
     if (A.n != B.m) return TSG_ERR_INVALID;
     const int m = A.m;
     const long nnzA = A.nnz;
-    if ((long long)B.n >= (1LL << 28) - 16) return TSG_ERR_UNSUPPORTED;  // tile column < 2^24 in a segment key
+    if ((long long)B.n >= kFusedMaxCols) return TSG_ERR_UNSUPPORTED;  // tile column < 2^24 in a segment key
     C = tsg_dev_csr{};
     C.m = m;
     C.n = B.n;

@@ -120,9 +120,8 @@ int dev_tile2csr(Context &cx, const tsg_dev_tiles &C, tsg_dev_csr &out, hipStrea
 // ev (optional): 0 start | 1 units built | 4, 5 around the unit kernel | 3 end
 // longest row of M, copied (stream-ordered) into *host_out
 int dev_row_maxlen_async(Context &cx, const tsg_dev_csr &M, int *host_out, hipStream_t s);
-// rows of C with at most this many element products (the longest C row, from
-// the row-merge setup) route to the fused path by default
-constexpr long long kFusedMaxRowProducts = 256;
+// the fused path's segment keys hold a tile column below 2^24: B.n below this
+constexpr long long kFusedMaxCols = (1LL << 28) - 16;
 // ebnd / cum (optional): the entry table of a row-merge setup (same layout), reused
 int dev_spgemm_fused(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, tsg_dev_csr &C, tsg_stats *st,
                      hipStream_t s, hipEvent_t *ev, int2 *ebnd_pre = nullptr, long long *cum_pre = nullptr);
@@ -164,6 +163,11 @@ struct RowsPlan {
 // products with hub rows of the second kind, or whose bitmap-kernel rows hold
 // over a quarter of the work.
 constexpr long long kRowsHubProducts = 65536;
+// the row-merge path sizes C by the products (no read-back of nnz(C) before the
+// compaction) while their 12 B each stay within this; past it C is sized exactly
+// (peak device memory of the path: 12 B per product of staging + C + the A
+// entry table)
+constexpr long long kRowsProductSizedC = 8LL << 30;
 int dev_rows_setup_async(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPlan &p, hipStream_t s);
 void dev_rows_setup_read(Context &cx, RowsPlan &p);  // after the stream synchronised
 bool dev_rows_accept(const RowsPlan &p);

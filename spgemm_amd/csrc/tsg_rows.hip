@@ -1745,19 +1745,32 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
     }
 #endif
     // row counts -> row pointers -> the compaction, with no host round trip:
-    // nnz(C) <= products, so when the products fit int32 the result arrays are
-    // sized by them and nnz(C) comes back with the call's final synchronisation
+    // nnz(C) <= products, so when the products fit int32 (and their 12 B each,
+    // beside the staging's 12 B, stay within kRowsProductSizedC) the result
+    // arrays are sized by them and nnz(C) comes back with the call's final
+    // synchronisation; otherwise -- or when that allocation fails -- the checked
+    // scan reads nnz(C) back first and C is sized exactly.
     long long nnz = 0;  // (C.rowpointer[m] = 0 from the binning kernel)
-    const bool small = products <= 0x7fffffffLL;
+    bool small = products <= 0x7fffffffLL && products * 12 <= kRowsProductSizedC;
     if (small) {
         TSG_TRY(scan_exclusive_i32(cx, C.rowpointer, (long)m + 1, s));
-    } else {  // past int32 products: the checked scan (nnz(C) past int32 fails)
+        if (cx.get(&C.columnindex, (size_t)products + 1) != TSG_OK ||
+            cx.get(&C.value, (size_t)products + 1) != TSG_OK) {
+            cx.put(C.columnindex);
+            C.columnindex = nullptr;
+            small = false;  // (the scan's total is read back below)
+            TSG_TRY(read_i32(cx, C.rowpointer + m, &C.nnz, s));
+            nnz = C.nnz;
+        }
+    } else {  // the checked scan (nnz(C) past int32 fails)
         TSG_TRY(scan_exclusive_i32_total(cx, C.rowpointer, (long)m + 1, s, &nnz));
         if (nnz > 0x7fffffffLL) return TSG_ERR_OVERFLOW;
     }
     const long long cap = small ? products : nnz;
-    TSG_TRY(cx.get(&C.columnindex, (size_t)cap + 1));
-    TSG_TRY(cx.get(&C.value, (size_t)cap + 1));
+    if (!small) {
+        TSG_TRY(cx.get(&C.columnindex, (size_t)cap + 1));
+        TSG_TRY(cx.get(&C.value, (size_t)cap + 1));
+    }
     int *cfirst = nullptr;
     if (cap > 0) {
         const int nch = (int)((cap + CP_CH - 1) / CP_CH);

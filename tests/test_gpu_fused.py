@@ -1,9 +1,9 @@
 """The fused element path (spgemm_amd/csrc/tsg_fused.hip): steps 1-3 and
 tile2csr in one persistent kernel over row units, C tile row-segments (one
 16-bit row mask of a 16x16 C tile) in an LDS hash, ranks by mask popcount,
-unit offsets by a decoupled look-back.  The library routes short-row products
-to it (longest A row x longest B row <= 256, e.g. mc2depi); TSG_PATH=fused
-forces it on every input here, covering its heavy-row column windows
+unit offsets by a decoupled look-back.  Since round 3 the library's default
+route sends short-row products to the row-merge path (faster there now);
+TSG_PATH=fused forces the fused path on every input here, covering its heavy-row column windows
 (histogram-merged windows, global-atomic values past the LDS accumulator).
 Pattern bit-exact, values within 1e-10 relative, against the oracle."""
 import os
@@ -107,12 +107,13 @@ def test_fused_real_values(fused):
     assert np.all(np.abs(got[4] - ref[4]) <= 1e-10 * mag)
 
 
-def test_default_routing_short_rows_fused():
-    """mc2depi A*A^T (rows of <= 4 entries on both sides) takes the fused path by
-    default; long rows spread over the columns take the row-merge path."""
+def test_default_routing_short_rows_go_to_row_merge():
+    """mc2depi A*A^T (rows of <= 4 entries on both sides) and long rows spread
+    over the columns both take the row-merge path by default (the fused path
+    only when forced)."""
     m, n, rp, ci, vv = synth.mc2depi()
     st = _check(m, n, rp, ci, vv, aat=True)
-    assert st["path"] == T.PATH_FUSED
+    assert st["path"] == T.PATH_ROWS
     m, n, rp, ci, vv = synth.random_csr(3000, 3000, density=0.01, seed=4)  # ~30-entry rows
     st = _check(m, n, rp, ci, vv)
     assert st["path"] == T.PATH_ROWS

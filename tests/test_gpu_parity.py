@@ -172,7 +172,7 @@ def test_mawi_star_small_scale_vs_oracle():
 def test_full_size_synthetic_vs_oracle(name, path, monkeypatch):
     """BASELINE configs at full size (synthetic stand-ins): pattern bit-exact,
     values exact, against the numeric Gustavson oracle -- on the default route
-    (cant: banded path, mc2depi: fused path, webbase: staged) and forced
+    (cant: banded path, mc2depi and webbase: row-merge path) and forced
     through the staged tile pipeline."""
     if path:
         monkeypatch.setenv("TSG_PATH", path)
@@ -194,7 +194,7 @@ def test_full_size_synthetic_vs_oracle(name, path, monkeypatch):
     # tile rows over 256 entries) equal the oracle csr2tile's numtile (the fused,
     # banded and row-merge paths build no A/B tiles and report -1)
     if path is None:  # the default routes
-        assert st["path"] == {"cant": T.PATH_BAND, "mc2depi": T.PATH_FUSED, "webbase": T.PATH_ROWS}[name]
+        assert st["path"] == {"cant": T.PATH_BAND, "mc2depi": T.PATH_ROWS, "webbase": T.PATH_ROWS}[name]
         assert st["numtileA"] == -1
         return
     assert st["path"] == T.PATH_TILES

@@ -180,8 +180,9 @@ def test_rows_aat_lj_prefix():
 
 
 def test_default_routing_declines_hub_dominated(monkeypatch):
-    """A product whose longest row passes kRowsMaxRowProducts (65,536) is
-    declined by the row-merge setup and runs on the staged tile pipeline."""
+    """A product with a hub row (past kRowsHubProducts = 65,536 products) that no
+    single run dominates is declined by the row-merge setup and runs on the
+    staged tile pipeline."""
     monkeypatch.delenv("TSG_PATH", raising=False)
     n, nb = 300, 100_000
     rng = np.random.default_rng(21)
@@ -202,10 +203,10 @@ def test_default_routing_declines_hub_dominated(monkeypatch):
     assert st["path"] == T.PATH_TILES
 
 
-def test_default_routing_fused_by_longest_row(monkeypatch):
-    """The fused path is chosen by the longest C row's element products (the
-    setup's statistic), not by longest A row x longest B row: a 100-entry A row
-    over 1-entry B rows, beside a 40-entry B row that no long A row selects."""
+def test_default_routing_short_rows_row_merge(monkeypatch):
+    """Short C rows (a 100-entry A row over 1-entry B rows, beside a 40-entry B
+    row that no long A row selects) take the row-merge path by default (the
+    fused path only when forced)."""
     monkeypatch.delenv("TSG_PATH", raising=False)
     n = 200
     brows = [np.array([(3 * j) % n]) for j in range(n)]
@@ -213,7 +214,7 @@ def test_default_routing_fused_by_longest_row(monkeypatch):
     B = _csr(n, n, [np.unique(r) for r in brows])
     arows = [np.arange(100)] + [np.array([150, (i * 11) % 100]) for i in range(1, 60)]
     A = _csr(60, n, [np.unique(r) for r in arows])
-    st = _check(A, B, real=True, seed=13, path=T.PATH_FUSED)
+    _check(A, B, real=True, seed=13, path=T.PATH_ROWS)
 
 
 def test_rows_class_boundaries_by_entries():
@@ -293,3 +294,47 @@ def test_rows_mawi_prefix_hub_rows():
     P = np.diff(cum[:r + 1])
     assert P.max() > 65536
     _check((r, n, rp[:r + 1].copy(), ci[:rp[r]].copy(), vv[:rp[r]].copy()), (m, n, rp, ci, vv), real=True, seed=47)
+
+
+def test_default_routing_wide_b_skips_fused(monkeypatch):
+    """Short C rows (the fused path's kind) with B wider than its segment keys
+    hold (B.n >= 2^28 - 16): the default route must not send them to the fused
+    path (which is UNSUPPORTED there) but to the row-merge path.  Checked
+    against a per-row numpy product (the oracle's dense row accumulator would
+    need B.n doubles per thread)."""
+    monkeypatch.delenv("TSG_PATH", raising=False)
+    rng = np.random.default_rng(51)
+    n = (1 << 28) + 1000
+    nb = 300
+    Brows = [np.sort(rng.choice(n, size=int(rng.integers(1, 6)), replace=False)) for _ in range(nb)]
+    B = _csr(nb, n, Brows)
+    arows = [np.sort(rng.choice(nb, size=int(rng.integers(0, 5)), replace=False)) for _ in range(200)]
+    A = _csr(200, nb, arows)
+    av = rng.uniform(-1, 1, len(A[3]))
+    bv = rng.uniform(-1, 1, len(B[3]))
+    Am = T.Matrix.from_csr(200, nb, A[2], A[3], av)
+    Bm = T.Matrix.from_csr(nb, n, B[2], B[3], bv)
+    Cm, st = T.spgemm(Am, Bm)
+    assert st["path"] == T.PATH_ROWS
+    _, _, grp, gci, gvv = Cm.csr()
+    want_rp, want_ci, want_v = [0], [], []
+    for i in range(200):
+        cols, vals = [], []
+        for p in range(A[2][i], A[2][i + 1]):
+            j = A[3][p]
+            cols.append(B[3][B[2][j]:B[2][j + 1]])
+            vals.append(av[p] * bv[B[2][j]:B[2][j + 1]])
+        if cols:
+            c = np.concatenate(cols)
+            v = np.concatenate(vals)
+            u, inv = np.unique(c, return_inverse=True)
+            s = np.zeros(len(u))
+            np.add.at(s, inv, v)
+            want_ci.append(u)
+            want_v.append(s)
+            want_rp.append(want_rp[-1] + len(u))
+        else:
+            want_rp.append(want_rp[-1])
+    np.testing.assert_array_equal(grp, np.array(want_rp))
+    np.testing.assert_array_equal(gci, np.concatenate(want_ci))
+    np.testing.assert_allclose(gvv, np.concatenate(want_v), rtol=1e-12, atol=1e-15)
