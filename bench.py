@@ -190,10 +190,27 @@ def tiled_leg(m, n, rp, ci, vv, mb, nb, rpb, cib, vvb, aat, tm, nnzcub, reps=3):
     runs = runs[1:]  # first call warms the context's caching allocator
     med = lambda k: float(np.median([r[0][k] for r in runs]))
     t = med("time_tile")
+    numblk, nnzc = int(runs[0][1]), int(runs[0][0]["nnzC"])
+    # roofline of the timed region (steps 1-3): the reference's byte model
+    # (B_alg) and, for context, the bytes of the reference LAYOUT the
+    # region must write -- C's tile structure (column + row index), tile_nnz, the
+    # per-tile row pointers and masks (tm u16 each, tm/16 mask words per row),
+    # the u16 local columns and fp64 values -- plus the A/B tile payloads it reads
+    b_alg = 4.0 * (m + 1) + 12.0 * len(ci) + 4.0 * (mb + 1) + 12.0 * len(cib) + 4.0 * (m + 1) + 12.0 * nnzc
+    wpr = max(1, tm // 16)
+    layout = (4.0 * (m // tm + 2) + 12.0 * numblk + 2.0 * tm * numblk * (1 + wpr) + 10.0 * nnzc
+              + 10.0 * (len(ci) + len(cib)))
     return {"t_kern_tiled_ms": round(t, 4), "gflops": round(2.0 * nnzcub / (t * 1e-3) / 1e9, 3),
             "t_step1_ms": round(med("time_step1"), 4), "t_step2_ms": round(med("time_step2"), 4),
             "t_step3_ms": round(med("time_step3"), 4), "t_malloc_ms": round(med("time_malloc"), 4),
-            "numblkC": int(runs[0][1]), "nnzC": int(runs[0][0]["nnzC"]), "reps": reps,
+            "numblkC": numblk, "nnzC": nnzc, "reps": reps, "tile": tm,
+            "roofline": {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                         "algorithmic_bytes": int(b_alg), "achieved": round(b_alg / (t * 1e-3) / 1e9, 2),
+                         "frac": round(b_alg / (t * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                         "layout_bytes": int(layout), "layout_achieved": round(layout / (t * 1e-3) / 1e9, 2),
+                         "layout_frac": round(layout / (t * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                         "note": "B_alg / the timed region (steps 1-3); layout_bytes = the reference tiled C "
+                                 "arrays written + the A/B tile payloads read"},
             "path": "tsg_tilespgemm (reference tiled layout in/out; the ./test CLI path)"}
 
 
@@ -424,6 +441,10 @@ def main():
                        "time")
         traffic, traffic_src = pmc_traffic(["k_rows_small", "k_rows_merge", "k_rows_bitmap", "k_rows_hwin",
                                             "k_rows_dr_"], workload)
+    elif path_id == 2:
+        kernel_desc = ("band row kernel k_band_rows (one workgroup per C row, LDS window accumulator): "
+                       "B_alg of SURVEY §8d / HIP-event kernel time")
+        traffic, traffic_src = pmc_traffic(["k_band_rows"], workload)
     else:
         kernel_desc = "step-3 numeric kernel (fused tile2csr): B_alg of SURVEY §8d / HIP-event kernel time"
         traffic, traffic_src = pmc_traffic(["k_step3"], workload)
