@@ -140,8 +140,11 @@ int tsg_tilespgemm(tsg_smatrix *A, tsg_smatrix *B, tsg_smatrix *C,
 int tsg_tile2csr(tsg_smatrix *C, int tile_size_m, int tile_size_n);
 
 /* One shot CSR -> CSR: C = A * B, fp64, structural pattern (no zero dropping),
- * ascending columns.  Runs csr2tile(A), csr2tile(B), steps 1-3 and tile2csr on
- * the GPU.  C->rowpointer/columnindex/value are malloc'd. stats may be NULL. */
+ * ascending columns.  Uploads A and B and runs tsg_dev_spgemm (below) -- the
+ * routed device pipeline (row-merge, banded or staged tile path, whichever
+ * its statistics pick; stats->path says which) -- then downloads C.  The same C
+ * as csr2tile + steps 1-3 + tile2csr.  C->rowpointer/columnindex/value are
+ * malloc'd. stats may be NULL. */
 int tsg_spgemm_csr(const tsg_smatrix *A, const tsg_smatrix *B, tsg_smatrix *C,
                    int tile_size_m, int tile_size_n, tsg_stats *stats);
 

@@ -155,6 +155,7 @@ struct RowsPlan {
     int ncls[8] = {};
     long long products = 0, hprod = 0, pmax = 0;  // all / class-H rows' products, the longest row's
     long long drprod = 0, hubrest = 0;  // hub rows' products: one run dominant (DR kernels) / not
+    long long hbig = 0;        // class-H rows' products past the one-walk register share (their scratch)
 };
 // Class-H rows past kRowsHubProducts products are hub rows: one run holding all
 // but 4,096 of them -> the dominant-run kernels (k_rows_dr_*), else the windowed

@@ -58,6 +58,11 @@ constexpr long long RH_SPAN = (long long)RH_WORDS * 64;  // columns per window (
 constexpr int RH_BLK = 512;           // words per rank block (int prefix); u16 prefix per 4-word group inside
 constexpr int RH_NBLK = RH_WORDS / RH_BLK;
 constexpr int RH_NGRP = RH_WORDS / 4;
+constexpr int RH_PPT = 16;            // class H, one-walk rows: products per thread held in registers
+constexpr int OW_CH = RH_PPT * RH_NT;  // ... so many per row (past it: the row's scratch slots)
+constexpr int OW_CV = 2 * RH_WORDS;    // column ranks per pass (int in the bitmap's LDS)
+constexpr int OW_RUNS = 2 * RH_NT;     // runs of a one-walk row (two per thread)
+static_assert(OW_CH <= RH_WORDS, "one-walk rows: a pass's values fit the bitmap's LDS");
 
 __device__ __forceinline__ u32 lanes_below(u64 b) {
     return __builtin_amdgcn_mbcnt_hi((u32)(b >> 32), __builtin_amdgcn_mbcnt_lo((u32)b, 0u));
@@ -69,8 +74,8 @@ __device__ __forceinline__ int key_col(u64 k) { return (int)(k >> 32); }
 // TSG_ROWS_PROF builds (make prof): per-phase wall-clock totals of the class
 // kernels' workgroups (thread 0 after each phase's barrier), printed per call
 #ifdef TSG_ROWS_PROF
-__device__ unsigned long long g_rows_prof[3][256][8];  // (spread over 256 slots: few same-address atomics)
-#define RP_INIT unsigned long long rp_acc[8] = {}, rp_t = wall_clock64();
+__device__ unsigned long long g_rows_prof[3][256][12];  // (spread over 256 slots: few same-address atomics)
+#define RP_INIT unsigned long long rp_acc[12] = {}, rp_t = wall_clock64();
 #define RP(k)                                         \
     do {                                              \
         const unsigned long long _t = wall_clock64(); \
@@ -80,7 +85,7 @@ __device__ unsigned long long g_rows_prof[3][256][8];  // (spread over 256 slots
 #define RP_DONE(K)                                                          \
     do {                                                                    \
         if (threadIdx.x == 0)                                               \
-            for (int _k = 0; _k < 8; ++_k) atomicAdd(&g_rows_prof[K][blockIdx.x & 255][_k], rp_acc[_k]); \
+            for (int _k = 0; _k < 12; ++_k) atomicAdd(&g_rows_prof[K][blockIdx.x & 255][_k], rp_acc[_k]); \
     } while (0)
 #else
 #define RP_INIT
@@ -110,7 +115,7 @@ struct RowsArgs {
 // (also zeroes the binning kernel's counters: no separate memset in the stream)
 __global__ __launch_bounds__(WG) void k_rows_entries(const int *ciA, long nnzA, const int *rpB, int2 *ebnd,
                                                      long long *E, int *cls) {
-    if (blockIdx.x == 0 && threadIdx.x < 24) cls[threadIdx.x] = 0;  // (class counts, statistics, cursors)
+    if (blockIdx.x == 0 && threadIdx.x < 32) cls[threadIdx.x] = 0;  // (class counts, statistics, cursors)
     for (long a = (long)blockIdx.x * WG + threadIdx.x; a <= nnzA; a += (long)gridDim.x * WG) {
         if (a == nnzA) {
             E[a] = 0;
@@ -138,7 +143,8 @@ __device__ __forceinline__ int row_class(long long P, int k) {
 // rows without products get nnz 0; hst[0] = the class-H rows' products, hst[1]
 // = the largest row's products (the routing statistics), hst[2] = all products,
 // hst[3] / hst[4] = the products of hub rows (past kRowsHubProducts) that one
-// run dominates (all but DR_SMAX products in it) / that none does
+// run dominates (all but DR_SMAX products in it) / that none does, hst[8] =
+// the class-H rows' products past OW_CH (the one-walk rows' scratch)
 // (*Etot, copied so that one read-back brings everything); rnnz[m] = 0 (the
 // row pointers' n+1 slot).  A workgroup per
 // BIN_ROWS rows: its counts first (one atomic per class), then its rows in
@@ -157,7 +163,7 @@ __global__ __launch_bounds__(WG) void k_rows_bin(const int *rpA, int m, const lo
         rnnz[m] = 0;
     }
     int n[NCLS] = {};
-    long long hp = 0, pmax = 0, drp = 0, hubr = 0;
+    long long hp = 0, pmax = 0, drp = 0, hubr = 0, hbig = 0;
     constexpr int RPT = BIN_ROWS / WG;  // rows per thread: every load of a sweep issued together
     int ra0[RPT], ra1[RPT];
 #pragma unroll
@@ -184,6 +190,7 @@ __global__ __launch_bounds__(WG) void k_rows_bin(const int *rpA, int m, const lo
 #pragma unroll
         for (int t = 0; t < NCLS; ++t) n[t] += c == t;
         hp += c == NCLS - 1 ? P : 0;
+        hbig += c == NCLS - 1 && P <= kRowsHubProducts && P > OW_CH ? P - OW_CH : 0;
         pmax = max(pmax, P);
         if (P > kRowsHubProducts) {  // a hub row: dominated by one run (-> the DR kernels) or not
             long long lmax = 0;
@@ -194,6 +201,7 @@ __global__ __launch_bounds__(WG) void k_rows_bin(const int *rpA, int m, const lo
     hp = block_sum(hp, red64);
     drp = block_sum(drp, red64);
     hubr = block_sum(hubr, red64);
+    hbig = block_sum(hbig, red64);
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) pmax = max(pmax, __shfl_xor(pmax, d, 64));
     if (lane == 0) red64[wv] = pmax;
@@ -204,6 +212,7 @@ __global__ __launch_bounds__(WG) void k_rows_bin(const int *rpA, int m, const lo
         if (pmax) atomicMax(&hst[1], (unsigned long long)pmax);
         if (drp) atomicAdd(&hst[3], (unsigned long long)drp);
         if (hubr) atomicAdd(&hst[4], (unsigned long long)hubr);
+        if (hbig) atomicAdd(&hst[8], (unsigned long long)hbig);
     }
 #pragma unroll
     for (int t = 0; t < NCLS; ++t) {
@@ -860,7 +869,8 @@ __device__ __forceinline__ int bm_rank(const u64 *bm, const u16 *g4, const int *
     return rk;
 }
 
-__global__ __launch_bounds__(RH_NT) void k_rows_bitmap(RowsArgs g) {
+__global__ __launch_bounds__(RH_NT) void k_rows_bitmap(RowsArgs g, int *Tc, double *Tx, int *Tr,
+                                                      unsigned long long *tcur) {
     {  // (hub rows, past kRowsHubProducts: k_rows_hwin's or the DR kernels')
         const int4 le0 = g.list[blockIdx.x];
         if (g.E[le0.y + le0.z] - g.E[le0.y] > kRowsHubProducts) return;  // (workgroup-uniform)
@@ -898,8 +908,172 @@ __global__ __launch_bounds__(RH_NT) void k_rows_bitmap(RowsArgs g) {
         lo = min(lo, red[w]);
         hi = max(hi, red[NW + w]);
     }
+    const int P = (int)(g.E[a0 + k] - base);  // (<= kRowsHubProducts: hub rows left above)
+    if (k <= OW_RUNS && (long long)hi - lo < RH_SPAN) {  // (workgroup-uniform)
+        // one window, ONE walk: each product's column and value gathered together
+        // once -- the first OW_CH products held in registers, the rest (rows past
+        // OW_CH products) in this row's scratch slots -- then ranks; the bitmap's
+        // LDS then holds the columns at their ranks (copied out coalesced) and
+        // the values (ds_add_f64 at the ranks, copied out), OW_CV / OW_CH ranks
+        // per pass.  No global atomic, no second walk over B.
+        // run table (2 runs per thread; the walk table's LDS): product prefix, B start
+        int *const opre = reinterpret_cast<int *>(&wt);
+        int *const obs = opre + OW_RUNS;
+        __syncthreads();  // (red: the span's reduction read above)
+        {
+            int2 be0 = make_int2(0, 0), be1 = make_int2(0, 0);
+            if (2 * tid < k) be0 = g.ebnd[a0 + 2 * tid];
+            if (2 * tid + 1 < k) be1 = g.ebnd[a0 + 2 * tid + 1];
+            const int l0 = be0.y - be0.x, l1 = be1.y - be1.x;
+            const int inc = wave_incl_scan_dpp(l0 + l1);
+            if (lane == 63) red[wv] = inc;
+            __syncthreads();
+            int woff = 0;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) woff += w < wv ? red[w] : 0;
+            const int ex = woff + inc - l0 - l1;
+            opre[2 * tid] = ex;
+            opre[2 * tid + 1] = ex + l0;
+            obs[2 * tid] = be0.x;
+            obs[2 * tid + 1] = be1.x;
+        }
+        __shared__ long long s_toff;
+        if (tid == 0 && P > OW_CH) s_toff = (long long)atomicAdd(tcur, (unsigned long long)(P - OW_CH));
+        const int nwd = (int)(((long long)hi - lo + 64) >> 6);
+        for (int i = tid; i < nwd; i += RH_NT) bm[i] = 0ull;
+        __syncthreads();
+        // products q = j * RH_NT + tid, four at a time: run search, then the
+        // column, value and A value loads together
+        auto gather4 = [&](int j0, int (&c4)[4], double (&x4)[4]) {
+            int b[4], len2[4], q[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                q[u] = (j0 + u) * RH_NT + tid;
+                b[u] = 0;
+                len2[u] = q[u] < P ? k : 0;
+                c4[u] = -1;
+                x4[u] = 0.0;
+            }
+            const bool ub[4] = {true, true, true, true};
+            search_ilp(opre, b, len2, q, ub);  // b - 1 = the run holding product q
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (q[u] < P) {
+                    const int jr = b[u] - 1;
+                    const int pp = obs[jr] + q[u] - opre[jr];
+                    c4[u] = g.Bcol[pp] - lo;
+                    x4[u] = g.vA[a0 + jr] * g.Bval[pp];
+                }
+        };
+        int cc[RH_PPT];
+        double xx[RH_PPT];
+#pragma unroll
+        for (int j0 = 0; j0 < RH_PPT; j0 += 4) {
+            int c4[4];
+            double x4[4];
+            if (j0 * RH_NT < P) {  // (workgroup-uniform)
+                gather4(j0, c4, x4);
+            } else {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    c4[u] = -1;
+                    x4[u] = 0.0;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                cc[j0 + u] = c4[u];
+                xx[j0 + u] = x4[u];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < RH_PPT; ++j)
+            if (cc[j] >= 0) atomicOr(&bm[cc[j] >> 6], 1ull << (cc[j] & 63));
+        const long long toff = P > OW_CH ? s_toff - OW_CH : 0;  // scratch slot of product q: toff + q
+        for (int j0 = RH_PPT; j0 * RH_NT < P; j0 += 4) {  // (workgroup-uniform) products past OW_CH
+            int c4[4];
+            double x4[4];
+            gather4(j0, c4, x4);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (c4[u] >= 0) {
+                    atomicOr(&bm[c4[u] >> 6], 1ull << (c4[u] & 63));
+                    const long long t = toff + (j0 + u) * RH_NT + tid;
+                    Tc[t] = c4[u];
+                    Tx[t] = x4[u];
+                }
+        }
+        __syncthreads();
+        for (int b = wv; b < RH_NBLK; b += NW) {
+            const int w0 = b * RH_BLK + lane * 8;
+            int s0 = 0, s1 = 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                s0 += w0 + u < nwd ? __popcll(bm[w0 + u]) : 0;
+                s1 += w0 + 4 + u < nwd ? __popcll(bm[w0 + 4 + u]) : 0;
+            }
+            const int inc = wave_incl_scan_dpp(s0 + s1);
+            g4[w0 / 4] = (u16)(inc - s0 - s1);
+            g4[w0 / 4 + 1] = (u16)(inc - s1);
+            if (lane == 63) blk[b] = inc;
+        }
+        __syncthreads();
+        if (wv == 0) {
+            const int v = lane < RH_NBLK ? blk[lane] : 0;
+            const int inc = wave_incl_scan_dpp(v);
+            if (lane < RH_NBLK) blk[lane] = inc - v;
+            if (lane == 63) red[0] = inc;
+        }
+        __syncthreads();
+        const int wn = red[0];
+        RP(6);
+        int rk[RH_PPT];
+#pragma unroll
+        for (int j = 0; j < RH_PPT; ++j) rk[j] = cc[j] >= 0 ? bm_rank(bm, g4, blk, cc[j]) : 0;
+        for (int q = OW_CH + tid; q < P; q += RH_NT) Tr[toff + q] = bm_rank(bm, g4, blk, Tc[toff + q]);
+        RP(8);
+        __syncthreads();  // (every bitmap read done: its LDS becomes the columns, then the values)
+        RP(9);
+        // the columns at their ranks in LDS (a column's products store the same
+        // one), then out coalesced; OW_CV ranks per pass
+        int *const cl = reinterpret_cast<int *>(bm);
+        for (int r0 = 0; r0 < wn; r0 += OW_CV) {
+#pragma unroll
+            for (int j = 0; j < RH_PPT; ++j)
+                if (cc[j] >= 0 && (unsigned)(rk[j] - r0) < (unsigned)OW_CV) cl[rk[j] - r0] = cc[j];
+            for (int q = OW_CH + tid; q < P; q += RH_NT) {
+                const int rq = Tr[toff + q] - r0;
+                if ((unsigned)rq < (unsigned)OW_CV) cl[rq] = Tc[toff + q];
+            }
+            __syncthreads();
+            const int n = min(OW_CV, wn - r0);
+            for (int i = tid; i < n; i += RH_NT) g.Scol[base + r0 + i] = lo + cl[i];
+            __syncthreads();
+        }
+        // the values: OW_CH ranks per pass
+        double *const val = reinterpret_cast<double *>(bm);
+        for (int r0 = 0; r0 < wn; r0 += OW_CH) {
+            const int n = min(OW_CH, wn - r0);
+            for (int i = tid; i < n; i += RH_NT) val[i] = 0.0;
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < RH_PPT; ++j)
+                if (cc[j] >= 0 && (unsigned)(rk[j] - r0) < (unsigned)OW_CH) atomicAdd(&val[rk[j] - r0], xx[j]);
+            for (int q = OW_CH + tid; q < P; q += RH_NT) {
+                const int rq = Tr[toff + q] - r0;
+                if ((unsigned)rq < (unsigned)OW_CH) atomicAdd(&val[rq], Tx[toff + q]);
+            }
+            __syncthreads();
+            RP(10);
+            for (int i = tid; i < n; i += RH_NT) g.Sval[base + r0 + i] = val[i];
+            __syncthreads();
+        }
+        if (tid == 0) g.rnnz[r] = wn;
+        RP(7);
+        RP_DONE(0);
+        return;
+    }
     if (k <= RH_NT) rows_batch(g, a0, k, 0, wt);  // one batch: its run table serves every walk
-    RP(0);
     long long out = 0;  // nonzeros of the earlier windows
     for (long long wlo = lo; wlo <= hi; wlo += RH_SPAN) {
         const long long whi = min((long long)hi, wlo + RH_SPAN - 1);
@@ -1596,7 +1770,9 @@ int dev_rows_setup_async(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B
     TSG_TRY(cx.get(&p.E, (size_t)A.nnz + 1));
     TSG_TRY(cx.get(&p.lists, (size_t)NCLS * (m > 0 ? m : 1)));
     TSG_TRY(cx.get(&p.soff, (size_t)m + 1));
-    TSG_TRY(cx.get(&p.cls, 24));  // class counts, 5 u64 statistics at [8..18), hub rows' cursors at [18..24)
+    // class counts [0..8), 5 u64 statistics [8..18), hub rows' cursors [18..22), the one-walk
+    // rows' scratch products (u64) [24..26) and its cursor [26..28)
+    TSG_TRY(cx.get(&p.cls, 32));
     TSG_TRY(cx.get(&p.rowpointer, (size_t)m + 1));
     unsigned long long *hst = reinterpret_cast<unsigned long long *>(p.cls + 8);
     k_rows_entries<<<grid_for((long)A.nnz + 1, WG, 16384), WG, 0, s>>>(A.columnindex, A.nnz, B.rowpointer, p.ebnd,
@@ -1607,7 +1783,7 @@ int dev_rows_setup_async(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B
     k_rows_bin<<<max(1, (m + BIN_ROWS - 1) / BIN_ROWS), WG, 0, s>>>(A.rowpointer, m, p.E, p.E + A.nnz, p.rowpointer,
                                                                     p.lists, p.cls, p.soff, hst);
     TSG_HIP(hipGetLastError());
-    TSG_HIP(hipMemcpyAsync(cx.pinned64, p.cls, 18 * sizeof(int), hipMemcpyDeviceToHost, s));
+    TSG_HIP(hipMemcpyAsync(cx.pinned64, p.cls, 26 * sizeof(int), hipMemcpyDeviceToHost, s));
     return TSG_OK;
 }
 
@@ -1618,6 +1794,7 @@ void dev_rows_setup_read(Context &cx, RowsPlan &p) {
     p.products = cx.pinned64[6];
     p.drprod = cx.pinned64[7];
     p.hubrest = cx.pinned64[8];
+    p.hbig = cx.pinned64[12];
 }
 
 // routing: the path is built for rows of modest length (class H's bitmap rows a
@@ -1658,7 +1835,7 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
 #ifdef TSG_ROWS_PROF
     unsigned long long *dprof = nullptr;
     TSG_HIP(hipGetSymbolAddress((void **)&dprof, HIP_SYMBOL(g_rows_prof)));
-    TSG_HIP(hipMemsetAsync(dprof, 0, sizeof(unsigned long long) * 3 * 256 * 8, s));
+    TSG_HIP(hipMemsetAsync(dprof, 0, sizeof(unsigned long long) * 3 * 256 * 12, s));
 #endif
     RowsArgs g{A.rowpointer, A.value, ebnd, E, B.columnindex, B.value, nullptr, 0, C.rowpointer, Scol, Sval};
     // the classes in turn on the call's stream, heaviest first: class H alone
@@ -1687,8 +1864,8 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
         k_rows_order_h<<<1, OH_NT, 0, s>>>(E, p.cls, lists + (long)(NCLS - 1) * m);
         TSG_HIP(hipGetLastError());
     }
-    int *Tcol = nullptr;
-    double *Tval = nullptr;
+    int *Tcol = nullptr, *Oc = nullptr, *Or = nullptr;
+    double *Tval = nullptr, *Ox = nullptr;
     DrRow *drows = nullptr;
     DrEnt *dents = nullptr;
     int2 *dchunks = nullptr;
@@ -1704,7 +1881,13 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
             TSG_HIP(hipGetLastError());
         }
         if (p.hprod > p.drprod + p.hubrest) {  // rows of the one-window bitmap kernel
-            k_rows_bitmap<<<ncls[7], RH_NT, 0, s>>>(g);
+            if (p.hbig > 0) {  // one-walk rows past OW_CH products: their scratch
+                TSG_TRY(cx.get(&Oc, (size_t)p.hbig));
+                TSG_TRY(cx.get(&Ox, (size_t)p.hbig));
+                TSG_TRY(cx.get(&Or, (size_t)p.hbig));
+            }
+            k_rows_bitmap<<<ncls[7], RH_NT, 0, s>>>(g, Oc, Ox, Or,
+                                                   reinterpret_cast<unsigned long long *>(p.cls + 26));
             TSG_HIP(hipGetLastError());
         }
         if (p.drprod > 0) {  // hub rows with a dominant run
@@ -1728,18 +1911,18 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
     if (ev) TSG_HIP(hipEventRecord(ev[5], s));
 #ifdef TSG_ROWS_PROF
     {
-        static unsigned long long raw[3 * 256 * 8];
-        unsigned long long pr[24] = {};
+        static unsigned long long raw[3 * 256 * 12];
+        unsigned long long pr[36] = {};
         TSG_HIP(hipMemcpyAsync(raw, dprof, sizeof(raw), hipMemcpyDeviceToHost, s));
         TSG_TRY(stream_wait(s));
         for (int c = 0; c < 3; ++c)
             for (int b = 0; b < 256; ++b)
-                for (int k = 0; k < 8; ++k) pr[c * 8 + k] += raw[(c * 256 + b) * 8 + k];
+                for (int k = 0; k < 12; ++k) pr[c * 12 + k] += raw[(c * 256 + b) * 12 + k];
         static const char *nm[3] = {"H", "M2-M4", "M0-M1"};
         for (int c = 0; c < 3; ++c) {
             const int cnt = c == 0 ? ncls[7] : c == 1 ? ncls[4] + ncls[5] + ncls[6] : ncls[2] + ncls[3];
             fprintf(stderr, "rows %s (%d rows) us/row:", nm[c], cnt);
-            for (int k = 0; k < 6; ++k) fprintf(stderr, " %.2f", cnt ? pr[c * 8 + k] / 100.0 / cnt : 0.0);
+            for (int k = 0; k < 12; ++k) fprintf(stderr, " %.2f", cnt ? pr[c * 12 + k] / 100.0 / cnt : 0.0);
             fprintf(stderr, "\n");
         }
     }
@@ -1791,6 +1974,9 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
     cx.put(Sval);
     cx.put(Tcol);
     cx.put(Tval);
+    cx.put(Oc);
+    cx.put(Ox);
+    cx.put(Or);
     cx.put(drows);
     cx.put(dents);
     cx.put(dchunks);

@@ -5,9 +5,12 @@ products: ranks by counting in 16 or 64 lanes), M0..M4 (<= 256 / 512 /
 bitonic sorts of packed (column, position) keys in registers and LDS, or
 merge-path rounds when the row's column span is too wide for packed keys) and
 H (longer rows or more entries: an LDS column bitmap per window of 1,048,576
-columns, f64 atomics for the values; hub rows past 65,536 products: the
-windowed kernel -- products bucketed by column, LDS bitmaps of 262,144
-columns, values added in LDS).  TSG_PATH=rows forces the path.  Pattern
+columns; rows of one window and <= 2,048 entries walk their products once --
+registers, then scratch past 16,384 -- and take columns and values through the
+bitmap's LDS by rank; other rows walk twice with f64 atomics for the values;
+hub rows past 65,536 products: the windowed kernel -- products bucketed by
+column, LDS bitmaps of 262,144 columns, values added in LDS -- or the
+dominant-run kernels).  TSG_PATH=rows forces the path.  Pattern
 bit-exact, values within 1e-10 relative, against the oracle (the reference's
 semantics: steps 1-3 + tile2csr, tilespgemm-cuda.h:279-2218)."""
 import numpy as np
@@ -338,3 +341,57 @@ def test_default_routing_wide_b_skips_fused(monkeypatch):
     np.testing.assert_array_equal(grp, np.array(want_rp))
     np.testing.assert_array_equal(gci, np.concatenate(want_ci))
     np.testing.assert_allclose(gvv, np.concatenate(want_v), rtol=1e-12, atol=1e-15)
+
+
+def test_rows_class_h_one_walk_rows():
+    """Class H's one-walk rows (tsg_rows.hip k_rows_bitmap: one gather walk, the
+    first 16,384 products in registers and the rest in the row's scratch slots,
+    columns and values through the bitmap's LDS by rank passes of 32,768 /
+    16,384): rows at the register boundary (16,384 and 16,385 products), past it
+    with up to 2,048 runs (two passes of column ranks, four of values), a row
+    of 2,049 runs and one spanning two column windows (both the windowed
+    bitmap walk), with repeated columns and real values."""
+    rng = np.random.default_rng(21)
+    nb, ncol = 6000, 3_000_000
+    lens = np.where(np.arange(nb) % 2 == 0, rng.integers(1, 5, nb), rng.integers(20, 60, nb))
+    brows = []
+    for i in range(nb):
+        lo = 0 if i % 3 else 40_000  # clustered and spread columns: repeats and unique ones
+        hi = 200_000 if i % 3 else 900_000
+        brows.append(np.sort(rng.choice(np.arange(lo, hi), size=int(lens[i]), replace=False)))
+    brows[nb - 1] = np.array([0, 2_500_000])  # the two-window row's far column
+    Bc = _csr(nb, ncol, brows)
+    blen = np.diff(Bc[2].astype(np.int64))
+
+    def pick(target, must=None, long_only=False):
+        """distinct B rows whose lengths sum to exactly `target` products"""
+        order = rng.permutation(nb - 1)
+        if long_only:
+            order = order[blen[order] >= 8]
+        sel, tot = set(), 0
+        for b in order:
+            if tot + blen[b] <= target - 4:
+                sel.add(int(b))
+                tot += blen[b]
+        for b in rng.permutation(nb - 1):  # close the gap exactly with rows of 1-4 products
+            if tot == target:
+                break
+            if b not in sel and blen[b] <= target - tot:
+                sel.add(int(b))
+                tot += blen[b]
+        if must is not None:
+            sel.add(must)
+        return np.sort(np.array(sorted(sel)))
+
+    rows = [pick(16384), pick(16385), pick(24000), pick(61000, long_only=True), pick(9000)]
+    # 2,049 runs (past the one-walk run table): short B rows only
+    short = np.nonzero(blen <= 4)[0]
+    rows.append(np.sort(rng.choice(short[short < nb - 1], 2049, replace=False)))
+    rows.append(pick(6000, must=nb - 1))  # two column windows
+    A = _csr(len(rows), nb, rows)
+    P = [int(blen[r].sum()) for r in rows]
+    assert P[0] == 16384 and P[1] == 16385 and all(4096 < p <= 65536 for p in P)
+    assert max(len(r) for r in rows[:5]) <= 2048 and len(rows[5]) == 2049, [len(r) for r in rows]
+    cls = _classes(len(rows), nb, A[2], A[3], Bc[2])
+    assert (cls == H).all()
+    _check(A, Bc, real=True, seed=9)
