@@ -268,6 +268,10 @@ def main():
                     help="N>1: strong (default) = the fixed product, A's tile rows partitioned by "
                          "work + RCCL gather of C to rank 0; weak = every rank owns one A-sized row "
                          "block of the stacked product (fixed work per GPU, no data-path collective)")
+    ap.add_argument("--gather-sub", type=int, default=0,
+                    help="N>1 strong: each rank computes its rows as this many sub-blocks and sends each "
+                         "to rank 0 as soon as it is done, overlapping the gather with the next one "
+                         "(dist.StreamingGather); 0 = auto: 4 when a rank holds >= 2e8 products, else 1")
     ap.add_argument("--block-products", type=float, default=1.5e9,
                     help="row-block size (intermediate products) when the product exceeds int32 "
                          "nnz(C): such products run as sequential row blocks, C kept per block")
@@ -332,8 +336,8 @@ def main():
     # this rank's tile rows: strong = a contiguous block of ~equal work
     if world > 1 and not weak:
         work = tdist.tile_row_work(rp, ci, rpb, m, tm)
-        t0r, t1r = tdist.partition_tile_rows(work, world)[rank]
-        r_lo, r_hi = min(m, t0r * tm), min(m, t1r * tm)
+        rank_rows = [(min(m, a * tm), min(m, b * tm)) for a, b in tdist.partition_tile_rows(work, world)]
+        r_lo, r_hi = rank_rows[rank]
     else:
         r_lo, r_hi = 0, m
     # products past int32 nnz(C) (the reference's `int nnzC`): sequential row
@@ -341,6 +345,13 @@ def main():
     blocked = nnzcub_full > args.block_products
     blocks = tdist.product_blocks(cum, r_lo, r_hi, args.block_products, tm) if blocked else [(r_lo, r_hi)]
     gather = world > 1 and not weak and not blocked
+    nsub = 1
+    if gather:
+        # the overlapped gather: every rank's rows as nsub sub-blocks of ~equal products
+        nsub = args.gather_sub or (4 if max(cum[b] - cum[a] for a, b in rank_rows) >= 2e8 else 1)
+        subs = [tdist.sub_blocks(cum, a, b, nsub, tm) for a, b in rank_rows]
+        sub_rows = [[b1 - b0 for b0, b1 in sb] for sb in subs]
+        blocks = subs[rank]
     dA_blocks = []
     for (b0, b1) in blocks:
         mb_, rpb_, cib_, vvb_ = tdist.slice_rows(m, rp, ci, vv, b0, b1)
@@ -360,21 +371,32 @@ def main():
     def one_step():
         sts, nnz = [], 0
         c = None
-        for (_, _, dAb) in dA_blocks:
-            ctx.reset()
-            c, st = ctx.spgemm(dAb, dB, tm, tm)  # returns with C complete on the device
-            sts.append(st)
-            nnz += c.nnz
-        st = {k: sum(s[k] for s in sts) for k in sts[0]}
         if gather:
+            # sub-blocks in turn, each handed to the streaming gather as soon as its C
+            # is complete (the context keeps every sub-block's C until the step ends)
+            ctx.reset()
+            sg = tdist.StreamingGather(rank, world, sub_rows, device="cpu" if host_coll else "cuda")
+            for s, (_, _, dAb) in enumerate(dA_blocks):
+                c, st = ctx.spgemm(dAb, dB, tm, tm)
+                sts.append(st)
+                nnz += c.nnz
+                cv = ctx.view_torch(c)  # zero-copy views of the context-owned C
+                if host_coll:
+                    sg.push(s, cv.rowptr.cpu(), cv.col.cpu(), cv.val.cpu())
+                else:
+                    sg.push(s, cv.rowptr, cv.col, cv.val)
             g0 = time.perf_counter()
-            cblk = ctx.view_torch(c)  # zero-copy views of the context-owned C block
-            if host_coll:
-                gathered[0] = tdist.gather_csr_blocks(cblk.rowptr.cpu(), cblk.col.cpu(), cblk.val.cpu(), rank, world)
-            else:
-                gathered[0] = tdist.gather_csr_blocks(cblk.rowptr, cblk.col, cblk.val, rank, world)
+            gathered[0] = sg.finish()
+            if not host_coll:
                 torch.cuda.synchronize()
-            gather_ms.append((time.perf_counter() - g0) * 1e3)
+            gather_ms.append((time.perf_counter() - g0) * 1e3)  # (the part not hidden behind compute)
+        else:
+            for (_, _, dAb) in dA_blocks:
+                ctx.reset()
+                c, st = ctx.spgemm(dAb, dB, tm, tm)  # returns with C complete on the device
+                sts.append(st)
+                nnz += c.nnz
+        st = {k: sum(s[k] for s in sts) for k in sts[0]}
         return c, st, nnz
 
     for _ in range(args.warmup):
@@ -411,6 +433,12 @@ def main():
         mean = sum(ws) / world
         work_share = {"products": [int(x) for x in ws],
                       "max_over_mean": round(max(ws) / mean, 4) if mean > 0 else None}
+        if not weak and mean > 0:
+            # hub tile rows: a single tile row heavier than a rank's fair share
+            # bounds the imbalance (the partition keeps tile rows whole)
+            heavy = np.nonzero(work > mean)[0]
+            work_share["hub_tile_rows"] = [int(t) for t in heavy[:16]]
+            work_share["max_tile_row_over_mean"] = round(float(work.max()) / mean, 4)
     ms_per_step = elapsed * 1e3 / args.steps
     gflops = 2.0 * nnzcub_total * args.steps / elapsed / 1e9
 
@@ -420,8 +448,9 @@ def main():
     # SURVEY §8d algorithmic bytes (src/external/cusparse/main.cu:205-208), this rank's share
     mrank = r_hi - r_lo
     nnza_rank = int(rp[r_hi] - rp[r_lo])
-    b_alg = (4.0 * (mrank + len(blocks)) + 12.0 * nnza_rank + (4.0 * (mb + 1) + 12.0 * len(cib)) * len(blocks)
-             + 4.0 * (mrank + len(blocks)) + 12.0 * nnz_rank)
+    nb_calls = 1 if gather else len(blocks)  # (the gather's sub-blocks: B counted once, as one call)
+    b_alg = (4.0 * (mrank + nb_calls) + 12.0 * nnza_rank + (4.0 * (mb + 1) + 12.0 * len(cib)) * nb_calls
+             + 4.0 * (mrank + nb_calls) + 12.0 * nnz_rank)
     achieved_pipe = b_alg / (dev_ms * 1e-3) / 1e9
     # context only (never the graded figure): + one fp64 value and one u16 local column
     # per intermediate product of this rank (SURVEY §8d B_stream)
@@ -524,7 +553,8 @@ def main():
                        "numblkC_kind": ("element-level C tiles (non-empty 16x16 tiles of C; the reference's "
                                         "tile-pattern step 1 also lists empty ones, see t_kern_tiled)") if path_id == 0
                                        else "-1: this path builds no C tiles (the reference-layout tiled C: see tiled)",
-                       "row_blocks": len(blocks),
+                       "row_blocks": 1 if gather else len(blocks),
+                       "gather_sub": nsub if gather else None,
                        "parallelism": par},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
@@ -541,6 +571,8 @@ def main():
                                                         "t_kern_ms", "t_e2e_ms")},
             "stage_ms_min": {k: round(v, 4) for k, v in mins.items()},
             "gather_ms": round(float(np.median(gather_ms[-args.steps:])), 4) if gather_ms else None,
+            "gather_note": ("rank 0: the gather's exposed part (after the last sub-block's compute; the "
+                            "earlier sub-blocks travel while the next ones compute)") if gather_ms else None,
             "work_share": work_share,
             "gflops_kern": round(2.0 * nnzcub_total / (med["t_kern_ms"] * 1e-3) / 1e9, 3) if world == 1 else None,
             "tiled": tiled,

@@ -110,3 +110,114 @@ def gather_csr_blocks(rowptr, col, val, rank, world, device=None):
         ro += rows[r]
         no += nnzs[r]
     return out_rp, out_ci, out_v
+
+
+def sub_blocks(cum, r_lo, r_hi, nsub, tile_m):
+    """Rows [r_lo, r_hi) as `nsub` consecutive tile-row-aligned sub-blocks of
+    ~equal intermediate products (cum = nnzCub of the row prefixes); some may
+    be empty.  Every rank computes every rank's split the same way."""
+    cum = np.asarray(cum, dtype=np.int64)
+    bounds = [r_lo]
+    for s in range(1, nsub):
+        tgt = cum[r_lo] + (cum[r_hi] - cum[r_lo]) * s / nsub
+        b = int(np.searchsorted(cum, tgt, side="left")) // tile_m * tile_m
+        bounds.append(min(r_hi, max(bounds[-1], b)))
+    bounds.append(r_hi)
+    return list(zip(bounds[:-1], bounds[1:]))
+
+
+class StreamingGather:
+    """Gather of C row blocks to rank 0 overlapped with their computation.
+
+    Each rank computes its rows as sub-blocks (sub_blocks above) and hands
+    each one to push() as soon as it is done: a peer posts non-blocking sends
+    of its row pointers (whose last entry, nnz, sizes the rest) and then its
+    columns and values, and goes on computing the next sub-block while they
+    travel; rank 0 posts the row-pointer receive of every peer's next
+    sub-block ahead, and after each of its own sub-blocks turns the arrived
+    row pointers into the column / value receives.  Point-to-point messages
+    between a pair match in posting order (RCCL/NCCL P2P have no tags), so
+    every peer's sub-blocks are received in order.  finish() returns the
+    concatenated CSR (rank 0's sub-blocks, then rank 1's, ...) on rank 0 and
+    None elsewhere.  sub_rows[r] = the row counts of rank r's sub-blocks."""
+
+    def __init__(self, rank, world, sub_rows, device=None):
+        import torch
+        import torch.distributed as dist
+        self.t, self.d = torch, dist
+        self.rank, self.world, self.sub_rows = rank, world, sub_rows
+        self.dev = device
+        self.mine = []       # rank 0: its own sub-blocks
+        self.sends = []      # peers: (work handle, tensor) kept alive until finish
+        self.rp = {}         # rank 0: (peer, s) -> row pointer tensor being received
+        self.rp_work = {}
+        self.arr = {}        # rank 0: (peer, s) -> (col, val)
+        self.arr_work = []
+        self.next_s = [0] * world  # rank 0: each peer's next sub-block to turn into array receives
+        if rank == 0:
+            for r in range(1, world):
+                self._post_rp(r, 0)
+
+    def _post_rp(self, r, s):
+        if s >= len(self.sub_rows[r]):
+            return
+        buf = self.t.empty(self.sub_rows[r][s] + 1, dtype=self.t.int32, device=self.dev)
+        self.rp[(r, s)] = buf
+        self.rp_work[(r, s)] = self.d.irecv(buf, r)
+
+    def _advance(self, upto):
+        """rank 0: every peer's sub-blocks < upto: row pointers waited for,
+        column / value receives posted, the next row-pointer receive posted."""
+        for r in range(1, self.world):
+            while self.next_s[r] < min(upto, len(self.sub_rows[r])):
+                s = self.next_s[r]
+                self.rp_work.pop((r, s)).wait()
+                nnz = int(self.rp[(r, s)][-1].item())
+                col = self.t.empty(nnz, dtype=self.t.int32, device=self.dev)
+                val = self.t.empty(nnz, dtype=self.t.float64, device=self.dev)
+                if nnz:
+                    self.arr_work.append(self.d.irecv(col, r))
+                    self.arr_work.append(self.d.irecv(val, r))
+                self.arr[(r, s)] = (col, val)
+                self.next_s[r] = s + 1
+                self._post_rp(r, s + 1)
+
+    def push(self, s, rowptr, col, val):
+        """this rank's sub-block s (its rows' CSR; row pointers from 0)"""
+        if self.rank != 0:
+            rp = rowptr.contiguous()
+            self.sends.append((self.d.isend(rp, 0), rp))
+            if col.numel():
+                c, v = col.contiguous(), val.contiguous()
+                self.sends.append((self.d.isend(c, 0), c))
+                self.sends.append((self.d.isend(v, 0), v))
+            return
+        self.mine.append((rowptr, col, val))
+        self._advance(s + 1)  # (peers finish sub-block s about when rank 0 does)
+
+    def finish(self):
+        if self.rank != 0:
+            for w, _ in self.sends:
+                w.wait()
+            self.sends = []
+            return None
+        self._advance(max(len(x) for x in self.sub_rows))
+        for w in self.arr_work:
+            w.wait()
+        t = self.t
+        parts = [(rp, c, v) for rp, c, v in self.mine]
+        for r in range(1, self.world):
+            parts += [(self.rp[(r, s)],) + self.arr[(r, s)] for s in range(len(self.sub_rows[r]))]
+        M = sum(p[0].numel() - 1 for p in parts)
+        NNZ = sum(p[1].numel() for p in parts)
+        out_rp = t.empty(M + 1, dtype=t.int32, device=self.dev)
+        ro, no = 0, 0
+        for rp, c, v in parts:
+            k = rp.numel() - 1
+            out_rp[ro:ro + k + 1] = rp.to(t.int32) + no
+            ro += k
+            no += c.numel()
+        out_rp[M] = no
+        out_ci = t.cat([p[1] for p in parts]) if parts else t.empty(0, dtype=t.int32, device=self.dev)
+        out_v = t.cat([p[2] for p in parts]) if parts else t.empty(0, dtype=t.float64, device=self.dev)
+        return out_rp, out_ci, out_v

@@ -124,3 +124,62 @@ def test_product_blocks_cover_rows_within_cap(cap):
             assert b1 > b0 and (b0 % 16 == 0)
             work = cum[b1] - cum[b0]
             assert work <= cap or b1 - b0 <= 16
+
+
+def _worker_stream(rank, world, port, kind, nsub, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m, n, rp, ci, vv = _matrix(kind)
+        oB = O.transpose(O.OMat.from_csr(m, n, rp, ci, vv)) if kind == "aat" else O.OMat.from_csr(m, n, rp, ci, vv)
+        mb, nb, rpb, cib, vvb = oB.csr()
+        blen = np.diff(rpb.astype(np.int64))
+        cum = np.concatenate([[0], np.cumsum(blen[ci])])[rp]
+        parts = tdist.partition_tile_rows(tdist.tile_row_work(rp, ci, rpb, m, 16), world)
+        subs = [tdist.sub_blocks(cum, min(m, a * 16), min(m, b * 16), nsub, 16) for a, b in parts]
+        g = tdist.StreamingGather(rank, world, [[b1 - b0 for b0, b1 in sb] for sb in subs])
+        for s, (b0, b1) in enumerate(subs[rank]):  # each sub-block "computed" (oracle) then pushed
+            mk, rpk, cik, vvk = tdist.slice_rows(m, rp, ci, vv, b0, b1)
+            _, _, crp, cci, cvv = O.gustavson(O.OMat.from_csr(mk, n, rpk, cik, vvk), oB).csr()
+            g.push(s, torch.from_numpy(crp.astype(np.int32)), torch.from_numpy(cci.astype(np.int32)),
+                   torch.from_numpy(cvv.copy()))
+        out = g.finish()
+        if rank == 0:
+            q.put(("ok", subs, [x.numpy() for x in out]))
+        else:
+            assert out is None
+    except Exception as e:  # surface worker failures to the parent
+        q.put(("err", repr(e), None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,nsub", [(2, 3), (3, 4), (2, 1)])
+@pytest.mark.parametrize("kind", ["powerlaw", "aat", "empty"])
+def test_streaming_gather_of_sub_blocks_matches_full_product(world, nsub, kind):
+    """The overlapped gather (dist.StreamingGather): every rank's rows as
+    sub-blocks pushed as they are computed, rank 0 receiving them in order;
+    the gathered row pointers, columns and values equal the full product
+    array by array, and the sub-blocks tile each rank's rows."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_stream, args=(r, world, port, kind, nsub, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    status, subs, got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert status == "ok", subs
+    m, n, rp, ci, vv = _matrix(kind)
+    oA = O.OMat.from_csr(m, n, rp, ci, vv)
+    oB = O.transpose(oA) if kind == "aat" else O.OMat.alias(oA)
+    _, _, erp, eci, evv = O.gustavson(oA, oB).csr()
+    flat = [b for sb in subs for b in sb]
+    assert flat[0][0] == 0 and flat[-1][1] == m and all(flat[i][1] == flat[i + 1][0] for i in range(len(flat) - 1))
+    assert all(len(sb) == nsub for sb in subs)
+    np.testing.assert_array_equal(got[0], erp)
+    np.testing.assert_array_equal(got[1], eci)
+    np.testing.assert_array_equal(got[2], evv)

@@ -94,8 +94,10 @@ def test_mawi_eight_ranks_gather_vs_oracle(tmp_path):
     import _oracle as O
     (m, n, rp, ci, vv), rows = _mawi_rows(0.01, 2e8)
     dump = str(tmp_path / "c8.npz")
-    eight = _bench(8, None, 0, extra=("--matrix", "mawi", "--scale", "0.01", "--rows", str(rows), "--dump", dump))
+    eight = _bench(8, None, 0, extra=("--matrix", "mawi", "--scale", "0.01", "--rows", str(rows), "--dump", dump,
+                                      "--gather-sub", "3"))
     assert eight["n_gpus"] == 8 and eight["scaling"] == "strong"
+    assert eight["config"]["gather_sub"] == 3  # the overlapped gather: sub-blocks streamed to rank 0
     assert eight["config"]["parallelism"] == "row-block8 + RCCL gather"
     ws = eight["work_share"]
     assert len(ws["products"]) == 8 and sum(ws["products"]) == eight["config"]["nnzCub"]
@@ -125,4 +127,21 @@ def test_blocked_rows_equal_single_block():
     assert blk["config"]["nnzCub"] == one["config"]["nnzCub"]
     two = _bench(2, mtx, 0, extra=("--block-products", "300"))
     assert "sequential blocks" in two["config"]["parallelism"]
+    assert two["check"] == one["check"]
+
+
+@pytest.mark.parametrize("nsub", [1, 3])
+def test_two_ranks_streaming_gather_arrays(tmp_path, nsub):
+    """The overlapped gather (--gather-sub): each rank's rows as sub-blocks,
+    each sent to rank 0 as soon as its C is complete; the gathered C equals
+    the single-rank C array by array (--dump)."""
+    import numpy as np
+    mtx = os.path.join(REPO, "tests", "golden", "fixtures", "x_powerlaw_400.mtx")
+    d1, d2 = str(tmp_path / "one.npz"), str(tmp_path / "two.npz")
+    one = _bench(1, mtx, 0, extra=("--dump", d1))
+    two = _bench(2, mtx, 0, extra=("--dump", d2, "--gather-sub", str(nsub)))
+    assert two["config"]["gather_sub"] == nsub and two["gather_ms"] is not None
+    a, b = np.load(d1), np.load(d2)
+    for k in ("rowptr", "col", "val"):
+        np.testing.assert_array_equal(a[k], b[k])
     assert two["check"] == one["check"]
