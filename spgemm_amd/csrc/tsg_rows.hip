@@ -109,6 +109,7 @@ struct RowsArgs {
     int *rnnz;             // nnz of each row (the row pointers after a scan)
     int *Scol;             // staging: row r's nonzeros from E[rpA[r]]
     double *Sval;
+    const int *Crp;        // direct output (non-null): row r's nonzeros at Scol/Sval + Crp[r]
 };
 
 // per A entry: its B row's range and products (the latter scanned into E)
@@ -313,7 +314,7 @@ __global__ __launch_bounds__(WG) void k_rows_small(RowsArgs g) {
         r = e.x;
         a0 = e.y;
         k = e.z;
-        base = g.E[a0];  // (the staging offset: not waited for until the output)
+        base = g.Crp ? g.Crp[r] : g.E[a0];  // (the output offset: not waited for until the output)
     }
     // lane sl < k: run sl's B range and A value; the runs' offsets in the row
     // by a scan of their lengths over the group
@@ -387,7 +388,7 @@ __global__ __launch_bounds__(WG) void k_rows_small(RowsArgs g) {
         g.Scol[o] = col;
         g.Sval[o] = s;
     }
-    if (live && sl == 0) g.rnnz[r] = __popcll(hb);
+    if (live && sl == 0 && !g.Crp) g.rnnz[r] = __popcll(hb);
 }
 
 // U independent searches in lockstep (U LDS reads in flight per step): first
@@ -508,7 +509,7 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 8 : 1) void k_rows_merge(RowsArgs 
         be = g.ebnd[le.y + tid];
         av = g.vA[le.y + tid];
     }
-    const long long base = g.E[le.y];  // (the staging offset: not waited for until the output)
+    const long long base = g.Crp ? g.Crp[le.x] : g.E[le.y];  // (the output offset: not waited for until the output)
     double *const V = reinterpret_cast<double *>(kp[1][0]);
     {
         const int r = le.x;
@@ -744,7 +745,7 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 8 : 1) void k_rows_merge(RowsArgs 
             o += w < wv ? red[w] : 0;
             tot += red[w];
         }
-        if (tid == 0) g.rnnz[r] = tot;
+        if (tid == 0 && !g.Crp) g.rnnz[r] = tot;  // (direct output: counted before)
         if (packed) {
 #pragma unroll
             for (int u = 0; u < 4; ++u)
@@ -1699,6 +1700,160 @@ __global__ __launch_bounds__(DR_NT) void k_rows_dr_fill(RowsArgs g, const DrRow 
         }
 }
 
+// ---- direct output: every row's exact nnz before any class writes, so the
+// classes S16..M4 write C at its final CSR offsets (no staging, no second pass
+// over C).  A row's nnz is the number of distinct columns among its products:
+// each product's column inserted into an LDS hash set (Fibonacci hash, linear
+// probing, twice the class's products in slots), the successful inserts counted.
+// Only B's columns are read (4 B per product), no values, no sort.
+__device__ __forceinline__ bool hset_insert(u32 *ht, int hb, u32 c) {
+    u32 h = (c * 0x9E3779B1u) >> (32 - hb);
+    const u32 msk = (1u << hb) - 1u;
+    for (;;) {
+        const u32 old = atomicCAS(&ht[h], ~0u, c);  // (columns < 2^31: never the empty mark)
+        if (old == ~0u) return true;
+        if (old == c) return false;
+        h = (h + 1u) & msk;
+    }
+}
+
+// classes M0..M4: NT threads per row, four products per thread (the merge
+// kernels' run table and expansion, columns only)
+template <int NT, int CAP, int RUNS>
+__global__ __launch_bounds__(NT) void k_rows_count(RowsArgs g) {
+    constexpr int NW = NT / 64, HS = 2 * CAP;
+    constexpr int HB = CAP == 256 ? 9 : CAP == 512 ? 10 : CAP == 1024 ? 11 : CAP == 2048 ? 12 : 13;
+    static_assert((1 << HB) == HS && CAP == 4 * NT && RUNS <= NT, "count: table and thread shapes");
+    __shared__ u32 ht[HS];
+    __shared__ int roff[RUNS + 1];
+    __shared__ int rbs[RUNS];
+    __shared__ int red[2 * NW];
+    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    const int4 le = g.list[blockIdx.x];
+    int2 be = make_int2(0, 0);
+    if (tid < le.z) be = g.ebnd[le.y + tid];
+#pragma unroll
+    for (int u = 0; u < HS / NT; ++u) ht[u * NT + tid] = ~0u;
+    int k = 0, P = 0;
+    {
+        const int len = be.y - be.x;
+        const u64 b = __ballot(len > 0);
+        const int inc = wave_incl_scan_dpp(len);
+        if (lane == 63) {
+            red[wv] = __popcll(b);
+            red[NW + wv] = inc;
+        }
+        __syncthreads();
+        int off = 0, loff = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            off += w < wv ? red[w] : 0;
+            k += red[w];
+            loff += w < wv ? red[NW + w] : 0;
+            P += red[NW + w];
+        }
+        if (len > 0) {
+            const int d = off + lanes_below(b);
+            roff[d] = loff + inc - len;
+            rbs[d] = be.x;
+        }
+        if (tid == 0) roff[k] = P;
+        __syncthreads();
+    }
+    const int e0 = 4 * tid, ne = max(0, min(4, P - e0));
+    int c[4] = {0, 0, 0, 0};
+    {
+        int j = 0, pa[4] = {0, 0, 0, 0};
+        if (ne > 0) j = lower_bound_dev(roff, 0, k + 1, e0 + 1) - 1;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (u < ne) {
+                const int q = e0 + u;
+                while (roff[j + 1] <= q) ++j;
+                pa[u] = rbs[j] + q - roff[j];
+            }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (u < ne) c[u] = g.Bcol[pa[u]];
+    }
+    int cnt = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        if (u < ne) cnt += hset_insert(ht, HB, (u32)c[u]);
+    cnt = wave_sum(cnt);
+    __syncthreads();  // (red's run counts read by every thread above)
+    if (lane == 0) red[wv] = cnt;
+    __syncthreads();
+    if (tid == 0) {
+        int tot = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) tot += red[w];
+        g.rnnz[le.x] = tot;
+    }
+}
+
+// classes S16 / S64: G lanes per row (as k_rows_small), a 2G-slot set per row
+template <int G>
+__global__ __launch_bounds__(WG) void k_rows_count_small(RowsArgs g) {
+    constexpr int RPW = 64 / G, HB = G == 16 ? 5 : 7;
+    __shared__ u32 ht[WAVES][128];
+    const int lane = lane_id(), wv = wave_id(), sl = lane % G, gb = lane - sl;
+    const int i = (blockIdx.x * WAVES + wv) * RPW + lane / G;
+    if ((blockIdx.x * WAVES + wv) * RPW >= g.nrows) return;  // wave-uniform
+    ht[wv][lane] = ~0u;
+    ht[wv][lane + 64] = ~0u;
+    const bool live = i < g.nrows;
+    int r = 0, a0 = 0, k = 0;
+    if (live) {
+        const int4 e = g.list[i];
+        r = e.x;
+        a0 = e.y;
+        k = e.z;
+    }
+    int2 be = make_int2(0, 0);
+    if (sl < k) be = g.ebnd[a0 + sl];
+    const int len = be.y - be.x, bs = be.x;
+    int inc = len;
+    inc += dpp_mov<0x111, 0xf>(0, inc);
+    inc += dpp_mov<0x112, 0xf>(0, inc);
+    inc += dpp_mov<0x114, 0xf>(0, inc);
+    inc += dpp_mov<0x118, 0xf>(0, inc);
+    if constexpr (G == 64) {
+        inc += dpp_mov<0x142, 0xa>(0, inc);
+        inc += dpp_mov<0x143, 0xc>(0, inc);
+    }
+    const int roff = sl < k ? inc - len : INT_MAX;
+    const int P = __shfl(inc, G - 1, G);
+    int run = 0;
+    if constexpr (G == 64) {
+        for (int j = 1; j < k; ++j) run = (__builtin_amdgcn_readlane(roff, j) <= sl) ? j : run;
+    } else {
+#pragma unroll
+        for (int j = 1; j < G; ++j) run = __shfl(roff, j, G) <= sl ? j : run;
+    }
+    const int rs = __shfl(roff, run, G), rb = __shfl(bs, run, G);
+    bool fresh = false;
+    wave_lds_sync();  // (the sets' empty marks before any insert)
+    if (sl < P) fresh = hset_insert(&ht[wv][(lane / G) * 2 * G], HB, (u32)g.Bcol[rb + sl - rs]);
+    const u64 gm = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << gb;
+    const int n = __popcll(__ballot(fresh) & gm);
+    if (live && sl == 0) g.rnnz[r] = n;
+}
+
+// class H rows from the staging (at soff[r]) to their CSR place: a workgroup per row
+__global__ __launch_bounds__(WG) void k_rows_hcopy(const int4 *list, int n, const long long *soff, const int *Crp,
+                                                   const int *Scol, const double *Sval, int *Ccol, double *Cval) {
+    for (int i = blockIdx.x; i < n; i += gridDim.x) {
+        const int r = list[i].x;
+        const long long s = soff[r];
+        const int d = Crp[r], cnt = Crp[r + 1] - d;
+        for (int j = threadIdx.x; j < cnt; j += WG) {
+            __builtin_nontemporal_store(__builtin_nontemporal_load(Scol + s + j), Ccol + d + j);
+            __builtin_nontemporal_store(__builtin_nontemporal_load(Sval + s + j), Cval + d + j);
+        }
+    }
+}
+
 // every row's run from the staging area (at soff[r]) to its CSR place, by
 // chunks of CP_CH output positions (a workgroup each, consecutive lanes on
 // consecutive positions): the chunk's rows from cfirst (the row holding each
@@ -1826,10 +1981,19 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
     const long long products = p.products;
     int ncls[NCLS];
     for (int t = 0; t < NCLS; ++t) ncls[t] = p.ncls[t];
+    // TSG_ROWS_DIRECT=1: exact row counts first (k_rows_count*), the classes
+    // S16..M4 write C in place, only class H's rows go through the staging (and
+    // a copy): no products-sized staging for the other rows (less device
+    // memory), but on webbase the count kernels (318 us, latency-bound: three
+    // dependent loads per row) cost more than the compaction they save (e2e
+    // 1.40 vs 1.30 ms), so the default stages every row and compacts.
+    const bool direct = getenv("TSG_ROWS_DIRECT") && atoi(getenv("TSG_ROWS_DIRECT")) != 0;
     int *Scol = nullptr;
     double *Sval = nullptr;
-    TSG_TRY(cx.get(&Scol, (size_t)products + 1));
-    TSG_TRY(cx.get(&Sval, (size_t)products + 1));
+    if (!direct || ncls[7] > 0) {
+        TSG_TRY(cx.get(&Scol, (size_t)products + 1));
+        TSG_TRY(cx.get(&Sval, (size_t)products + 1));
+    }
     if (ev) TSG_HIP(hipEventRecord(ev[1], s));
     if (ev) TSG_HIP(hipEventRecord(ev[4], s));
 #ifdef TSG_ROWS_PROF
@@ -1901,68 +2065,99 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
             TSG_HIP(hipGetLastError());
         }
     }
-    TSG_TRY(launch_m(6, k_rows_merge<M4_NT, M4_CAP, M4_RUNS>, ncls[6], M4_NT, s));
-    TSG_TRY(launch_m(5, k_rows_merge<M3_NT, M3_CAP, M3_RUNS>, ncls[5], M3_NT, s));
-    TSG_TRY(launch_m(4, k_rows_merge<M2_NT, M2_CAP, M2_RUNS>, ncls[4], M2_NT, s));
-    TSG_TRY(launch_m(3, k_rows_merge<M1_NT, M1_CAP, M1_RUNS>, ncls[3], M1_NT, s));
-    TSG_TRY(launch_m(2, k_rows_merge<M0_NT, M0_CAP, M0_RUNS>, ncls[2], M0_NT, s));
-    TSG_TRY(launch(1, k_rows_small<64>, (ncls[1] + WAVES - 1) / WAVES, WG, s));
-    TSG_TRY(launch(0, k_rows_small<16>, (ncls[0] + 4 * WAVES - 1) / (4 * WAVES), WG, s));
-    if (ev) TSG_HIP(hipEventRecord(ev[5], s));
-#ifdef TSG_ROWS_PROF
-    {
-        static unsigned long long raw[3 * 256 * 12];
-        unsigned long long pr[36] = {};
-        TSG_HIP(hipMemcpyAsync(raw, dprof, sizeof(raw), hipMemcpyDeviceToHost, s));
-        TSG_TRY(stream_wait(s));
-        for (int c = 0; c < 3; ++c)
-            for (int b = 0; b < 256; ++b)
-                for (int k = 0; k < 12; ++k) pr[c * 12 + k] += raw[(c * 256 + b) * 12 + k];
-        static const char *nm[3] = {"H", "M2-M4", "M0-M1"};
-        for (int c = 0; c < 3; ++c) {
-            const int cnt = c == 0 ? ncls[7] : c == 1 ? ncls[4] + ncls[5] + ncls[6] : ncls[2] + ncls[3];
-            fprintf(stderr, "rows %s (%d rows) us/row:", nm[c], cnt);
-            for (int k = 0; k < 12; ++k) fprintf(stderr, " %.2f", cnt ? pr[c * 12 + k] / 100.0 / cnt : 0.0);
-            fprintf(stderr, "\n");
-        }
-    }
-#endif
-    // row counts -> row pointers -> the compaction, with no host round trip:
-    // nnz(C) <= products, so when the products fit int32 (and their 12 B each,
-    // beside the staging's 12 B, stay within kRowsProductSizedC) the result
-    // arrays are sized by them and nnz(C) comes back with the call's final
-    // synchronisation; otherwise -- or when that allocation fails -- the checked
-    // scan reads nnz(C) back first and C is sized exactly.
+    auto classes = [&]() -> int {
+        TSG_TRY(launch_m(6, k_rows_merge<M4_NT, M4_CAP, M4_RUNS>, ncls[6], M4_NT, s));
+        TSG_TRY(launch_m(5, k_rows_merge<M3_NT, M3_CAP, M3_RUNS>, ncls[5], M3_NT, s));
+        TSG_TRY(launch_m(4, k_rows_merge<M2_NT, M2_CAP, M2_RUNS>, ncls[4], M2_NT, s));
+        TSG_TRY(launch_m(3, k_rows_merge<M1_NT, M1_CAP, M1_RUNS>, ncls[3], M1_NT, s));
+        TSG_TRY(launch_m(2, k_rows_merge<M0_NT, M0_CAP, M0_RUNS>, ncls[2], M0_NT, s));
+        TSG_TRY(launch(1, k_rows_small<64>, (ncls[1] + WAVES - 1) / WAVES, WG, s));
+        TSG_TRY(launch(0, k_rows_small<16>, (ncls[0] + 4 * WAVES - 1) / (4 * WAVES), WG, s));
+        return TSG_OK;
+    };
+    // row counts -> row pointers -> C's arrays, with no host round trip: nnz(C)
+    // <= products, so when the products fit int32 (and their 12 B each, beside
+    // the staging's, stay within kRowsProductSizedC) the result arrays are sized
+    // by them and nnz(C) comes back with the call's final synchronisation;
+    // otherwise -- or when that allocation fails -- the checked scan reads nnz(C)
+    // back first and C is sized exactly.
     long long nnz = 0;  // (C.rowpointer[m] = 0 from the binning kernel)
     bool small = products <= 0x7fffffffLL && products * 12 <= kRowsProductSizedC;
-    if (small) {
-        TSG_TRY(scan_exclusive_i32(cx, C.rowpointer, (long)m + 1, s));
-        if (cx.get(&C.columnindex, (size_t)products + 1) != TSG_OK ||
-            cx.get(&C.value, (size_t)products + 1) != TSG_OK) {
-            cx.put(C.columnindex);
-            C.columnindex = nullptr;
-            small = false;  // (the scan's total is read back below)
-            TSG_TRY(read_i32(cx, C.rowpointer + m, &C.nnz, s));
-            nnz = C.nnz;
+    long long cap = 0;
+    auto scan_alloc = [&]() -> int {
+        if (small) {
+            TSG_TRY(scan_exclusive_i32(cx, C.rowpointer, (long)m + 1, s));
+            if (cx.get(&C.columnindex, (size_t)products + 1) != TSG_OK ||
+                cx.get(&C.value, (size_t)products + 1) != TSG_OK) {
+                cx.put(C.columnindex);
+                C.columnindex = nullptr;
+                small = false;  // (the scan's total is read back below)
+                TSG_TRY(read_i32(cx, C.rowpointer + m, &C.nnz, s));
+                nnz = C.nnz;
+            }
+        } else {  // the checked scan (nnz(C) past int32 fails)
+            TSG_TRY(scan_exclusive_i32_total(cx, C.rowpointer, (long)m + 1, s, &nnz));
+            if (nnz > 0x7fffffffLL) return TSG_ERR_OVERFLOW;
         }
-    } else {  // the checked scan (nnz(C) past int32 fails)
-        TSG_TRY(scan_exclusive_i32_total(cx, C.rowpointer, (long)m + 1, s, &nnz));
-        if (nnz > 0x7fffffffLL) return TSG_ERR_OVERFLOW;
-    }
-    const long long cap = small ? products : nnz;
-    if (!small) {
-        TSG_TRY(cx.get(&C.columnindex, (size_t)cap + 1));
-        TSG_TRY(cx.get(&C.value, (size_t)cap + 1));
-    }
+        cap = small ? products : nnz;
+        if (!small) {
+            TSG_TRY(cx.get(&C.columnindex, (size_t)cap + 1));
+            TSG_TRY(cx.get(&C.value, (size_t)cap + 1));
+        }
+        return TSG_OK;
+    };
     int *cfirst = nullptr;
-    if (cap > 0) {
-        const int nch = (int)((cap + CP_CH - 1) / CP_CH);
-        TSG_TRY(cx.get(&cfirst, (size_t)nch + 1));
-        k_rows_cfirst<<<grid_for(m, WG, 8192), WG, 0, s>>>(m, C.rowpointer, cfirst);
+    if (direct) {
+        // the classes' exact counts (class H's came with its rows, in the staging)
+        TSG_TRY(launch(6, k_rows_count<M4_NT, M4_CAP, M4_RUNS>, ncls[6], M4_NT, s));
+        TSG_TRY(launch(5, k_rows_count<M3_NT, M3_CAP, M3_RUNS>, ncls[5], M3_NT, s));
+        TSG_TRY(launch(4, k_rows_count<M2_NT, M2_CAP, M2_RUNS>, ncls[4], M2_NT, s));
+        TSG_TRY(launch(3, k_rows_count<M1_NT, M1_CAP, M1_RUNS>, ncls[3], M1_NT, s));
+        TSG_TRY(launch(2, k_rows_count<M0_NT, M0_CAP, M0_RUNS>, ncls[2], M0_NT, s));
+        TSG_TRY(launch(1, k_rows_count_small<64>, (ncls[1] + WAVES - 1) / WAVES, WG, s));
+        TSG_TRY(launch(0, k_rows_count_small<16>, (ncls[0] + 4 * WAVES - 1) / (4 * WAVES), WG, s));
+        TSG_TRY(scan_alloc());
+        g.Crp = C.rowpointer;
+        g.Scol = C.columnindex;
+        g.Sval = C.value;
+        TSG_TRY(classes());
+        if (ncls[7] > 0) {
+            k_rows_hcopy<<<min(ncls[7], 8192), WG, 0, s>>>(lists + (long)7 * m, ncls[7], soff, C.rowpointer, Scol,
+                                                           Sval, C.columnindex, C.value);
+            TSG_HIP(hipGetLastError());
+        }
+        if (ev) TSG_HIP(hipEventRecord(ev[5], s));
+    } else {
+        TSG_TRY(classes());
+        if (ev) TSG_HIP(hipEventRecord(ev[5], s));
+#ifdef TSG_ROWS_PROF
+        {
+            static unsigned long long raw[3 * 256 * 12];
+            unsigned long long pr[36] = {};
+            TSG_HIP(hipMemcpyAsync(raw, dprof, sizeof(raw), hipMemcpyDeviceToHost, s));
+            TSG_TRY(stream_wait(s));
+            for (int c = 0; c < 3; ++c)
+                for (int b = 0; b < 256; ++b)
+                    for (int k = 0; k < 12; ++k) pr[c * 12 + k] += raw[(c * 256 + b) * 12 + k];
+            static const char *nm[3] = {"H", "M2-M4", "M0-M1"};
+            for (int c = 0; c < 3; ++c) {
+                const int cnt = c == 0 ? ncls[7] : c == 1 ? ncls[4] + ncls[5] + ncls[6] : ncls[2] + ncls[3];
+                fprintf(stderr, "rows %s (%d rows) us/row:", nm[c], cnt);
+                for (int k = 0; k < 12; ++k) fprintf(stderr, " %.2f", cnt ? pr[c * 12 + k] / 100.0 / cnt : 0.0);
+                fprintf(stderr, "\n");
+            }
+        }
+#endif
+        TSG_TRY(scan_alloc());
+        if (cap > 0) {
+            const int nch = (int)((cap + CP_CH - 1) / CP_CH);
+            TSG_TRY(cx.get(&cfirst, (size_t)nch + 1));
+            k_rows_cfirst<<<grid_for(m, WG, 8192), WG, 0, s>>>(m, C.rowpointer, cfirst);
+            TSG_HIP(hipGetLastError());
+            k_rows_compact<<<nch, WG, 0, s>>>(m, cfirst, soff, C.rowpointer, Scol, Sval, C.columnindex, C.value);
+        }
         TSG_HIP(hipGetLastError());
-        k_rows_compact<<<nch, WG, 0, s>>>(m, cfirst, soff, C.rowpointer, Scol, Sval, C.columnindex, C.value);
     }
-    TSG_HIP(hipGetLastError());
     if (small) TSG_HIP(hipMemcpyAsync(cx.pinned64 + 15, C.rowpointer + m, sizeof(int), hipMemcpyDeviceToHost, s));
     if (ev) TSG_HIP(hipEventRecord(ev[3], s));
     TSG_TRY(stream_wait(s));

@@ -395,3 +395,18 @@ def test_rows_class_h_one_walk_rows():
     cls = _classes(len(rows), nb, A[2], A[3], Bc[2])
     assert (cls == H).all()
     _check(A, Bc, real=True, seed=9)
+
+
+def test_rows_direct_output_mode(monkeypatch):
+    """TSG_ROWS_DIRECT=1: exact row counts (LDS hash sets, k_rows_count*) before
+    the classes, which then write C at its final offsets; class H rows through
+    the staging and k_rows_hcopy.  Every class (webbase), real values, edge
+    cases, duplicate runs."""
+    monkeypatch.setenv("TSG_ROWS_DIRECT", "1")
+    m, n, rp, ci, vv = synth.GENERATORS["webbase"]()
+    assert all((_classes(m, n, rp, ci, rp) == c).any() for c in range(H + 1))
+    _check((m, n, rp, ci, vv), real=True, seed=21)
+    test_rows_random_mixed_classes_real_values()
+    test_rows_edge_cases()
+    test_rows_duplicate_runs_sum()
+    _check(synth.GENERATORS["mc2depi"](), aat=True)
