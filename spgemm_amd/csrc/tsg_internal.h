@@ -154,15 +154,15 @@ struct RowsPlan {
     int *rowpointer = nullptr; // C's row pointers (row counts until the scan)
     int ncls[8] = {};
     long long products = 0, hprod = 0, pmax = 0;  // all / class-H rows' products, the longest row's
-    long long drprod = 0, hubrest = 0;  // hub rows' products: one run dominant (DR kernels) / not
+    long long hubprod = 0;     // hub rows' products (past kRowsHubProducts)
+    long long hk = 0;          // class-H rows with more runs than the one-walk kernel takes
     long long hbig = 0;        // class-H rows' products past the one-walk register share (their scratch)
 };
 // Class-H rows past kRowsHubProducts products are hub rows: one run holding all
-// but 4,096 of them -> the dominant-run kernels (k_rows_dr_*), else the windowed
-// kernel (k_rows_hwin); the shorter ones take the one-window bitmap kernel
-// (k_rows_bitmap).  Unless forced, the path declines (dev_rows_accept false)
-// products with hub rows of the second kind, or whose bitmap-kernel rows hold
-// over a quarter of the work.
+// but 4,096 of them -> the dominant-run kernels (k_rows_dr_*); the other hub
+// rows and the rows past the one-walk kernel's runs or column span -> the
+// windowed kernels (k_rows_w*: (row, column window) units); the rest the
+// one-walk bitmap kernel (k_rows_bitmap).
 constexpr long long kRowsHubProducts = 65536;
 // the row-merge path sizes C by the products (no read-back of nnz(C) before the
 // compaction) while their 12 B each stay within this; past it C is sized exactly

@@ -143,9 +143,9 @@ __device__ __forceinline__ int row_class(long long P, int k) {
 // rows -> classes: lists (class c's rows from lists + c*m) and counts cls[0..NCLS);
 // rows without products get nnz 0; hst[0] = the class-H rows' products, hst[1]
 // = the largest row's products (the routing statistics), hst[2] = all products,
-// hst[3] / hst[4] = the products of hub rows (past kRowsHubProducts) that one
-// run dominates (all but DR_SMAX products in it) / that none does, hst[8] =
-// the class-H rows' products past OW_CH (the one-walk rows' scratch)
+// hst[3] = the products of hub rows (past kRowsHubProducts), hst[4] = the
+// class-H rows with more than OW_RUNS runs, hst[8] = the class-H rows'
+// products past OW_CH (the one-walk rows' scratch)
 // (*Etot, copied so that one read-back brings everything); rnnz[m] = 0 (the
 // row pointers' n+1 slot).  A workgroup per
 // BIN_ROWS rows: its counts first (one atomic per class), then its rows in
@@ -193,11 +193,10 @@ __global__ __launch_bounds__(WG) void k_rows_bin(const int *rpA, int m, const lo
         hp += c == NCLS - 1 ? P : 0;
         hbig += c == NCLS - 1 && P <= kRowsHubProducts && P > OW_CH ? P - OW_CH : 0;
         pmax = max(pmax, P);
-        if (P > kRowsHubProducts) {  // a hub row: dominated by one run (-> the DR kernels) or not
-            long long lmax = 0;
-            for (int a = ra0[u]; a < ra1[u]; ++a) lmax = max(lmax, E[a + 1] - E[a]);
-            if (P - lmax <= DR_SMAX) drp += P; else hubr += P;
-        }
+        // hub rows (the DR or windowed kernels decide which, k_rows_wplan) and
+        // class-H rows with more runs than the one-walk kernel takes
+        if (P > kRowsHubProducts) drp += P;
+        if (c == NCLS - 1 && ra1[u] - ra0[u] > OW_RUNS) ++hubr;
     }
     hp = block_sum(hp, red64);
     drp = block_sum(drp, red64);
@@ -821,38 +820,35 @@ __device__ __forceinline__ void rows_batch(const RowsArgs &g, int a0, int k, int
     if (tid == 0) tb.tot = tot;
     __syncthreads();
 }
-// every product of the row (its column, and with VAL its a*b) to f; the run
-// table is reloaded per batch unless the row has one batch (loaded by the caller)
+// products [q0, q1) of a batch whose run table tb holds (rows_batch; nb runs),
+// U per thread at a time: each product's column (and with VAL its a*b) to f
 template <bool VAL, class F>
-__device__ __forceinline__ void rows_walk(const RowsArgs &g, int a0, int k, WalkTab &tb, F &&f) {
+__device__ __forceinline__ void batch_walk(const RowsArgs &g, int nb, int q0, int q1, const WalkTab &tb, F &&f) {
     constexpr int U = 4;
     const int tid = threadIdx.x;
-    for (int b0 = 0; b0 < k; b0 += RH_NT) {
-        if (k > RH_NT) rows_batch(g, a0, k, b0, tb);
-        const int nb = min(RH_NT, k - b0), tot = tb.tot;
-        for (int q0 = 0; q0 < tot; q0 += U * RH_NT) {
-            int b[U], len2[U], q[U], p[U], c[U];
-            double x[U];
+    for (int qb = q0; qb < q1; qb += U * RH_NT) {
+        int b[U], len2[U], q[U], c[U];
+        double x[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                q[u] = q0 + u * RH_NT + tid;
-                b[u] = 0;
-                len2[u] = q[u] < tot ? nb : 0;
-            }
-            const bool ub[U] = {true, true, true, true};
-            search_ilp(tb.pre, b, len2, q, ub);  // b - 1 = the run holding product q
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (q[u] < tot) {
-                    p[u] = tb.bs[b[u] - 1] + q[u] - tb.pre[b[u] - 1];
-                    c[u] = g.Bcol[p[u]];
-                    if (VAL) x[u] = tb.av[b[u] - 1] * g.Bval[p[u]];
-                }
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (q[u] < tot) f(c[u], VAL ? x[u] : 0.0);
+        for (int u = 0; u < U; ++u) {
+            q[u] = qb + u * RH_NT + tid;
+            b[u] = 0;
+            len2[u] = q[u] < q1 ? nb : 0;
+            c[u] = 0;
+            x[u] = 0.0;
         }
-        if (k > RH_NT) __syncthreads();
+        const bool ub[U] = {true, true, true, true};
+        search_ilp(tb.pre, b, len2, q, ub);  // b - 1 = the run holding product q
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (q[u] < q1) {
+                const int pp = tb.bs[b[u] - 1] + q[u] - tb.pre[b[u] - 1];
+                c[u] = g.Bcol[pp];
+                if (VAL) x[u] = tb.av[b[u] - 1] * g.Bval[pp];
+            }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (q[u] < q1) f(c[u], x[u]);
     }
 }
 
@@ -872,7 +868,7 @@ __device__ __forceinline__ int bm_rank(const u64 *bm, const u16 *g4, const int *
 
 __global__ __launch_bounds__(RH_NT) void k_rows_bitmap(RowsArgs g, int *Tc, double *Tx, int *Tr,
                                                       unsigned long long *tcur) {
-    {  // (hub rows, past kRowsHubProducts: k_rows_hwin's or the DR kernels')
+    {  // (hub rows, past kRowsHubProducts: the windowed or the DR kernels')
         const int4 le0 = g.list[blockIdx.x];
         if (g.E[le0.y + le0.z] - g.E[le0.y] > kRowsHubProducts) return;  // (workgroup-uniform)
     }
@@ -910,7 +906,9 @@ __global__ __launch_bounds__(RH_NT) void k_rows_bitmap(RowsArgs g, int *Tc, doub
         hi = max(hi, red[NW + w]);
     }
     const int P = (int)(g.E[a0 + k] - base);  // (<= kRowsHubProducts: hub rows left above)
-    if (k <= OW_RUNS && (long long)hi - lo < RH_SPAN) {  // (workgroup-uniform)
+    // (rows of more runs or a wider span: the windowed kernels, k_rows_w*)
+    if (k > OW_RUNS || (long long)hi - lo >= RH_SPAN) return;  // (workgroup-uniform)
+    {
         // one window, ONE walk: each product's column and value gathered together
         // once -- the first OW_CH products held in registers, the rest (rows past
         // OW_CH products) in this row's scratch slots -- then ranks; the bitmap's
@@ -1074,110 +1072,6 @@ __global__ __launch_bounds__(RH_NT) void k_rows_bitmap(RowsArgs g, int *Tc, doub
         RP_DONE(0);
         return;
     }
-    if (k <= RH_NT) rows_batch(g, a0, k, 0, wt);  // one batch: its run table serves every walk
-    long long out = 0;  // nonzeros of the earlier windows
-    for (long long wlo = lo; wlo <= hi; wlo += RH_SPAN) {
-        const long long whi = min((long long)hi, wlo + RH_SPAN - 1);
-        const int nwd = (int)((whi - wlo + 64) >> 6);
-        for (int i = tid; i < nwd; i += RH_NT) bm[i] = 0ull;
-        __syncthreads();
-        RP(1);
-        rows_walk<false>(g, a0, k, wt, [&](int col, double) {
-            const long long c = (long long)col - wlo;
-            if (c >= 0 && c < RH_SPAN) atomicOr(&bm[c >> 6], 1ull << (c & 63));
-        });
-        __syncthreads();
-        RP(2);
-        // ranks: a wave per 512-word block (lane: two 4-word groups), then the blocks
-        for (int b = wv; b < RH_NBLK; b += NW) {
-            const int w0 = b * RH_BLK + lane * 8;
-            int s0 = 0, s1 = 0;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                s0 += w0 + u < nwd ? __popcll(bm[w0 + u]) : 0;
-                s1 += w0 + 4 + u < nwd ? __popcll(bm[w0 + 4 + u]) : 0;
-            }
-            const int inc = wave_incl_scan_dpp(s0 + s1);
-            g4[w0 / 4] = (u16)(inc - s0 - s1);
-            g4[w0 / 4 + 1] = (u16)(inc - s1);
-            if (lane == 63) blk[b] = inc;
-        }
-        __syncthreads();
-        if (wv == 0) {
-            const int v = lane < RH_NBLK ? blk[lane] : 0;
-            const int inc = wave_incl_scan_dpp(v);
-            if (lane < RH_NBLK) blk[lane] = inc - v;
-            if (lane == 63) red[0] = inc;
-        }
-        __syncthreads();
-        const int wn = red[0];
-        RP(3);
-        // the window's values zeroed (coalesced); the walk below stores each column
-        // at its rank (a column's products store the same value) and adds the values
-        // with workgroup-scope atomics.  Ordering: __syncthreads' workgroup release
-        // compiles to a bare s_barrier here (no vmcnt wait: the ISA showed the
-        // zeroing stores still in flight at the barrier), so each wave drains its
-        // own stores first -- every zero has completed before any atomic issues.
-        // (An agent-scope fence instead wrote the L2 back, ~85 us per window.)
-        for (int i = tid; i < wn; i += RH_NT) g.Sval[base + out + i] = 0.0;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        RP(4);
-        rows_walk<true>(g, a0, k, wt, [&](int col, double x) {
-            const long long c = (long long)col - wlo;
-            if (c >= 0 && c < RH_SPAN) {
-                const long long o = base + out + bm_rank(bm, g4, blk, c);
-                g.Scol[o] = col;
-                __hip_atomic_fetch_add(&g.Sval[o], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-        });
-        out += wn;
-        __syncthreads();
-        RP(5);
-    }
-    if (tid == 0) g.rnnz[r] = (int)out;
-    RP_DONE(0);
-}
-
-// ---- class H, windowed: a workgroup per row, any length (web-graph heavy
-// rows, R-MAT and mawi hub rows alike).
-//   1. one walk over the row's products (runs in batches of HW_RUNS, flattened
-//      over the threads): each product's (column, a*b) stored in expansion
-//      order into the row's own staging slots (coalesced; the products bound
-//      the row's nonzeros, so the slots exist);
-//   2. the row's column span cut into buckets of 2^bs columns (at most
-//      HW_MAXB): a counting pass and a scatter pass over those slots (both
-//      streaming) gather each bucket's products into the row's region of a
-//      bucket area -- skipped when the span fits one window;
-//   3. each bucket in column order, as windows of 2^HW_WB columns: a bitmap of
-//      the window in LDS (its products' bits ORed in), ranks by popcount
-//      prefixes, the values added at their ranks in LDS (ds_add_f64), and the
-//      window's nonzeros emitted in column order at the row's running output
-//      offset -- no per-product global atomic, no second gather of B.
-// A window with more than HW_VCAP nonzeros takes its values in rank chunks of
-// HW_VCAP (one more streaming pass over the window's products per chunk).  The
-// bucket pass is skipped only for a row of one window and at most HW_VCAP
-// products, which then reads its slots and writes its output in place.
-constexpr int HW_NT = 1024;
-constexpr int HW_RUNS = 512;                    // runs per walk batch
-constexpr int HW_WB = 18;                       // window: 2^18 columns
-constexpr int HW_WORDS = (1 << HW_WB) / 64;     // 4,096 bitmap words: 32 KB
-constexpr int HW_BLK = 512;                     // words per rank block
-constexpr int HW_NBLK = HW_WORDS / HW_BLK;      // 8
-constexpr int HW_NGRP = HW_WORDS / 4;
-constexpr int HW_VCAP = 4096;                   // window nonzeros with LDS values: 32 KB
-constexpr int HW_MAXB = 256;                    // buckets per row
-
-__device__ __forceinline__ int hw_rank(const u64 *bm, const u16 *g4, const int *blk, int c) {
-    const int w = c >> 6, gi = w >> 2, sub = w & 3;
-    const ulonglong2 lo = reinterpret_cast<const ulonglong2 *>(bm)[gi * 2];
-    const ulonglong2 hi = reinterpret_cast<const ulonglong2 *>(bm)[gi * 2 + 1];
-    const u64 word = sub == 0 ? lo.x : sub == 1 ? lo.y : sub == 2 ? hi.x : hi.y;
-    int rk = blk[w / HW_BLK] + g4[gi] + __popcll(word & ((1ull << (c & 63)) - 1ull));
-    rk += sub > 0 ? __popcll(lo.x) : 0;
-    rk += sub > 1 ? __popcll(lo.y) : 0;
-    rk += sub > 2 ? __popcll(hi.x) : 0;
-    return rk;
 }
 
 // the longest run of a row (entries a0 .. a0+k, products from the prefix E)
@@ -1186,12 +1080,20 @@ __device__ __forceinline__ long long row_longest_run(const long long *E, int a0,
     const int nw = blockDim.x >> 6, lane = lane_id(), wv = wave_id();
     long long best = -1;
     int bj = INT_MAX;
-    for (int j = threadIdx.x; j < k; j += blockDim.x) {
-        const long long len = E[a0 + j + 1] - E[a0 + j];
-        if (len > best) {
-            best = len;
-            bj = j;
+    for (int j0 = threadIdx.x; j0 < k; j0 += 4 * blockDim.x) {  // (four runs' loads in flight)
+        long long e0[4], e1[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = min(j0 + u * (int)blockDim.x, k - 1);
+            e0[u] = E[a0 + j];
+            e1[u] = E[a0 + j + 1];
         }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (j0 + u * (int)blockDim.x < k && e1[u] - e0[u] > best) {
+                best = e1[u] - e0[u];
+                bj = j0 + u * (int)blockDim.x;
+            }
     }
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) {
@@ -1223,256 +1125,402 @@ __device__ __forceinline__ long long row_longest_run(const long long *E, int a0,
     return best;
 }
 
-struct HwTab {
-    int pre[HW_RUNS];     // products before each run of the batch
-    int bs[HW_RUNS];      // B start
-    double av[HW_RUNS];   // A value
-    int red[HW_NT / 64];
-    int tot;
-};
+// ---- windowed rows (W rows): class-H rows that neither the one-walk bitmap
+// kernel (more than OW_RUNS runs or a span past RH_SPAN) nor the dominant-run
+// kernels take -- R-MAT hub rows (LiveJournal: rows of 10^5..10^7 products over
+// 4 M columns, half of them repeated columns).  Each such row is cut into
+// windows of 2^wb columns (wb per row, so that a window holds about W_UNIT
+// products); a (row, window) pair is a UNIT, and units, not rows, are what the
+// kernels spread over the GPU:
+//   k_rows_wplan   a workgroup per class-H row: DR / one-walk / W, the W row's
+//                  span, wb, its units and its chunks (W_CH products of one run
+//                  batch each);
+//   k_rows_wchunks the chunk list and each unit's row;
+//   k_rows_wcount  a workgroup per chunk: the chunk's products counted per
+//                  window in LDS, one global add per nonempty window;
+//   k_rows_wscan   per W row, the units' counts scanned (bucket offsets inside
+//                  the row's staging slots, later the output offsets);
+//                  (that add's result: the chunk's place in the window's bucket);
+//   k_rows_wscatter a workgroup per chunk: each product's (column, a*b) to its
+//                  window's bucket in the row's staging, at the chunk's place
+//                  plus an LDS cursor;
+//   k_rows_wunit   a workgroup per unit: the bucket's columns ORed into an LDS
+//                  bitmap of the window, ranks by popcount prefixes, the values
+//                  added at their ranks in LDS, the unit's nonzeros out in
+//                  column order (to a second area: the bucket is still read);
+//   k_rows_wgather each unit's nonzeros to the row's staging slots at the
+//                  unit's output offset (then the common compaction).
+// Every product is read from B once for its column (counts) and once with its
+// value (scatter), then through its bucket once; no global atomic per
+// product, and a hub row's work is spread over as many workgroups as it has
+// chunks and units.
+constexpr int W_NT = RH_NT;        // (the run-batch tables are RH_NT wide)
+constexpr int W_CH = 32768;        // products per chunk
+constexpr int W_UNIT = 8192;       // products per unit, the target of wb
+constexpr int W_MAXW = 8192;       // windows per row
+constexpr int W_WBMIN = 8, W_WBMAX = 18;
+constexpr int W_WORDS = (1 << W_WBMAX) / 64;  // bitmap words of the widest window: 32 KB
+constexpr int W_BLK = 512;                    // words per rank block
+constexpr int W_NBLK = W_WORDS / W_BLK;
+constexpr int W_VCAP = 4096;                  // a unit's values per LDS pass
+constexpr int W_RPT = 8;                      // a unit's products per thread held in registers
 
-__global__ __launch_bounds__(HW_NT, 8) void k_rows_hwin(RowsArgs g, int *Tcol, double *Tval,
-                                                     unsigned long long *tnext) {
-    constexpr int NW = HW_NT / 64;
-    __shared__ __align__(16) u64 bm[HW_WORDS];
-    __shared__ u16 g4[HW_NGRP];
-    __shared__ int blk[HW_NBLK];
-    __shared__ __align__(16) double vals[HW_VCAP];
-    __shared__ HwTab tb;
-    __shared__ int bcnt[HW_MAXB + 1];   // per bucket: products, then (scanned) first slot
-    __shared__ int bcur[HW_MAXB];       // scatter cursors
+__device__ __forceinline__ int ceil_log2_ll(long long v) {
+    int l = 0;
+    while ((1ll << l) < v) ++l;
+    return l;
+}
+
+// (W_NT threads) workgroup sum of a long long
+__device__ __forceinline__ long long w_block_sum(long long x, long long *red) {
+    constexpr int NW = W_NT / 64;
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) x += __shfl_xor(x, d, 64);
+    __syncthreads();
+    if (lane_id() == 0) red[wave_id()] = x;
+    __syncthreads();
+    long long t = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) t += red[w];
+    return t;
+}
+
+// a workgroup per class-H row i.  Outputs (zero unless a W row): wnw[i] units,
+// wnch[i] chunks, wlo[i] first column, wwb[i] window bits, wpre[i] products;
+// wst[0] += W rows' products, wst[1] / wst[2] += DR rows' products / rows.
+__global__ __launch_bounds__(W_NT) void k_rows_wplan(RowsArgs g, int *wnw, int *wnch, int *wlo, int *wwb,
+                                                    long long *wpre, long long *wmat, unsigned long long *wst) {
+    constexpr int NW = W_NT / 64;
     __shared__ int red[2 * NW];
-    __shared__ long long s_toff;
-    RP_INIT
+    __shared__ long long red64[NW];
     const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
-    const int4 le = g.list[blockIdx.x];
-    const int r = le.x, a0 = le.y, k = le.z;
-    const long long base = g.E[a0];
-    const int P = (int)(g.E[a0 + k] - base);
-    if (P <= kRowsHubProducts) return;  // (k_rows_bitmap's row; workgroup-uniform)
-    {
+    const int i = blockIdx.x;
+    const int4 le = g.list[i];
+    const int a0 = le.y, k = le.z;
+    const long long base = g.E[a0], P = g.E[a0 + k] - base;
+    int nw = 0, nch = 0, lo = 0, wb = 0;
+    long long pw = 0;
+    bool dr = false;
+    if (P > kRowsHubProducts) {
         int jl;
-        const long long lmax = row_longest_run(g.E, a0, k, &jl, red);
-        if (P - lmax <= DR_SMAX) return;  // (the DR kernels' row)
+        const long long L = row_longest_run(g.E, a0, k, &jl, red);
+        dr = P - L <= DR_SMAX;
     }
-    int *const Acol = g.Scol + base;  // the row's staging slots: expansion-order products, then its output
-    double *const Aval = g.Sval + base;
-    // the row's columns [lo, hi] (each run's first and last)
-    int lo = INT_MAX, hi = -1;
-    for (int j = tid; j < k; j += HW_NT) {
-        const int2 be = g.ebnd[a0 + j];
-        if (be.y > be.x) {
-            lo = min(lo, g.Bcol[be.x]);
-            hi = max(hi, g.Bcol[be.y - 1]);
-        }
-    }
-    lo = wave_last(wave_incl_dpp(lo, INT_MAX, OpMin{}));
-    hi = wave_last(wave_incl_dpp(hi, INT_MIN, OpMax{}));
-    if (lane == 0) {
-        red[wv] = lo;
-        red[NW + wv] = hi;
-    }
-    __syncthreads();
-    lo = red[0];
-    hi = red[NW];
+    if (!dr) {
+        int l = INT_MAX, h = -1;
+        for (int j0 = tid; j0 < k; j0 += 4 * W_NT) {  // (four runs' loads in flight)
+            int2 be[4];
 #pragma unroll
-    for (int w = 1; w < NW; ++w) {
-        lo = min(lo, red[w]);
-        hi = max(hi, red[NW + w]);
-    }
-    // 1. the walk: every product's (column, a*b) into the row's slots, in expansion order
-    {
-        constexpr int U = 4;
-        int qb = 0;  // products of the earlier batches
-        for (int b0 = 0; b0 < k; b0 += HW_RUNS) {  // (workgroup-uniform)
-            __syncthreads();  // (the previous batch's table reads done)
-            {
-                const int j = b0 + tid;
-                int2 be = make_int2(0, 0);
-                double av = 0.0;
-                if (tid < HW_RUNS && j < k) {
-                    be = g.ebnd[a0 + j];
-                    av = g.vA[a0 + j];
-                }
-                const int len = be.y - be.x;
-                const int inc = wave_incl_scan_dpp(len);
-                if (lane == 63) tb.red[wv] = inc;
-                __syncthreads();
-                int woff = 0, tot = 0;
-#pragma unroll
-                for (int w = 0; w < NW; ++w) {
-                    const int v = tb.red[w];
-                    woff += w < wv ? v : 0;
-                    tot += v;
-                }
-                if (tid < HW_RUNS) {
-                    tb.pre[tid] = woff + inc - len;
-                    tb.bs[tid] = be.x;
-                    tb.av[tid] = av;
-                }
-                if (tid == 0) tb.tot = tot;
-                __syncthreads();
-            }
-            const int nb = min(HW_RUNS, k - b0), tot = tb.tot;
-            for (int q0 = 0; q0 < tot; q0 += U * HW_NT) {
-                int b[U], len2[U], q[U];
-                int c[U] = {0, 0, 0, 0};
-                double x[U] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    q[u] = q0 + u * HW_NT + tid;
-                    b[u] = 0;
-                    len2[u] = q[u] < tot ? nb : 0;
-                }
-                const bool ub[U] = {true, true, true, true};
-                search_ilp(tb.pre, b, len2, q, ub);  // b - 1 = the run holding product q
-#pragma unroll
-                for (int u = 0; u < U; ++u)
-                    if (q[u] < tot) {
-                        const int pp = tb.bs[b[u] - 1] + q[u] - tb.pre[b[u] - 1];
-                        c[u] = g.Bcol[pp];
-                        x[u] = tb.av[b[u] - 1] * g.Bval[pp];
-                    }
-#pragma unroll
-                for (int u = 0; u < U; ++u)
-                    if (q[u] < tot) {
-                        Acol[qb + q[u]] = c[u];
-                        Aval[qb + q[u]] = x[u];
-                    }
-            }
-            qb += tot;
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (each wave's stores complete before the barrier:
-    __syncthreads();                                   //  the slots are read back by other waves)
-    RP(0);
-    // 2. buckets of 2^bsh columns (bsh >= HW_WB, at most HW_MAXB of them)
-    const long long span = (long long)hi - lo + 1;
-    int bsh = HW_WB;
-    while (bsh < 31 && (span + (1ll << bsh) - 1) >> bsh > HW_MAXB) ++bsh;
-    const int nbk = P > 0 ? (int)((span + (1ll << bsh) - 1) >> bsh) : 0;
-    const int *Bkc = Acol;     // the bucketed products (in place: the slots themselves)
-    const double *Bkv = Aval;
-    if (nbk > 1 || P > HW_VCAP) {
-        for (int i = tid; i <= HW_MAXB; i += HW_NT) bcnt[i] = 0;
-        if (tid == 0) s_toff = (long long)atomicAdd(tnext, (unsigned long long)P);
-        __syncthreads();
-        for (int q = tid; q < P; q += HW_NT) atomicAdd(&bcnt[(Acol[q] - lo) >> bsh], 1);
-        __syncthreads();
-        if (wv == 0) {  // exclusive scan of the (<= 256) bucket counts, four per lane
-            int v[4], sum = 0;
+            for (int u = 0; u < 4; ++u) be[u] = j0 + u * W_NT < k ? g.ebnd[a0 + j0 + u * W_NT] : make_int2(0, 0);
+            int cl[4], ch[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                v[u] = 4 * lane + u < nbk ? bcnt[4 * lane + u] : 0;
-                sum += v[u];
+                cl[u] = be[u].y > be[u].x ? g.Bcol[be[u].x] : INT_MAX;
+                ch[u] = be[u].y > be[u].x ? g.Bcol[be[u].y - 1] : -1;
             }
-            const int inc = wave_incl_scan_dpp(sum);
-            int run = inc - sum;
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                if (4 * lane + u < nbk) {
-                    bcnt[4 * lane + u] = run;
-                    bcur[4 * lane + u] = run;
-                }
-                run += v[u];
+                l = min(l, cl[u]);
+                h = max(h, ch[u]);
             }
-            if (lane == 63) bcnt[nbk] = inc;
+        }
+        l = wave_last(wave_incl_dpp(l, INT_MAX, OpMin{}));
+        h = wave_last(wave_incl_dpp(h, INT_MIN, OpMax{}));
+        __syncthreads();
+        if (lane == 0) {
+            red[wv] = l;
+            red[NW + wv] = h;
         }
         __syncthreads();
-        const long long toff = s_toff;
-        for (int q = tid; q < P; q += HW_NT) {
-            const int c = Acol[q];
-            const int d = atomicAdd(&bcur[(c - lo) >> bsh], 1);
-            Tcol[toff + d] = c;
-            Tval[toff + d] = Aval[q];
+        l = red[0];
+        h = red[NW];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) {
+            l = min(l, red[w]);
+            h = max(h, red[NW + w]);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();  // (the bucket area read back by the other waves)
-        Bkc = Tcol + toff;
-        Bkv = Tval + toff;
-    } else if (tid == 0) {
-        bcnt[0] = 0;
-        bcnt[1] = P;
+        // (the one-walk bitmap kernel's rows: k_rows_bitmap's own test)
+        const bool onewalk = P <= kRowsHubProducts && k <= OW_RUNS && (long long)h - l < RH_SPAN;
+        if (!onewalk && P > 0) {
+            const long long span = (long long)h - l + 1;
+            const int lg = ceil_log2_ll(span);
+            wb = ceil_log2_ll((span * W_UNIT + P - 1) / P);
+            wb = max(wb, lg - 13);  // (at most W_MAXW windows)
+            wb = min(max(wb, W_WBMIN), W_WBMAX);
+            nw = (int)((span + (1ll << wb) - 1) >> wb);
+            lo = l;
+            pw = P;
+            // chunks: per run batch of RH_NT runs, W_CH products each
+            long long c = 0;
+            for (int b0 = tid * RH_NT; b0 < k; b0 += W_NT * RH_NT) {
+                const long long tot = g.E[a0 + min(k, b0 + RH_NT)] - g.E[a0 + b0];
+                c += (tot + W_CH - 1) / W_CH;
+            }
+            nch = (int)w_block_sum(c, red64);
+        }
+    }
+    if (tid == 0) {
+        wnw[i] = nw;
+        wnch[i] = nch;
+        wlo[i] = lo;
+        wwb[i] = wb;
+        wpre[i] = pw;
+        wmat[i] = (long long)nch * nw;
+        if (pw) atomicAdd(&wst[0], (unsigned long long)pw);
+        if (dr) {
+            atomicAdd(&wst[1], (unsigned long long)P);
+            atomicAdd(&wst[2], 1ull);
+        }
+    }
+}
+
+// a workgroup per class-H row i: its units' row (umap) and its chunks
+// (class-H index, batch, slice) from cbase[i], each chunk's row of the
+// per-window offset matrix at cmoff (wnw, wnch, wmat scanned: ubase, cbase, mbase)
+__global__ __launch_bounds__(WG) void k_rows_wchunks(RowsArgs g, const int *ubase, const int *cbase,
+                                                    const long long *mbase, int4 *chunks, long long *cmoff,
+                                                    int *umap) {
+    __shared__ int red[WAVES];
+    const int i = blockIdx.x;
+    const int u0 = ubase[i], nw = ubase[i + 1] - u0;
+    if (nw == 0) return;  // (workgroup-uniform)
+    for (int w = threadIdx.x; w < nw; w += WG) umap[u0 + w] = i;
+    const int4 le = g.list[i];
+    const int a0 = le.y, k = le.z, c0 = cbase[i];
+    const long long m0 = mbase[i];
+    int carry = 0;
+    for (int bb = 0; bb * RH_NT < k; bb += WG) {  // (workgroup-uniform) WG batches at a time
+        const int b = bb + threadIdx.x;
+        int ns = 0;
+        if (b * RH_NT < k) {
+            const long long tot = g.E[a0 + min(k, (b + 1) * RH_NT)] - g.E[a0 + b * RH_NT];
+            ns = (int)((tot + W_CH - 1) / W_CH);
+        }
+        int tot = 0;
+        const int off = carry + block_excl_scan(ns, &tot, red);
+        for (int j = 0; j < ns; ++j) {
+            const int c = c0 + off + j;
+            chunks[c] = make_int4(i, b, j, 0);
+            cmoff[c] = m0 + (long long)(off + j) * nw;
+        }
+        carry += tot;
+    }
+}
+
+// the chunk's products counted per window into LDS hist (zeroed by the caller
+// before; the batch's run table loaded into wt); returns the row's window shape
+__device__ __forceinline__ void w_chunk_hist(const RowsArgs &g, int4 ch, int lo, int wb, int *hist, WalkTab &wt) {
+    const int4 le = g.list[ch.x];
+    const int a0 = le.y, k = le.z, b0 = ch.y * RH_NT;
+    rows_batch(g, a0, k, b0, wt);  // (its barriers also order the caller's zeroing)
+    const int q0 = ch.z * W_CH, q1 = min(wt.tot, q0 + W_CH);
+    batch_walk<false>(g, min(RH_NT, k - b0), q0, q1, wt,
+                      [&](int c, double) { atomicAdd(&hist[(c - lo) >> wb], 1); });
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(W_NT) void k_rows_wcount(RowsArgs g, const int4 *chunks, const long long *cmoff,
+                                                     const int *wlo, const int *wwb, const int *ubase, int *ucnt,
+                                                     int *cbo) {
+    __shared__ int hist[W_MAXW];
+    __shared__ WalkTab wt;
+    const int4 ch = chunks[blockIdx.x];
+    const int u0 = ubase[ch.x], nw = ubase[ch.x + 1] - u0;
+    for (int w = threadIdx.x; w < nw; w += W_NT) hist[w] = 0;
+    w_chunk_hist(g, ch, wlo[ch.x], wwb[ch.x], hist, wt);
+    int *const cb = cbo + cmoff[blockIdx.x];  // the chunk's place in each window's bucket
+    for (int w = threadIdx.x; w < nw; w += W_NT)
+        if (hist[w]) cb[w] = atomicAdd(&ucnt[u0 + w], hist[w]);
+}
+
+// per W row (a workgroup per class-H row): out[u] = exclusive scan of in[u]
+// over the row's units; rnnz (optional) gets the row's total
+__global__ __launch_bounds__(W_NT) void k_rows_wscan(RowsArgs g, const int *ubase, const int *in, int *out,
+                                                    int *rnnz) {
+    constexpr int NW = W_NT / 64, PT = W_MAXW / W_NT;
+    __shared__ int red[NW];
+    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    const int u0 = ubase[blockIdx.x], nw = ubase[blockIdx.x + 1] - u0;
+    if (nw == 0) return;  // (workgroup-uniform)
+    int v[PT], sum = 0;
+#pragma unroll
+    for (int t = 0; t < PT; ++t) {
+        const int w = tid * PT + t;
+        v[t] = w < nw ? in[u0 + w] : 0;
+        sum += v[t];
+    }
+    const int inc = wave_incl_scan_dpp(sum);
+    if (lane == 63) red[wv] = inc;
+    __syncthreads();
+    int off = inc - sum, tot = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        off += w < wv ? red[w] : 0;
+        tot += red[w];
+    }
+#pragma unroll
+    for (int t = 0; t < PT; ++t) {
+        const int w = tid * PT + t;
+        if (w < nw) out[u0 + w] = off;
+        off += v[t];
+    }
+    if (rnnz && tid == 0) rnnz[g.list[blockIdx.x].x] = tot;
+}
+
+// the chunk's products to their windows' buckets in the row's staging slots
+// (bucket u at E[a0] + ubo[u]; the chunk's place in it from k_rows_wcount)
+__global__ __launch_bounds__(W_NT) void k_rows_wscatter(RowsArgs g, const int4 *chunks, const long long *cmoff,
+                                                       const int *wlo, const int *wwb, const int *ubase,
+                                                       const int *ubo, const int *cbo) {
+    __shared__ int cur[W_MAXW];  // row-relative slots (windows this chunk does not reach: unused)
+    __shared__ WalkTab wt;
+    const int4 ch = chunks[blockIdx.x];
+    const int u0 = ubase[ch.x], nw = ubase[ch.x + 1] - u0;
+    const int lo = wlo[ch.x], wb = wwb[ch.x];
+    const int *const cb = cbo + cmoff[blockIdx.x];
+    for (int w = threadIdx.x; w < nw; w += W_NT) cur[w] = ubo[u0 + w] + cb[w];
+    const int4 le = g.list[ch.x];
+    const int a0 = le.y, k = le.z, b0 = ch.y * RH_NT;
+    rows_batch(g, a0, k, b0, wt);  // (its barriers also order the cursors above)
+    const long long base = g.E[a0];
+    const int q0 = ch.z * W_CH, q1 = min(wt.tot, q0 + W_CH);
+    batch_walk<true>(g, min(RH_NT, k - b0), q0, q1, wt, [&](int c, double x) {
+        const long long o = base + atomicAdd(&cur[(c - lo) >> wb], 1);
+        g.Scol[o] = c;
+        g.Sval[o] = x;
+    });
+}
+
+// rank of column c inside a unit's window (bitmap bm, block and group prefixes)
+__device__ __forceinline__ int w_rank(const u64 *bm, const u16 *g4, const int *blk, int c) {
+    const int w = c >> 6, gi = w >> 2, sub = w & 3;
+    const ulonglong2 lo = reinterpret_cast<const ulonglong2 *>(bm)[gi * 2];
+    const ulonglong2 hi = reinterpret_cast<const ulonglong2 *>(bm)[gi * 2 + 1];
+    const u64 word = sub == 0 ? lo.x : sub == 1 ? lo.y : sub == 2 ? hi.x : hi.y;
+    int rk = blk[w / W_BLK] + g4[gi] + __popcll(word & ((1ull << (c & 63)) - 1ull));
+    rk += sub > 0 ? __popcll(lo.x) : 0;
+    rk += sub > 1 ? __popcll(lo.y) : 0;
+    rk += sub > 2 ? __popcll(hi.x) : 0;
+    return rk;
+}
+
+// a workgroup per unit u (row i = umap[u], window u - ubase[i]): its bucket
+// (ucnt[u] products at E[a0] + ubo[u]) -> its nonzeros, column-sorted, at
+// Ocol/Oval + wpre[i] + ubo[u]; ucount[u] = their number
+__global__ __launch_bounds__(W_NT) void k_rows_wunit(RowsArgs g, const int *umap, const int *ubase, const int *wlo,
+                                                    const int *wwb, const long long *wpre, const int *ucnt,
+                                                    const int *ubo, int *ucount, int *Ocol, double *Oval) {
+    constexpr int NW = W_NT / 64;
+    __shared__ __align__(16) u64 bm[W_WORDS];
+    __shared__ u16 g4[W_WORDS / 4];
+    __shared__ int blk[W_NBLK];
+    __shared__ __align__(16) double vals[W_VCAP];
+    __shared__ int red[NW];
+    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    const int u = blockIdx.x, i = umap[u];
+    const int n = ucnt[u];
+    if (n == 0) {  // (workgroup-uniform)
+        if (tid == 0) ucount[u] = 0;
+        return;
+    }
+    const int4 le = g.list[i];
+    const int wb = wwb[i];
+    const long long wlo0 = (long long)wlo[i] + ((long long)(u - ubase[i]) << wb);
+    const long long s0 = g.E[le.y] + ubo[u];
+    const int nwd = 1 << (wb - 6);
+    for (int w = tid; w < nwd; w += W_NT) bm[w] = 0ull;
+    // the first W_RPT * W_NT products in registers (the rest read again below)
+    int cc[W_RPT];
+    double xx[W_RPT];
+#pragma unroll
+    for (int t = 0; t < W_RPT; ++t) {
+        const int q = t * W_NT + tid;
+        cc[t] = q < n ? (int)(g.Scol[s0 + q] - wlo0) : -1;
+        xx[t] = q < n ? g.Sval[s0 + q] : 0.0;
     }
     __syncthreads();
-    RP(1);
-    // 3. the buckets in column order, each as windows of 2^HW_WB columns
-    long long out = 0;  // the row's nonzeros so far
-    for (int bk = 0; bk < nbk; ++bk) {  // (workgroup-uniform)
-        const int s0 = bcnt[bk], s1 = bcnt[bk + 1];
-        if (s1 == s0) continue;
-        const long long blo = (long long)lo + ((long long)bk << bsh);
-        const long long bhi = min((long long)hi, blo + (1ll << bsh) - 1);
-        for (long long wlo = blo; wlo <= bhi; wlo += 1ll << HW_WB) {  // (workgroup-uniform)
-            const int nwd = (int)((min(bhi, wlo + (1ll << HW_WB) - 1) - wlo + 64) >> 6);
-            for (int i = tid; i < nwd; i += HW_NT) bm[i] = 0ull;
-            __syncthreads();
-            for (int q = s0 + tid; q < s1; q += HW_NT) {
-                const long long c = (long long)Bkc[q] - wlo;
-                if (c >= 0 && c < (1ll << HW_WB)) atomicOr(&bm[c >> 6], 1ull << (c & 63));
-            }
-            __syncthreads();
-            // ranks: a wave per 512-word block (a lane: two 4-word groups), then the blocks
-            for (int bb = wv; bb < HW_NBLK; bb += NW) {
-                const int w0 = bb * HW_BLK + lane * 8;
-                int t0 = 0, t1 = 0;
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    t0 += w0 + u < nwd ? __popcll(bm[w0 + u]) : 0;
-                    t1 += w0 + 4 + u < nwd ? __popcll(bm[w0 + 4 + u]) : 0;
-                }
-                const int inc = wave_incl_scan_dpp(t0 + t1);
-                g4[w0 / 4] = (u16)(inc - t0 - t1);
-                g4[w0 / 4 + 1] = (u16)(inc - t1);
-                if (lane == 63) blk[bb] = inc;
-            }
-            __syncthreads();
-            if (wv == 0) {
-                const int v = lane < HW_NBLK ? blk[lane] : 0;
-                const int inc = wave_incl_scan_dpp(v);
-                if (lane < HW_NBLK) blk[lane] = inc - v;
-                if (lane == 63) red[0] = inc;
-            }
-            __syncthreads();
-            const int wn = red[0];  // the window's nonzeros
-            int *const Ocol = g.Scol + base + out;
-            double *const Oval = g.Sval + base + out;
-            for (int r0 = 0; r0 < wn; r0 += HW_VCAP) {  // (workgroup-uniform; one chunk unless wn > HW_VCAP)
-                const int r1 = min(wn, r0 + HW_VCAP);
-                for (int i = tid; i < r1 - r0; i += HW_NT) vals[i] = 0.0;
-                __syncthreads();
-                for (int q = s0 + tid; q < s1; q += HW_NT) {
-                    const long long c = (long long)Bkc[q] - wlo;
-                    if (c >= 0 && c < (1ll << HW_WB)) {
-                        const int rk = hw_rank(bm, g4, blk, (int)c) - r0;
-                        if ((unsigned)rk < (unsigned)HW_VCAP) atomicAdd(&vals[rk], Bkv[q]);
-                    }
-                }
-                __syncthreads();
-                // emit: a thread per bitmap word, its columns at their ranks
-                for (int w = tid; w < nwd; w += HW_NT) {
-                    u64 word = bm[w];
-                    int rk = blk[w / HW_BLK] + g4[w >> 2];
-                    for (int t = w & ~3; t < w; ++t) rk += __popcll(bm[t]);
-                    while (word && rk < r1) {
-                        const int bit = __builtin_ctzll(word);
-                        word &= word - 1ull;
-                        if (rk >= r0) {
-                            Ocol[rk] = (int)(wlo + w * 64 + bit);
-                            Oval[rk] = vals[rk - r0];
-                        }
-                        ++rk;
-                    }
-                }
-                __syncthreads();  // (the chunk's values read before the next chunk's zeroing)
-            }
-            out += wn;
-            __syncthreads();  // (the window's LDS reads done before the next window's zeroing)
-        }
+    for (int t = 0; t < W_RPT; ++t)
+        if (cc[t] >= 0) atomicOr(&bm[cc[t] >> 6], 1ull << (cc[t] & 63));
+    for (int q = W_RPT * W_NT + tid; q < n; q += W_NT) {
+        const int c = (int)(g.Scol[s0 + q] - wlo0);
+        atomicOr(&bm[c >> 6], 1ull << (c & 63));
     }
-    RP(2);
-    if (tid == 0) g.rnnz[r] = (int)out;
-    RP_DONE(0);
+    __syncthreads();
+    // ranks: a wave per W_BLK-word block (a lane: two 4-word groups), then the blocks
+    for (int bb = wv; bb * W_BLK < nwd; bb += NW) {
+        const int w0 = bb * W_BLK + lane * 8;
+        int t0 = 0, t1 = 0;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            t0 += w0 + v < nwd ? __popcll(bm[w0 + v]) : 0;
+            t1 += w0 + 4 + v < nwd ? __popcll(bm[w0 + 4 + v]) : 0;
+        }
+        const int inc = wave_incl_scan_dpp(t0 + t1);
+        if (w0 < nwd) g4[w0 / 4] = (u16)(inc - t0 - t1);
+        if (w0 + 4 < nwd) g4[w0 / 4 + 1] = (u16)(inc - t1);
+        if (lane == 63) blk[bb] = inc;
+    }
+    __syncthreads();
+    const int nb = (nwd + W_BLK - 1) / W_BLK;
+    if (wv == 0) {
+        const int v = lane < nb ? blk[lane] : 0;
+        const int inc = wave_incl_scan_dpp(v);
+        if (lane < nb) blk[lane] = inc - v;
+        if (lane == 63) red[0] = inc;
+    }
+    __syncthreads();
+    const int wn = red[0];
+    int rk[W_RPT];
+#pragma unroll
+    for (int t = 0; t < W_RPT; ++t) rk[t] = cc[t] >= 0 ? w_rank(bm, g4, blk, cc[t]) : 0;
+    const long long o0 = wpre[i] + ubo[u];
+    for (int r0 = 0; r0 < wn; r0 += W_VCAP) {  // (workgroup-uniform; one pass unless wn > W_VCAP)
+        const int r1 = min(wn, r0 + W_VCAP);
+        for (int j = tid; j < r1 - r0; j += W_NT) vals[j] = 0.0;
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < W_RPT; ++t)
+            if (cc[t] >= 0 && (unsigned)(rk[t] - r0) < (unsigned)W_VCAP) atomicAdd(&vals[rk[t] - r0], xx[t]);
+        for (int q = W_RPT * W_NT + tid; q < n; q += W_NT) {
+            const int c = (int)(g.Scol[s0 + q] - wlo0);
+            const int rq = w_rank(bm, g4, blk, c) - r0;
+            if ((unsigned)rq < (unsigned)W_VCAP) atomicAdd(&vals[rq], g.Sval[s0 + q]);
+        }
+        __syncthreads();
+        // emit: a thread per bitmap word, its columns at their ranks
+        for (int w = tid; w < nwd; w += W_NT) {
+            u64 word = bm[w];
+            if (!word) continue;
+            int r = w_rank(bm, g4, blk, w * 64);
+            if (r >= r1) continue;
+            while (word) {
+                const int bit = __builtin_ctzll(word);
+                word &= word - 1ull;
+                if (r >= r0 && r < r1) {
+                    Ocol[o0 + r] = (int)(wlo0 + w * 64 + bit);
+                    Oval[o0 + r] = vals[r - r0];
+                }
+                ++r;
+            }
+        }
+        __syncthreads();  // (the pass's values read before the next pass zeroes them)
+    }
+    if (tid == 0) ucount[u] = wn;
+}
+
+// each unit's nonzeros from the output area to the row's staging slots at the
+// unit's output offset (uoff, from k_rows_wscan of ucount)
+__global__ __launch_bounds__(WG) void k_rows_wgather(RowsArgs g, const int *umap, const long long *wpre,
+                                                    const int *ubo, const int *uoff, const int *ucount,
+                                                    const int *Ocol, const double *Oval) {
+    const int u = blockIdx.x, i = umap[u];
+    const long long src = wpre[i] + ubo[u], dst = g.E[g.list[i].y] + uoff[u];
+    const int n = ucount[u];
+    for (int j = threadIdx.x; j < n; j += WG) {
+        g.Scol[dst + j] = Ocol[src + j];
+        g.Sval[dst + j] = Oval[src + j];
+    }
 }
 
 // ---- hub rows dominated by one run (mawi: a hub neighbour's C row is the
@@ -1517,7 +1565,7 @@ __global__ __launch_bounds__(DR_NT) void k_rows_dr_prep(RowsArgs g, DrRow *rows,
     int jl;
     const long long L = row_longest_run(g.E, a0, k, &jl, red);
     const int nS = (int)(P - L);
-    if (nS > DR_SMAX) return;  // (k_rows_hwin's row)
+    if (nS > DR_SMAX) return;  // (a windowed row)
     __shared__ int s_h;
     if (tid == 0) s_h = atomicAdd(ndr, 1);  // this row's slot among the DR rows
     const long long eL = g.E[a0 + jl] - base;  // L's first product in the row's product order
@@ -1947,16 +1995,16 @@ void dev_rows_setup_read(Context &cx, RowsPlan &p) {
     p.hprod = cx.pinned64[4];
     p.pmax = cx.pinned64[5];
     p.products = cx.pinned64[6];
-    p.drprod = cx.pinned64[7];
-    p.hubrest = cx.pinned64[8];
+    p.hubprod = cx.pinned64[7];
+    p.hk = cx.pinned64[8];
     p.hbig = cx.pinned64[12];
 }
 
-// routing: the path is built for rows of modest length (class H's bitmap rows a
-// minority of the work) and for hub rows that one run dominates (the DR
-// kernels); hub rows without a dominant run (R-MAT) take the staged pipeline
+// routing: every product whose B rows are column-sorted (class H's rows take
+// the one-walk bitmap, dominant-run or windowed kernels)
 bool dev_rows_accept(const RowsPlan &p) {
-    return (p.hprod - p.drprod) * 4 <= p.products && p.hubrest == 0;
+    (void)p;
+    return true;
 }
 
 void dev_rows_release(Context &cx, RowsPlan &p) {
@@ -2028,38 +2076,106 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
         k_rows_order_h<<<1, OH_NT, 0, s>>>(E, p.cls, lists + (long)(NCLS - 1) * m);
         TSG_HIP(hipGetLastError());
     }
-    int *Tcol = nullptr, *Oc = nullptr, *Or = nullptr;
-    double *Tval = nullptr, *Ox = nullptr;
+    int *Oc = nullptr, *Or = nullptr;
+    double *Ox = nullptr;
     DrRow *drows = nullptr;
     DrEnt *dents = nullptr;
     int2 *dchunks = nullptr;
+    // windowed (W) rows' arrays: per class-H row, per unit, per chunk
+    int *wnw = nullptr, *wnch = nullptr, *wlo = nullptr, *wwb = nullptr, *umap = nullptr;
+    int *ucnt = nullptr, *ubo = nullptr, *ucount = nullptr, *uoff = nullptr, *Wc = nullptr;
+    long long *wpre = nullptr, *wmat = nullptr, *cmoff = nullptr;
+    int *cbo = nullptr;
+    unsigned long long *wst = nullptr;
+    int4 *wchunks = nullptr;
+    double *Wv = nullptr;
     if (ncls[7] > 0) {
-        // class H: each kernel takes its rows of the class (hub rows the windowed
-        // one) and its other workgroups return at once
+        // class H: each kernel takes its rows of the class and its other
+        // workgroups return at once
+        const int n7 = ncls[7];
         g.list = lists + (long)7 * m;
-        g.nrows = ncls[7];
-        if (p.hubrest > 0) {  // hub rows without a dominant run: their bucket area
-            TSG_TRY(cx.get(&Tcol, (size_t)p.hubrest + 1));
-            TSG_TRY(cx.get(&Tval, (size_t)p.hubrest + 1));
-            k_rows_hwin<<<ncls[7], HW_NT, 0, s>>>(g, Tcol, Tval, reinterpret_cast<unsigned long long *>(p.cls + 18));
+        g.nrows = n7;
+        long long wprod = 0, drprod = 0, ndr = 0, nmat = 0;
+        int nu = 0, nc = 0;
+        // rows past the one-walk kernel (hub rows, more than OW_RUNS runs, or a
+        // span that may pass RH_SPAN): the plan sorts them into dominant-run and
+        // windowed rows (one more host round trip: sizes of the unit and chunk lists)
+        if (p.hubprod > 0 || p.hk > 0 || (long long)B.n > RH_SPAN) {
+            TSG_TRY(cx.get(&wnw, (size_t)n7 + 1));
+            TSG_TRY(cx.get(&wnch, (size_t)n7 + 1));
+            TSG_TRY(cx.get(&wlo, (size_t)n7));
+            TSG_TRY(cx.get(&wwb, (size_t)n7));
+            TSG_TRY(cx.get(&wpre, (size_t)n7 + 1));
+            TSG_TRY(cx.get(&wmat, (size_t)n7 + 1));
+            TSG_TRY(cx.get(&wst, 4));
+            TSG_HIP(hipMemsetAsync(wst, 0, 4 * sizeof(unsigned long long), s));
+            k_rows_wplan<<<n7, W_NT, 0, s>>>(g, wnw, wnch, wlo, wwb, wpre, wmat, wst);
+            TSG_HIP(hipGetLastError());
+            TSG_HIP(hipMemsetAsync(wnw + n7, 0, sizeof(int), s));
+            TSG_HIP(hipMemsetAsync(wnch + n7, 0, sizeof(int), s));
+            TSG_HIP(hipMemsetAsync(wpre + n7, 0, sizeof(long long), s));
+            TSG_HIP(hipMemsetAsync(wmat + n7, 0, sizeof(long long), s));
+            TSG_TRY(scan_exclusive_i32(cx, wnw, (long)n7 + 1, s));   // -> ubase
+            TSG_TRY(scan_exclusive_i32(cx, wnch, (long)n7 + 1, s));  // -> cbase
+            TSG_TRY(scan_exclusive_i64(cx, wpre, (long)n7 + 1, s));  // -> output-area offsets
+            TSG_TRY(scan_exclusive_i64(cx, wmat, (long)n7 + 1, s));  // -> chunk x window offset matrix
+            TSG_HIP(hipMemcpyAsync(cx.pinned64 + 16, wst, 3 * sizeof(long long), hipMemcpyDeviceToHost, s));
+            TSG_HIP(hipMemcpyAsync(reinterpret_cast<int *>(cx.pinned64 + 20), wnw + n7, sizeof(int),
+                                   hipMemcpyDeviceToHost, s));
+            TSG_HIP(hipMemcpyAsync(reinterpret_cast<int *>(cx.pinned64 + 21), wnch + n7, sizeof(int),
+                                   hipMemcpyDeviceToHost, s));
+            TSG_HIP(hipMemcpyAsync(cx.pinned64 + 22, wmat + n7, sizeof(long long), hipMemcpyDeviceToHost, s));
+            TSG_TRY(stream_wait(s));
+            wprod = cx.pinned64[16];
+            nmat = cx.pinned64[22];
+            drprod = cx.pinned64[17];
+            ndr = cx.pinned64[18];
+            nu = *reinterpret_cast<const int *>(cx.pinned64 + 20);
+            nc = *reinterpret_cast<const int *>(cx.pinned64 + 21);
+        }
+        if (nu > 0) {  // the windowed rows
+            const int *ubase = wnw, *cbase = wnch;
+            TSG_TRY(cx.get(&wchunks, (size_t)nc));
+            TSG_TRY(cx.get(&cmoff, (size_t)nc));
+            TSG_TRY(cx.get(&cbo, (size_t)nmat + 1));
+            TSG_TRY(cx.get(&umap, (size_t)nu));
+            TSG_TRY(cx.get(&ucnt, (size_t)nu));
+            TSG_TRY(cx.get(&ubo, (size_t)nu));
+            TSG_TRY(cx.get(&ucount, (size_t)nu));
+            TSG_TRY(cx.get(&uoff, (size_t)nu));
+            TSG_TRY(cx.get(&Wc, (size_t)wprod + 1));
+            TSG_TRY(cx.get(&Wv, (size_t)wprod + 1));
+            TSG_HIP(hipMemsetAsync(ucnt, 0, (size_t)nu * sizeof(int), s));
+            k_rows_wchunks<<<n7, WG, 0, s>>>(g, ubase, cbase, wmat, wchunks, cmoff, umap);
+            TSG_HIP(hipGetLastError());
+            k_rows_wcount<<<nc, W_NT, 0, s>>>(g, wchunks, cmoff, wlo, wwb, ubase, ucnt, cbo);
+            TSG_HIP(hipGetLastError());
+            k_rows_wscan<<<n7, W_NT, 0, s>>>(g, ubase, ucnt, ubo, nullptr);
+            TSG_HIP(hipGetLastError());
+            k_rows_wscatter<<<nc, W_NT, 0, s>>>(g, wchunks, cmoff, wlo, wwb, ubase, ubo, cbo);
+            TSG_HIP(hipGetLastError());
+            k_rows_wunit<<<nu, W_NT, 0, s>>>(g, umap, ubase, wlo, wwb, wpre, ucnt, ubo, ucount, Wc, Wv);
+            TSG_HIP(hipGetLastError());
+            k_rows_wscan<<<n7, W_NT, 0, s>>>(g, ubase, ucount, uoff, g.rnnz);
+            TSG_HIP(hipGetLastError());
+            k_rows_wgather<<<nu, WG, 0, s>>>(g, umap, wpre, ubo, uoff, ucount, Wc, Wv);
             TSG_HIP(hipGetLastError());
         }
-        if (p.hprod > p.drprod + p.hubrest) {  // rows of the one-window bitmap kernel
+        if (p.hprod > wprod + drprod) {  // rows of the one-walk bitmap kernel
             if (p.hbig > 0) {  // one-walk rows past OW_CH products: their scratch
                 TSG_TRY(cx.get(&Oc, (size_t)p.hbig));
                 TSG_TRY(cx.get(&Ox, (size_t)p.hbig));
                 TSG_TRY(cx.get(&Or, (size_t)p.hbig));
             }
-            k_rows_bitmap<<<ncls[7], RH_NT, 0, s>>>(g, Oc, Ox, Or,
-                                                   reinterpret_cast<unsigned long long *>(p.cls + 26));
+            k_rows_bitmap<<<n7, RH_NT, 0, s>>>(g, Oc, Ox, Or, reinterpret_cast<unsigned long long *>(p.cls + 26));
             TSG_HIP(hipGetLastError());
         }
-        if (p.drprod > 0) {  // hub rows with a dominant run
-            const long long ndr = p.drprod / kRowsHubProducts + 1, nch = p.drprod / DR_CH + ndr;
+        if (drprod > 0) {  // hub rows with a dominant run
+            const long long nch = drprod / DR_CH + ndr;
             TSG_TRY(cx.get(&drows, (size_t)ndr));
             TSG_TRY(cx.get(&dents, (size_t)ndr * DR_SMAX));
             TSG_TRY(cx.get(&dchunks, (size_t)nch));
-            k_rows_dr_prep<<<ncls[7], DR_NT, 0, s>>>(g, drows, dents, dchunks, p.cls + 20, p.cls + 21);
+            k_rows_dr_prep<<<n7, DR_NT, 0, s>>>(g, drows, dents, dchunks, p.cls + 20, p.cls + 21);
             TSG_HIP(hipGetLastError());
             k_rows_dr_fill<<<(unsigned)nch, DR_NT, 0, s>>>(g, drows, dents, dchunks, p.cls + 20);
             TSG_HIP(hipGetLastError());
@@ -2167,8 +2283,10 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
     dev_rows_release(cx, p);
     cx.put(Scol);
     cx.put(Sval);
-    cx.put(Tcol);
-    cx.put(Tval);
+    {
+        void *ws[] = {wnw, wnch, wlo, wwb, wpre, wmat, wst, wchunks, cmoff, cbo, umap, ucnt, ubo, ucount, uoff, Wc, Wv};
+        for (void *q : ws) cx.put(q);
+    }
     cx.put(Oc);
     cx.put(Ox);
     cx.put(Or);

@@ -8,9 +8,10 @@ H (longer rows or more entries: an LDS column bitmap per window of 1,048,576
 columns; rows of one window and <= 2,048 entries walk their products once --
 registers, then scratch past 16,384 -- and take columns and values through the
 bitmap's LDS by rank; other rows walk twice with f64 atomics for the values;
-hub rows past 65,536 products: the windowed kernel -- products bucketed by
-column, LDS bitmaps of 262,144 columns, values added in LDS -- or the
-dominant-run kernels).  TSG_PATH=rows forces the path.  Pattern
+hub rows past 65,536 products and rows past the one-walk kernel's runs or
+span: the windowed kernels -- (row, column window) units, products bucketed
+per unit, an LDS bitmap per unit, values added in LDS -- or, for hub rows that
+one run dominates, the dominant-run kernels).  TSG_PATH=rows forces the path.  Pattern
 bit-exact, values within 1e-10 relative, against the oracle (the reference's
 semantics: steps 1-3 + tile2csr, tilespgemm-cuda.h:279-2218)."""
 import numpy as np
@@ -182,10 +183,10 @@ def test_rows_aat_lj_prefix():
     _check((r, n, rp[:r + 1].copy(), ci[:e].copy(), vv[:e].copy()), aat=True)
 
 
-def test_default_routing_declines_hub_dominated(monkeypatch):
+def test_default_routing_hub_rows_windowed(monkeypatch):
     """A product with a hub row (past kRowsHubProducts = 65,536 products) that no
-    single run dominates is declined by the row-merge setup and runs on the
-    staged tile pipeline."""
+    single run dominates stays on the row-merge path: the windowed kernels
+    (k_rows_w*) take the hub row."""
     monkeypatch.delenv("TSG_PATH", raising=False)
     n, nb = 300, 100_000
     rng = np.random.default_rng(21)
@@ -203,7 +204,7 @@ def test_default_routing_declines_hub_dominated(monkeypatch):
     np.testing.assert_array_equal(got[2], ref[2])
     np.testing.assert_array_equal(got[3], ref[3])
     np.testing.assert_allclose(got[4], ref[4], rtol=1e-10, atol=0)
-    assert st["path"] == T.PATH_TILES
+    assert st["path"] == T.PATH_ROWS
 
 
 def test_default_routing_short_rows_row_merge(monkeypatch):
@@ -260,8 +261,8 @@ def test_rows_unpacked_wide_span(cls_products):
 
 def test_rows_hub_rows_windowed_and_dominant_run():
     """Hub rows (past 65,536 products): without a dominant run the windowed
-    class-H kernel (products bucketed by column, per-window LDS bitmaps, LDS
-    values) -- many runs over 1,500,000 columns with heavy collisions (several
+    kernels ((row, window) units, products bucketed per unit, per-unit LDS
+    bitmaps, LDS values) -- many runs over 1,500,000 columns with heavy collisions (several
     buckets, windows with more nonzeros than one LDS value chunk), two long
     colliding runs; with one (all but <= 4,096 products in one run) the DR
     kernels -- one long run with a few short ones (the mawi pattern) and a row
