@@ -411,3 +411,13 @@ def test_rows_direct_output_mode(monkeypatch):
     test_rows_edge_cases()
     test_rows_duplicate_runs_sum()
     _check(synth.GENERATORS["mc2depi"](), aat=True)
+
+
+@pytest.mark.parametrize("opt", ["TSG_W_SCATTER=1", "TSG_W_RUNMAP=0"])
+def test_rows_windowed_kernel_options(monkeypatch, opt):
+    """The windowed kernels' non-default options (the LDS-binned scatter; run
+    table binary searches instead of the run map) on the hub-row cases."""
+    k, v = opt.split("=")
+    monkeypatch.setenv(k, v)
+    test_rows_hub_rows_windowed_and_dominant_run()
+    test_default_routing_hub_rows_windowed(monkeypatch)
