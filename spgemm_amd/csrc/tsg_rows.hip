@@ -1235,8 +1235,9 @@ __device__ __forceinline__ long long w_block_sum(long long x, long long *red) {
 // a workgroup per class-H row i.  Outputs (zero unless a W row): wnw[i] units,
 // wnch[i] chunks, wlo[i] first column, wwb[i] window bits, wpre[i] products;
 // wst[0] += W rows' products, wst[1] / wst[2] += DR rows' products / rows.
-__global__ __launch_bounds__(W_NT) void k_rows_wplan(RowsArgs g, int bn, int *wnw, int *wnch, int *wlo, int *wwb,
-                                                    long long *wpre, long long *wmat, unsigned long long *wst) {
+__global__ __launch_bounds__(W_NT) void k_rows_wplan(RowsArgs g, int bn, long long unit, int *wnw, int *wnch,
+                                                    int *wlo, int *wwb, long long *wpre, long long *wmat,
+                                                    unsigned long long *wst, long long *soff) {
     constexpr int NW = W_NT / 64;
     __shared__ int red[2 * NW];
     __shared__ long long red64[NW];
@@ -1293,7 +1294,7 @@ __global__ __launch_bounds__(W_NT) void k_rows_wplan(RowsArgs g, int bn, int *wn
         if (!onewalk && P > 0) {
             const long long span = (long long)h - l + 1;
             const int lg = ceil_log2_ll(span);
-            wb = ceil_log2_ll((span * W_UNIT + P - 1) / P);
+            wb = ceil_log2_ll((span * unit + P - 1) / P);
             wb = max(wb, lg - 13);                // (at most W_MAXW windows)
             wb = max(wb, min(lg - 10, W_WBMAX));  // (at most W_SBW where the widest window allows)
             wb = min(max(wb, W_WBMIN), W_WBMAX);
@@ -1316,6 +1317,7 @@ __global__ __launch_bounds__(W_NT) void k_rows_wplan(RowsArgs g, int bn, int *wn
         wwb[i] = wb;
         wpre[i] = pw;
         wmat[i] = (long long)nch * nw;
+        if (nw) soff[le.x] = -1;  // (the compaction skips the row: k_rows_wgather writes it)
         if (pw) atomicAdd(&wst[0], (unsigned long long)pw);
         if (dr) {
             atomicAdd(&wst[1], (unsigned long long)P);
@@ -1654,17 +1656,18 @@ __global__ __launch_bounds__(W_NT) void k_rows_wunit(RowsArgs g, const int *umap
     if (tid == 0) ucount[u] = wn;
 }
 
-// each unit's nonzeros from the output area to the row's staging slots at the
-// unit's output offset (uoff, from k_rows_wscan of ucount)
+// each unit's nonzeros from the output area to C at the row's pointer plus the
+// unit's output offset (uoff, from k_rows_wscan of ucount); after the row scan
 __global__ __launch_bounds__(WG) void k_rows_wgather(RowsArgs g, const int *umap, const long long *wpre,
                                                     const int *ubo, const int *uoff, const int *ucount,
-                                                    const int *Ocol, const double *Oval) {
+                                                    const int *Ocol, const double *Oval, const int *Crp, int *Ccol,
+                                                    double *Cval) {
     const int u = blockIdx.x, i = umap[u];
-    const long long src = wpre[i] + ubo[u], dst = g.E[g.list[i].y] + uoff[u];
+    const long long src = wpre[i] + ubo[u], dst = (long long)Crp[g.list[i].x] + uoff[u];
     const int n = ucount[u];
     for (int j = threadIdx.x; j < n; j += WG) {
-        g.Scol[dst + j] = Ocol[src + j];
-        g.Sval[dst + j] = Oval[src + j];
+        Ccol[dst + j] = Ocol[src + j];
+        Cval[dst + j] = Oval[src + j];
     }
 }
 
@@ -2039,6 +2042,7 @@ __global__ __launch_bounds__(WG) void k_rows_hcopy(const int4 *list, int n, cons
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
         const int r = list[i].x;
         const long long s = soff[r];
+        if (s < 0) continue;  // (a windowed row: k_rows_wgather writes it)
         const int d = Crp[r], cnt = Crp[r + 1] - d;
         for (int j = threadIdx.x; j < cnt; j += WG) {
             __builtin_nontemporal_store(__builtin_nontemporal_load(Scol + s + j), Ccol + d + j);
@@ -2101,7 +2105,9 @@ __global__ __launch_bounds__(WG) void k_rows_compact(int m, const int *cfirst, c
     __syncthreads();
     for (int i = tid; i < n; i += WG) {
         const int r = rowof[i];
-        const long long src = soff[r] + (c0 + i - Crp[r]);
+        const long long so = soff[r];
+        if (so < 0) continue;  // (a windowed row: k_rows_wgather writes it)
+        const long long src = so + (c0 + i - Crp[r]);
         // (streamed: staging read once, C not re-read by this call)
         __builtin_nontemporal_store(__builtin_nontemporal_load(Scol + src), Ccol + c0 + i);
         __builtin_nontemporal_store(__builtin_nontemporal_load(Sval + src), Cval + c0 + i);
@@ -2234,6 +2240,8 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
     unsigned long long *wst = nullptr;
     int4 *wchunks = nullptr;
     double *Wv = nullptr;
+    int nu = 0;
+    RowsArgs g7 = g;  // (class H's list, for the windowed rows' gather after the row scan)
     if (ncls[7] > 0) {
         // class H: each kernel takes its rows of the class and its other
         // workgroups return at once
@@ -2241,7 +2249,8 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
         g.list = lists + (long)7 * m;
         g.nrows = n7;
         long long wprod = 0, drprod = 0, ndr = 0, nmat = 0;
-        int nu = 0, nc = 0;
+        int nc = 0;
+        g7 = g;
         // rows past the one-walk kernel (hub rows, more than OW_RUNS runs, or a
         // span that may pass RH_SPAN): the plan sorts them into dominant-run and
         // windowed rows (one more host round trip: sizes of the unit and chunk lists)
@@ -2254,7 +2263,10 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
             TSG_TRY(cx.get(&wmat, (size_t)n7 + 1));
             TSG_TRY(cx.get(&wst, 4));
             TSG_HIP(hipMemsetAsync(wst, 0, 4 * sizeof(unsigned long long), s));
-            k_rows_wplan<<<n7, W_NT, 0, s>>>(g, B.n, wnw, wnch, wlo, wwb, wpre, wmat, wst);
+            // products per unit, the target of each row's window width (TSG_W_UNIT)
+            const long long wunit = getenv("TSG_W_UNIT") ? atoll(getenv("TSG_W_UNIT")) : W_UNIT;
+            k_rows_wplan<<<n7, W_NT, 0, s>>>(g, B.n, wunit > 0 ? wunit : W_UNIT, wnw, wnch, wlo, wwb, wpre, wmat,
+                                             wst, soff);
             TSG_HIP(hipGetLastError());
             TSG_HIP(hipMemsetAsync(wnw + n7, 0, sizeof(int), s));
             TSG_HIP(hipMemsetAsync(wnch + n7, 0, sizeof(int), s));
@@ -2308,8 +2320,6 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
             k_rows_wunit<<<nu, W_NT, 0, s>>>(g, umap, ubase, wlo, wwb, wpre, ucnt, ubo, ucount, Wc, Wv);
             TSG_HIP(hipGetLastError());
             k_rows_wscan<<<n7, W_NT, 0, s>>>(g, ubase, ucount, uoff, g.rnnz);
-            TSG_HIP(hipGetLastError());
-            k_rows_wgather<<<nu, WG, 0, s>>>(g, umap, wpre, ubo, uoff, ucount, Wc, Wv);
             TSG_HIP(hipGetLastError());
         }
         if (p.hprod > wprod + drprod) {  // rows of the one-walk bitmap kernel
@@ -2373,6 +2383,14 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
         }
         return TSG_OK;
     };
+    // the windowed rows' nonzeros straight into C (the compaction skips those rows)
+    auto wgather = [&]() -> int {
+        if (nu == 0) return TSG_OK;
+        k_rows_wgather<<<nu, WG, 0, s>>>(g7, umap, wpre, ubo, uoff, ucount, Wc, Wv, C.rowpointer, C.columnindex,
+                                         C.value);
+        TSG_HIP(hipGetLastError());
+        return TSG_OK;
+    };
     int *cfirst = nullptr;
     if (direct) {
         // the classes' exact counts (class H's came with its rows, in the staging)
@@ -2384,6 +2402,7 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
         TSG_TRY(launch(1, k_rows_count_small<64>, (ncls[1] + WAVES - 1) / WAVES, WG, s));
         TSG_TRY(launch(0, k_rows_count_small<16>, (ncls[0] + 4 * WAVES - 1) / (4 * WAVES), WG, s));
         TSG_TRY(scan_alloc());
+        TSG_TRY(wgather());
         g.Crp = C.rowpointer;
         g.Scol = C.columnindex;
         g.Sval = C.value;
@@ -2424,6 +2443,7 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
             k_rows_compact<<<nch, WG, 0, s>>>(m, cfirst, soff, C.rowpointer, Scol, Sval, C.columnindex, C.value);
         }
         TSG_HIP(hipGetLastError());
+        TSG_TRY(wgather());
     }
     if (small) TSG_HIP(hipMemcpyAsync(cx.pinned64 + 15, C.rowpointer + m, sizeof(int), hipMemcpyDeviceToHost, s));
     if (ev) TSG_HIP(hipEventRecord(ev[3], s));

@@ -17,11 +17,10 @@ dA = DeviceCSR.from_host(mb, n, rpb, cib, vvb)
 dB = DeviceCSR.from_host(m, n, rp, ci, vv)
 ctx = Context(0)
 os.environ["TSG_PATH"] = "rows"
-cfgs = [("binned+runmap", "1", "1"), ("direct+runmap", "0", "1"), ("binned+search", "1", "0"),
-        ("direct+search", "0", "0")]
+cfgs = [("unit 8192", "8192"), ("unit 16384", "16384"), ("unit 4096", "4096"), ("unit 32768", "32768")]
 for rnd in range(2):
-    for name, sc, rm in cfgs:
-        os.environ["TSG_W_SCATTER"], os.environ["TSG_W_RUNMAP"] = sc, rm
+    for name, un in cfgs:
+        os.environ["TSG_W_UNIT"] = un
         ts = []
         for i in range(reps):
             ctx.reset()
