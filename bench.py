@@ -397,6 +397,12 @@ def main():
                 sts.append(st)
                 nnz += c.nnz
         st = {k: sum(s[k] for s in sts) for k in sts[0]}
+        # (labels, not sums: the path every block took, -1 for "no C tiles")
+        paths = {int(s["path"]) for s in sts}
+        st["path"] = paths.pop() if len(paths) == 1 else -1
+        for k in ("numtileA", "numblkC"):
+            if k in st and all(s[k] == -1 for s in sts):
+                st[k] = -1
         return c, st, nnz
 
     for _ in range(args.warmup):
@@ -462,7 +468,7 @@ def main():
     k3_ms = med["t_step3_kernel_ms"]
     achieved = b_alg / (k3_ms * 1e-3) / 1e9
     path_id = int(med["path"])
-    path_name = {0: "tiles", 1: "fused", 2: "band", 3: "rows"}.get(path_id, str(path_id))
+    path_name = {-1: "mixed", 0: "tiles", 1: "fused", 2: "band", 3: "rows"}.get(path_id, str(path_id))
     workload = f"{name} C=A{'*A^T' if aat else '^2'} fp64 (device CSR in -> device CSR out), path {path_name}"
     if path_id == 3:
         kernel_desc = ("row-merge numeric phase (class H: k_rows_bitmap / hub rows k_rows_w*, k_rows_dr_*; "
