@@ -855,7 +855,9 @@ __device__ __forceinline__ void batch_runmap(const WalkTab &tb, int nb, int qb, 
 }
 
 // products [q0, q1) of a batch whose run table tb holds (rows_batch; nb runs),
-// U per thread at a time: each product's column (and with VAL its a*b) to f.
+// U per thread at a time: each product's column (and with VAL its a*b) to
+// f(column, value, valid), called by every lane (consecutive lanes hold
+// consecutive products; the invalid ones are a suffix of the wave).
 // With rmap (4 * RH_NT u16 + red: every thread must call), each step's runs come
 // from batch_runmap; else a binary search of the run table per product.
 template <bool VAL, class F>
@@ -890,8 +892,7 @@ __device__ __forceinline__ void batch_walk(const RowsArgs &g, int nb, int q0, in
                 if (VAL) x[u] = tb.av[b[u] - 1] * g.Bval[pp];
             }
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (q[u] < q1) f(c[u], x[u]);
+        for (int u = 0; u < U; ++u) f(c[u], x[u], q[u] < q1);  // (every lane: f may use wave operations)
         if (rmap) __syncthreads();  // (the map read before the next step rebuilds it)
     }
 }
@@ -1359,6 +1360,18 @@ __global__ __launch_bounds__(WG) void k_rows_wchunks(RowsArgs g, const int *ubas
     }
 }
 
+// lanes of a wave holding consecutive products: runs of equal window w
+// (w = -1 for invalid lanes, a suffix).  Returns the boundary mask (a bit per
+// lane that starts a run); *len = the run's length for its first lane.
+__device__ __forceinline__ u64 wave_runs(int w, int *len) {
+    const int lane = lane_id();
+    const int wp = __shfl_up(w, 1, 64);
+    const u64 bm = __ballot(lane == 0 || wp != w);
+    const u64 above = bm & ~((2ull << lane) - 1ull);  // (lane 63: none)
+    *len = (above ? __builtin_ctzll(above) : 64) - lane;
+    return bm;
+}
+
 // the chunk's products counted per window into LDS hist (zeroed by the caller
 // before; the batch's run table loaded into wt); returns the row's window shape
 __device__ __forceinline__ void w_chunk_hist(const RowsArgs &g, int4 ch, int lo, int wb, int *hist, WalkTab &wt,
@@ -1367,8 +1380,14 @@ __device__ __forceinline__ void w_chunk_hist(const RowsArgs &g, int4 ch, int lo,
     const int a0 = le.y, k = le.z, b0 = ch.y * RH_NT;
     rows_batch(g, a0, k, b0, wt);  // (its barriers also order the caller's zeroing)
     const int q0 = ch.z * W_CH, q1 = min(wt.tot, q0 + W_CH);
-    batch_walk<false>(g, min(RH_NT, k - b0), q0, q1, wt,
-                      [&](int c, double) { atomicAdd(&hist[(c - lo) >> wb], 1); }, rmap, red);
+    // one LDS add per run of equal windows in a wave (the runs of B are
+    // column-sorted: neighbouring lanes mostly share a window)
+    batch_walk<false>(g, min(RH_NT, k - b0), q0, q1, wt, [&](int c, double, bool v) {
+        const int w = v ? (c - lo) >> wb : -1;
+        int len;
+        const u64 bm = wave_runs(w, &len);
+        if (v && (bm >> lane_id() & 1ull)) atomicAdd(&hist[w], len);
+    }, rmap, red);
     __syncthreads();
 }
 
@@ -1454,10 +1473,22 @@ __global__ __launch_bounds__(W_NT) void k_rows_wscatter(RowsArgs g, const int4 *
     if (!binned || nw > W_SBW) {  // (workgroup-uniform)
         // (the run map above the cursors: W_MAXW * 4 + 8 KB within the union)
         unsigned short *const rm = reinterpret_cast<unsigned short *>(lds + W_MAXW * 4);
-        batch_walk<true>(g, nb, q0, q1, wt, [&](int c, double x) {
-            const long long o = base + atomicAdd(&cur[(c - lo) >> wb], 1);
-            g.Scol[o] = c;
-            g.Sval[o] = x;
+        // a run of equal windows in a wave takes its slots with one LDS add (its
+        // first lane's), so neighbouring lanes store to neighbouring slots
+        batch_walk<true>(g, nb, q0, q1, wt, [&](int c, double x, bool v) {
+            const int lane = lane_id();
+            const int w = v ? (c - lo) >> wb : -1;
+            int len;
+            const u64 bm = wave_runs(w, &len);
+            int b = 0;
+            if (v && (bm >> lane & 1ull)) b = atomicAdd(&cur[w], len);
+            const int hl = 63 - __builtin_clzll(bm & ((2ull << lane) - 1ull));  // this lane's run start
+            const int hb = __shfl(b, hl, 64);
+            if (v) {
+                const long long o = base + hb + (lane - hl);
+                g.Scol[o] = c;
+                g.Sval[o] = x;
+            }
         }, runmap ? rm : nullptr, red);
         return;
     }
@@ -2103,15 +2134,33 @@ __global__ __launch_bounds__(WG) void k_rows_compact(int m, const int *cfirst, c
 #pragma unroll
     for (int u = 0; u < PT; ++u) rowof[tid * PT + u] = max(carry, loc[u]);
     __syncthreads();
-    for (int i = tid; i < n; i += WG) {
-        const int r = rowof[i];
-        const long long so = soff[r];
-        if (so < 0) continue;  // (a windowed row: k_rows_wgather writes it)
-        const long long src = so + (c0 + i - Crp[r]);
-        // (streamed: staging read once, C not re-read by this call)
-        __builtin_nontemporal_store(__builtin_nontemporal_load(Scol + src), Ccol + c0 + i);
-        __builtin_nontemporal_store(__builtin_nontemporal_load(Sval + src), Cval + c0 + i);
+    // each thread's PT positions: their rows' offsets, then every load, then
+    // every store (a windowed row's positions, soff < 0, are k_rows_wgather's)
+    long long src[PT];
+    bool ok[PT];
+#pragma unroll
+    for (int u = 0; u < PT; ++u) {
+        const int i = u * WG + tid;
+        ok[u] = i < n;
+        const int r = ok[u] ? rowof[i] : 0;
+        const long long so = ok[u] ? soff[r] : -1;
+        ok[u] = so >= 0;
+        src[u] = ok[u] ? so + (c0 + i - Crp[r]) : 0;
     }
+    int cv[PT];
+    double xv[PT];
+#pragma unroll
+    for (int u = 0; u < PT; ++u)
+        if (ok[u]) {  // (streamed: staging read once, C not re-read by this call)
+            cv[u] = __builtin_nontemporal_load(Scol + src[u]);
+            xv[u] = __builtin_nontemporal_load(Sval + src[u]);
+        }
+#pragma unroll
+    for (int u = 0; u < PT; ++u)
+        if (ok[u]) {
+            __builtin_nontemporal_store(cv[u], Ccol + c0 + u * WG + tid);
+            __builtin_nontemporal_store(xv[u], Cval + c0 + u * WG + tid);
+        }
 }
 
 // Setup (stream-ordered, no host round trip): the entry table, its scan and the
