@@ -472,9 +472,11 @@ def main():
     workload = f"{name} C=A{'*A^T' if aat else '^2'} fp64 (device CSR in -> device CSR out), path {path_name}"
     if path_id == 3:
         kernel_desc = ("row-merge numeric phase (class H: k_rows_bitmap / hub rows k_rows_w*, k_rows_dr_*; "
-                       "k_rows_merge x5 classes, k_rows_small x2; in turn): B_alg of SURVEY §8d / HIP-event phase "
-                       "time")
-        traffic, traffic_src = pmc_traffic(["k_rows_small", "k_rows_merge", "k_rows_bitmap", "k_rows_wcount", "k_rows_wscatter", "k_rows_wunit", "k_rows_wgather",
+                       "k_rows_merge x5 classes, k_rows_small x2; in turn; with windowed or dominant-run rows "
+                       "to the end of their fills into C after the row scan): B_alg of SURVEY §8d / HIP-event "
+                       "phase time")
+        traffic, traffic_src = pmc_traffic(["k_rows_small", "k_rows_merge", "k_rows_bitmap", "k_rows_wplan",
+                                            "k_rows_wcount", "k_rows_wscatter", "k_rows_wunit", "k_rows_wgather",
                                             "k_rows_dr_"], workload)
     elif path_id == 2:
         kernel_desc = ("band row kernel k_band_rows (one workgroup per C row, LDS window accumulator): "

@@ -1710,8 +1710,9 @@ __global__ __launch_bounds__(WG) void k_rows_wgather(RowsArgs g, const int *umap
 //     in L (binary search of the B row) and whether L holds the column (then
 //     its sum joins that element); the row's nnz = |L| + the inserted columns;
 //     the row's chunks of DR_CH elements of L enqueued.
-//   k_rows_dr_fill, a workgroup per chunk: L streamed (coalesced) to the
-//     row's staging slots at i + (inserted columns before it), the inserted
+//   k_rows_dr_fill (after the row scan: the prep's counts are exact), a
+//     workgroup per chunk: L streamed (coalesced) straight into C at the
+//     row's pointer + i + (inserted columns before it), the inserted
 //     columns of its range beside them.  For L's element i the S columns
 //     before it are those with p <= i that L does not hold; an S column goes
 //     to p + (inserted columns before it).
@@ -1729,7 +1730,8 @@ struct DrEnt {     // one S column (sorted by column): insertion point, kind, co
 };
 constexpr int DR_NT = 1024;
 
-__global__ __launch_bounds__(DR_NT) void k_rows_dr_prep(RowsArgs g, DrRow *rows, DrEnt *ents, int2 *chunks,
+__global__ __launch_bounds__(DR_NT) void k_rows_dr_prep(RowsArgs g, long long *soff, DrRow *rows, DrEnt *ents,
+                                                        int2 *chunks,
                                                         int *nchunk, int *ndr) {
     constexpr int NW = DR_NT / 64;
     __shared__ unsigned long long sk[DR_SMAX];  // (column << 12 | S position), sorted
@@ -1862,13 +1864,15 @@ __global__ __launch_bounds__(DR_NT) void k_rows_dr_prep(RowsArgs g, DrRow *rows,
         d.aL = g.vA[a0 + jl];
         rows[h] = d;
         g.rnnz[r] = (int)L + ndt;
+        soff[r] = -1;  // (the compaction skips the row: k_rows_dr_fill writes it into C)
         const int nch = (int)((L + DR_CH - 1) / DR_CH);
         const int c0 = atomicAdd(nchunk, nch);
         for (int c = 0; c < nch; ++c) chunks[c0 + c] = make_int2(h, c * DR_CH);
     }
 }
 
-__global__ __launch_bounds__(DR_NT) void k_rows_dr_fill(RowsArgs g, const DrRow *rows, const DrEnt *ents,
+__global__ __launch_bounds__(DR_NT) void k_rows_dr_fill(RowsArgs g, const int *Crp, int *Ccol, double *Cval,
+                                                        const DrRow *rows, const DrEnt *ents,
                                                         const int2 *chunks, const int *nchunk) {
     __shared__ int sp[DR_SMAX];   // the chunk's S entries: insertion points
     __shared__ int snd[DR_SMAX];  // inserted columns before each
@@ -1903,8 +1907,8 @@ __global__ __launch_bounds__(DR_NT) void k_rows_dr_fill(RowsArgs g, const DrRow 
         sval[t] = e.val;
     }
     __syncthreads();
-    int *const Ocol = g.Scol + d.base;
-    double *const Oval = g.Sval + d.base;
+    int *const Ocol = Ccol + Crp[d.r];
+    double *const Oval = Cval + Crp[d.r];
     for (int i = i0 + tid; i < i1; i += DR_NT) {
         const int c = g.Bcol[d.bs + i];
         double v = d.aL * g.Bval[d.bs + i];
@@ -2218,6 +2222,12 @@ void dev_rows_release(Context &cx, RowsPlan &p) {
 int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPlan &p, tsg_dev_csr &C,
                  tsg_stats *st, hipStream_t s, hipEvent_t *ev) {
     const int m = A.m;
+    // (a row's products are counted in int inside the class-H kernels: a row past
+    // 2^31 - 1 products is refused rather than wrapped)
+    if (p.pmax > 0x7fffffffLL) {
+        dev_rows_release(cx, p);
+        return TSG_ERR_UNSUPPORTED;
+    }
     C = tsg_dev_csr{};
     C.m = m;
     C.n = B.n;
@@ -2290,6 +2300,7 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
     int4 *wchunks = nullptr;
     double *Wv = nullptr;
     int nu = 0;
+    long long drnch = 0;  // the dominant-run rows' fill chunks (launched after the row scan)
     RowsArgs g7 = g;  // (class H's list, for the windowed rows' gather after the row scan)
     if (ncls[7] > 0) {
         // class H: each kernel takes its rows of the class and its other
@@ -2385,10 +2396,9 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
             TSG_TRY(cx.get(&drows, (size_t)ndr));
             TSG_TRY(cx.get(&dents, (size_t)ndr * DR_SMAX));
             TSG_TRY(cx.get(&dchunks, (size_t)nch));
-            k_rows_dr_prep<<<n7, DR_NT, 0, s>>>(g, drows, dents, dchunks, p.cls + 20, p.cls + 21);
+            k_rows_dr_prep<<<n7, DR_NT, 0, s>>>(g, soff, drows, dents, dchunks, p.cls + 20, p.cls + 21);
             TSG_HIP(hipGetLastError());
-            k_rows_dr_fill<<<(unsigned)nch, DR_NT, 0, s>>>(g, drows, dents, dchunks, p.cls + 20);
-            TSG_HIP(hipGetLastError());
+            drnch = nch;
         }
     }
     auto classes = [&]() -> int {
@@ -2433,11 +2443,18 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
         return TSG_OK;
     };
     // the windowed rows' nonzeros straight into C (the compaction skips those rows)
+    // and the dominant-run rows' (their counts exact since k_rows_dr_prep)
     auto wgather = [&]() -> int {
-        if (nu == 0) return TSG_OK;
-        k_rows_wgather<<<nu, WG, 0, s>>>(g7, umap, wpre, ubo, uoff, ucount, Wc, Wv, C.rowpointer, C.columnindex,
-                                         C.value);
-        TSG_HIP(hipGetLastError());
+        if (nu > 0) {
+            k_rows_wgather<<<nu, WG, 0, s>>>(g7, umap, wpre, ubo, uoff, ucount, Wc, Wv, C.rowpointer,
+                                             C.columnindex, C.value);
+            TSG_HIP(hipGetLastError());
+        }
+        if (drnch > 0) {
+            k_rows_dr_fill<<<(unsigned)drnch, DR_NT, 0, s>>>(g7, C.rowpointer, C.columnindex, C.value, drows, dents,
+                                                              dchunks, p.cls + 20);
+            TSG_HIP(hipGetLastError());
+        }
         return TSG_OK;
     };
     int *cfirst = nullptr;
@@ -2464,7 +2481,11 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
         if (ev) TSG_HIP(hipEventRecord(ev[5], s));
     } else {
         TSG_TRY(classes());
-        if (ev) TSG_HIP(hipEventRecord(ev[5], s));
+        // (the numeric phase: to the class kernels' end, or -- with windowed or
+        // dominant-run rows, whose nonzeros go straight into C after the row
+        // scan -- to the end of those fills, the scan included)
+        const bool fills = nu > 0 || drnch > 0;
+        if (ev && !fills) TSG_HIP(hipEventRecord(ev[5], s));
 #ifdef TSG_ROWS_PROF
         {
             static unsigned long long raw[3 * 256 * 12];
@@ -2484,6 +2505,8 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
         }
 #endif
         TSG_TRY(scan_alloc());
+        TSG_TRY(wgather());
+        if (ev && fills) TSG_HIP(hipEventRecord(ev[5], s));
         if (cap > 0) {
             const int nch = (int)((cap + CP_CH - 1) / CP_CH);
             TSG_TRY(cx.get(&cfirst, (size_t)nch + 1));
@@ -2492,7 +2515,6 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
             k_rows_compact<<<nch, WG, 0, s>>>(m, cfirst, soff, C.rowpointer, Scol, Sval, C.columnindex, C.value);
         }
         TSG_HIP(hipGetLastError());
-        TSG_TRY(wgather());
     }
     if (small) TSG_HIP(hipMemcpyAsync(cx.pinned64 + 15, C.rowpointer + m, sizeof(int), hipMemcpyDeviceToHost, s));
     if (ev) TSG_HIP(hipEventRecord(ev[3], s));
