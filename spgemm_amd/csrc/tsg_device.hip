@@ -1311,13 +1311,37 @@ __global__ __launch_bounds__(WG) void k_entry_bounds(const int *ciA, long nnzA, 
 // by a system-scope store into the caller's host-mapped flag (no device flag,
 // no memset, no copy back).
 constexpr int SRT_TILE = 4096;
+// first index in [0, n) whose element is >= key (n if none), a wave at a time:
+// 64 probes per step (ballot), so log64(n) dependent loads instead of log2(n)
+// (mawi's 226 M row pointers: 5 instead of 28)
+__device__ __forceinline__ int wave_lower_bound(const int *a, int n, int key) {
+    const int lane = lane_id();
+    long long lo = 0, hi = n;  // the answer lies in [lo, hi]
+    while (hi - lo > 64) {
+        const long long step = (hi - lo + 63) / 64;
+        const long long x = lo + lane * step;
+        const bool ge = x >= hi || a[x] >= key;  // (monotone over the lanes)
+        const u64 b = __ballot(ge);
+        const int f = b ? __builtin_ctzll(b) : 64;
+        const long long nlo = f > 0 ? lo + (long long)(f - 1) * step + 1 : lo;
+        hi = f < 64 ? min(hi, lo + (long long)f * step) : hi;
+        lo = nlo;
+    }
+    const long long x = lo + lane;
+    const u64 b = __ballot(x < hi && a[x] >= key);
+    return b ? (int)(lo + __builtin_ctzll(b)) : (int)hi;
+}
+
 __global__ __launch_bounds__(WG) void k_rows_sorted_tiles(const int *rp, const int *ci, int m, int nnz, int *hflag) {
     __shared__ u32 st[SRT_TILE / 32];
     __shared__ int rr[2];
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, wv = wave_id();
     const int p0 = blockIdx.x * SRT_TILE, p1 = min(nnz, p0 + SRT_TILE);
     for (int i = tid; i < SRT_TILE / 32; i += WG) st[i] = 0;
-    if (tid < 2) rr[tid] = lower_bound_dev(rp, 0, m + 1, tid ? p1 : p0);  // rows starting in [p0, p1)
+    if (wv < 2) {  // rows starting in [p0, p1): waves 0 and 1 search the row pointers
+        const int r = wave_lower_bound(rp, m + 1, wv ? p1 : p0);
+        if (lane_id() == 0) rr[wv] = r;
+    }
     __syncthreads();
     for (int r = rr[0] + tid; r < rr[1]; r += WG) {
         const int p = rp[r];

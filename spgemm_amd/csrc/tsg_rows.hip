@@ -2113,6 +2113,7 @@ __global__ __launch_bounds__(WG) void k_rows_compact(int m, const int *cfirst, c
     const int n = min(CP_CH, nnz - c0);
     const int rf = cfirst[blockIdx.x];
     const int rl = c0 + CP_CH < nnz ? cfirst[blockIdx.x + 1] : m - 1;
+    if (rf == rl && soff[rf] < 0) return;  // (inside one row written elsewhere: windowed / dominant-run)
     for (int i = tid; i < CP_CH; i += WG) rowof[i] = i == 0 ? rf : -1;
     __syncthreads();
     for (int r = rf + 1 + tid; r <= rl; r += WG) {
