@@ -157,7 +157,18 @@ struct RowsPlan {
     long long hubprod = 0;     // hub rows' products (past kRowsHubProducts)
     long long hk = 0;          // class-H rows with more runs than the one-walk kernel takes
     long long hbig = 0;        // class-H rows' products past the one-walk register share (their scratch)
+    // ordered batches (k_rows_ob): per row (first A entry, entries, products, class),
+    // its class byte, the packing segments' batch lists, their counts, the batches' first rows
+    int4 *rinfo = nullptr;
+    signed char *rcls = nullptr;
+    int *lstart = nullptr, *nbs = nullptr, *bstart = nullptr;
+    int nseg = 0, nb = 0;
+    bool ob_prep = false;
 };
+// the ordered-batch kernel packs each row's keys as (column - the row's first
+// column, position) in 32 bits with up to 12 position bits: B's columns must
+// span less than 2^20 - 1
+constexpr long long kObMaxCols = (1LL << 20) - 2;
 // Class-H rows past kRowsHubProducts products are hub rows: one run holding all
 // but 4,096 of them -> the dominant-run kernels (k_rows_dr_*); the other hub
 // rows and the rows past the one-walk kernel's runs or column span -> the
