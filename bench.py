@@ -103,12 +103,13 @@ def _strided_rows(m, rp, ci, vv, stride):
 def _timed_sample(fn, m, rp, ci, vv, rpb, budget_s):
     """fn(A sample) timed on the whole A when a probe predicts it fits budget_s,
     else on a strided row sample sized to it ("time a strided
-    row sample and extrapolate"); (stride, products of the sample, seconds)."""
+    row sample and extrapolate"); (stride, products of the sample, seconds,
+    fn's result on the sample)."""
     blen = np.diff(rpb.astype(np.int64))
     probe = max(1, m // 2000)
     sub = _strided_rows(m, rp, ci, vv, probe)
     t0 = time.perf_counter()
-    fn(*sub)
+    res = fn(*sub)
     t = time.perf_counter() - t0
     stride = probe
     while True:  # (small samples overestimate: fixed per-call costs) -- refine once or twice
@@ -119,32 +120,52 @@ def _timed_sample(fn, m, rp, ci, vv, rpb, budget_s):
         stride = min(nxt, stride)
         sub = _strided_rows(m, rp, ci, vv, stride) if stride > 1 else (m, rp, ci, vv)
         t0 = time.perf_counter()
-        fn(*sub)
+        res = fn(*sub)
         t = time.perf_counter() - t0
         if stride == 1:
             break
-    return stride, int(blen[sub[2]].sum()), t
+    return stride, int(blen[sub[2]].sum()), t, res
+
+
+def _row_chunks(mm, r, c, blen, cap=1.5e9):
+    """[r0, r1) row ranges of a CSR whose intermediate products stay <= cap each
+    (products bound nnz(C): every chunk's C fits the oracle's int32 row pointers)."""
+    cum = np.concatenate([[0], np.cumsum(blen[c])])[r.astype(np.int64)]
+    out, r0 = [], 0
+    while r0 < mm:
+        r1 = int(np.searchsorted(cum, cum[r0] + cap, side="right")) - 1
+        r1 = min(mm, max(r1, r0 + 1))
+        out.append((r0, r1))
+        r0 = r1
+    return out
 
 
 def cpu_baseline(m, n, rp, ci, vv, mb, nb, rpb, cib, vvb, budget_s):
-    """The reference's CPU SPA (spgemm_serialref_spa_new.h, clean-room oracle
+    """The reference's CPU SPA (spgemm_serialref_spa_new.h:7-105, clean-room oracle
     restatement, both passes; symbolic only) on the same workload -- whole when it
     fits the budget, else a strided row sample marked "extrapolated" -- plus the
-    oracle's numeric Gustavson timed beside it."""
+    oracle's numeric Gustavson timed beside it.  The SPA runs in
+    row chunks of <= 1.5e9 products so that every chunk's C fits int32 row
+    pointers (the oracle's, as the reference's `int nnzC`); its nnz(C) is
+    reported (the whole C's when every row ran)."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import _oracle as O
     B = O.OMat.from_csr(mb, nb, rpb, cib, vvb)
+    blen = np.diff(rpb.astype(np.int64))
 
     def spa(mm, r, c, v):
         A = O.OMat.from_csr(mm, n, r, c, v)
-        O.spa(A, B, 0, mm)
+        nnz = 0
+        for r0, r1 in _row_chunks(mm, r, c, blen):
+            nnz += len(O.spa(A, B, r0, r1)[1])
+        return nnz
 
     def gus(mm, r, c, v):
         A = O.OMat.from_csr(mm, n, r, c, v)
-        O.gustavson_rows(A, B, 0, mm)
+        return O.gustavson_rows(A, B, 0, mm)
 
-    stride, cub, t = _timed_sample(spa, m, rp, ci, vv, rpb, budget_s)
-    nstride, ncub, nt = _timed_sample(gus, m, rp, ci, vv, rpb, budget_s / 2)
+    stride, cub, t, spa_nnz = _timed_sample(spa, m, rp, ci, vv, rpb, budget_s)
+    nstride, ncub, nt, _ = _timed_sample(gus, m, rp, ci, vv, rpb, budget_s / 2)
     thr = O.num_threads()
     nproc = os.cpu_count()
     affinity = _AFFINITY
@@ -158,7 +179,8 @@ def cpu_baseline(m, n, rp, ci, vv, mb, nb, rpb, cib, vvb, budget_s):
     return {"value": round(2.0 * cub / t / 1e9, 4), "unit": "GFLOPS", "cores": cores, "omp_threads": thr,
             "nproc": nproc, "affinity_cpus": affinity,
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
-            "kind": "port", "extrapolated": stride > 1,
+            "kind": "port", "extrapolated": stride > 1, "seconds": round(t, 3),
+            "nnzC": int(spa_nnz), "nnzC_of": "all rows" if stride == 1 else f"the sample (every {stride}-th row)",
             "sample": f"spgemm_spa restatement (count+fill passes, symbolic), {what(stride)} of {m} "
                       f"({cub} intermediate products), {t:.1f} s; {thr} OpenMP threads on {cores} "
                       f"usable CPU(s) of {nproc} (affinity mask {affinity}; OMP_PROC_BIND="
@@ -168,7 +190,7 @@ def cpu_baseline(m, n, rp, ci, vv, mb, nb, rpb, cib, vvb, budget_s):
                                   f"{nt:.1f} s"}}
 
 
-def tiled_leg(m, n, rp, ci, vv, mb, nb, rpb, cib, vvb, aat, tm, nnzcub, reps=3):
+def tiled_leg(m, n, rp, ci, vv, mb, nb, rpb, cib, vvb, aat, tm, nnzcub, reps=3, warmup=1):
     """The reference-layout drop-in path, timed like the reference: csr2tile of A
     (row-major) and B (col-major) on the host API, then tsg_tilespgemm -- tiles
     in, the reference's tiled C out (tile-pattern step 1 incl. empty C tiles,
@@ -183,11 +205,11 @@ def tiled_leg(m, n, rp, ci, vv, mb, nb, rpb, cib, vvb, aat, tm, nnzcub, reps=3):
     T.csr2tile_row_major(A, tm, tm)
     T.csr2tile_col_major(B, tm, tm)
     runs = []
-    for _ in range(reps + 1):
+    for _ in range(reps + max(1, warmup)):
         Cm, info = T.tilespgemm(A, B, tm, tm, nnzCub=nnzcub)
         runs.append((info, Cm.s.numtile))
         del Cm
-    runs = runs[1:]  # first call warms the context's caching allocator
+    runs = runs[max(1, warmup):]  # the first call(s) warm the context's caching allocator
     med = lambda k: float(np.median([r[0][k] for r in runs]))
     t = med("time_tile")
     numblk, nnzc = int(runs[0][1]), int(runs[0][0]["nnzC"])
@@ -214,12 +236,14 @@ def tiled_leg(m, n, rp, ci, vv, mb, nb, rpb, cib, vvb, aat, tm, nnzcub, reps=3):
             "path": "tsg_tilespgemm (reference tiled layout in/out; the ./test CLI path)"}
 
 
-def pmc_traffic(kernels, workload):
-    """HBM bytes per call of the `kernels` (name substrings; their per-dispatch
-    bytes summed) from the newest committed PMC summary of the same workload
-    (profiles/<round>_pmc.json, written by tools/profile.sh: 2*FETCH_SIZE +
-    WRITE_SIZE, separate --pmc passes).  (None, None) when absent."""
+def pmc_file(workload, explicit=None):
+    """The PMC summary the line's traffic comes from: `explicit` (--pmc-from: the
+    profile run of the same build writes it right before its timed run), else the
+    newest committed profiles/<round>_pmc.json of the same workload."""
     import glob
+    if explicit:
+        return explicit if os.path.exists(explicit) else None
+
     def workload_of(f):
         try:
             return json.load(open(f)).get("_workload")
@@ -227,15 +251,24 @@ def pmc_traffic(kernels, workload):
             return None
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc.json")))
     files = [f for f in files if workload_of(f) == workload]
-    if not files:
+    return files[-1] if files else None
+
+
+def pmc_traffic(kernels, path):
+    """HBM bytes per call of the `kernels` (name substrings; their per-dispatch
+    bytes summed) and of every kernel of the call, from a PMC summary
+    (tools/pmc_summary.py: 2*FETCH_SIZE + WRITE_SIZE, separate --pmc passes).
+    (unit bytes, all-kernel bytes per call), None where absent."""
+    if not path:
         return None, None
-    d = json.load(open(files[-1]))
+    d = json.load(open(path))
     tot, found = 0, False
     for kernel in kernels:  # (the kernels of the unit that ran for this workload)
         hits = [v for k, v in d.items() if kernel in k and isinstance(v, dict) and v.get("hbm_bytes_per_dispatch")]
         found |= bool(hits)
         tot += sum(int(v["hbm_bytes_per_dispatch"]) for v in hits)
-    return (tot, os.path.relpath(files[-1], REPO)) if found else (None, None)
+    allk = (d.get("_per_call") or {}).get("hbm_bytes")
+    return (tot if found else None), allk
 
 
 def main():
@@ -275,6 +308,12 @@ def main():
     ap.add_argument("--block-products", type=float, default=1.5e9,
                     help="row-block size (intermediate products) when the product exceeds int32 "
                          "nnz(C): such products run as sequential row blocks, C kept per block")
+    ap.add_argument("--pmc-from", default=None,
+                    help="PMC summary (tools/pmc_summary.py) the roofline's traffic comes from; default: the newest "
+                         "committed profiles/r*_pmc.json of the same workload")
+    ap.add_argument("--leg", default="device", choices=["device", "tiled"],
+                    help="tiled: time only the reference-layout drop-in path tsg_tilespgemm (the ./test timed "
+                         "region; e.g. under rocprofv3 for its kernel stats) and print its line")
     ap.add_argument("--tiled", type=int, default=None,
                     help="also time the reference-layout host path tsg_tilespgemm (csr2tile tiles "
                          "in, tiled C out; the reference's timed region) -> t_kern_tiled_ms; "
@@ -311,6 +350,22 @@ def main():
         mb, nb, rpb, cib, vvb = m, n, rp, ci, vv
     tm = args.tile
     full_m = m
+    if args.leg == "tiled":
+        # the drop-in path alone: csr2tile on the host API (untimed, as in the reference),
+        # then tsg_tilespgemm's timed region (steps 1-3 with allocations) per call
+        if args.rows is not None:
+            m, rp, ci, vv = args.rows, rp[:args.rows + 1].copy(), ci[:rp[args.rows]].copy(), vv[:rp[args.rows]].copy()
+        cub = nnzcub_rows(rp, ci, rpb, 0, m)
+        tl = tiled_leg(m, n, rp, ci, vv, mb, nb, rpb, cib, vvb, aat, tm, cub, reps=args.steps, warmup=args.warmup)
+        out = {"metric": METRIC, "value": tl["gflops"], "unit": "GFLOPS", "n_gpus": 1, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": tl["t_kern_tiled_ms"], "higher_is_better": True,
+               "scaling": "single", "vs_baseline": None, "dtype": "f64", "data": data_kind,
+               "config": {"workload": f"{name} C=A{'*A^T' if aat else '^2'} fp64, tsg_tilespgemm {tm}x{tm} "
+                                      f"(tiles in -> tiled C out; the reference's timed region)",
+                          "m": m, "nnzA": int(len(ci)), "nnzCub": cub, "nnzC": tl["nnzC"], "path": "tiled"},
+               "roofline": tl["roofline"], "tiled": tl}
+        print(json.dumps(out), flush=True)
+        return
     blen_b = np.diff(rpb.astype(np.int64))
     cum = np.concatenate([[0], np.cumsum(blen_b[ci])])[rp]  # nnzCub of row prefixes
     rows = args.rows
@@ -468,23 +523,25 @@ def main():
     k3_ms = med["t_step3_kernel_ms"]
     achieved = b_alg / (k3_ms * 1e-3) / 1e9
     path_id = int(med["path"])
-    path_name = {-1: "mixed", 0: "tiles", 1: "fused", 2: "band", 3: "rows"}.get(path_id, str(path_id))
+    path_name = {-1: "mixed", 0: "tiles", 2: "band", 3: "rows"}.get(path_id, str(path_id))
     workload = f"{name} C=A{'*A^T' if aat else '^2'} fp64 (device CSR in -> device CSR out), path {path_name}"
     if path_id == 3:
         kernel_desc = ("row-merge numeric phase (class H: k_rows_bitmap / hub rows k_rows_w*, k_rows_dr_*; "
                        "k_rows_merge x5 classes, k_rows_small x2; in turn; with windowed or dominant-run rows "
                        "to the end of their fills into C after the row scan): B_alg of SURVEY §8d / HIP-event "
                        "phase time")
-        traffic, traffic_src = pmc_traffic(["k_rows_small", "k_rows_merge", "k_rows_bitmap", "k_rows_wplan",
-                                            "k_rows_wcount", "k_rows_wscatter", "k_rows_wunit", "k_rows_wgather",
-                                            "k_rows_dr_"], workload)
+        unit_kernels = ["k_rows_small", "k_rows_merge", "k_rows_bitmap", "k_rows_wplan", "k_rows_wcount",
+                        "k_rows_wscatter", "k_rows_wunit", "k_rows_wgather", "k_rows_dr_", "k_rows_ob"]
     elif path_id == 2:
         kernel_desc = ("band row kernel k_band_rows (one workgroup per C row, LDS window accumulator): "
                        "B_alg of SURVEY §8d / HIP-event kernel time")
-        traffic, traffic_src = pmc_traffic(["k_band_rows"], workload)
+        unit_kernels = ["k_band_rows"]
     else:
         kernel_desc = "step-3 numeric kernel (fused tile2csr): B_alg of SURVEY §8d / HIP-event kernel time"
-        traffic, traffic_src = pmc_traffic(["k_step3"], workload)
+        unit_kernels = ["k_step3"]
+    pfile = pmc_file(workload, args.pmc_from)
+    traffic, traffic_all = pmc_traffic(unit_kernels, pfile)
+    traffic_src = os.path.relpath(pfile, REPO) if pfile else None
     chk = None
     if args.check and not gather:
         # checksum of this rank's C (every block), recomputed outside the timed region;
@@ -572,6 +629,15 @@ def main():
                          "pipeline": {"achieved": round(achieved_pipe, 2),
                                       "frac": round(achieved_pipe / HBM_PEAK_GBS, 5),
                                       "device_ms": round(dev_ms, 4)},
+                         # the whole pass as the driver times it: B_alg / ms_per_step (this rank's
+                         # bytes over the max-over-ranks step time), and every kernel's measured
+                         # HBM bytes of one call against B_alg
+                         "pass": {"achieved": round(b_alg / (ms_per_step * 1e-3) / 1e9, 2),
+                                  "frac": round(b_alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                                  "ms": round(ms_per_step, 4),
+                                  "traffic_all_kernels": traffic_all,
+                                  "traffic_all_over_b_alg": round(traffic_all / b_alg, 3) if traffic_all else None},
+                         "traffic_over_b_alg": round(traffic / b_alg, 3) if traffic else None,
                          "stream_bytes": int(b_stream),
                          "stream_achieved": round(b_stream / (k3_ms * 1e-3) / 1e9, 2)},
             "stage_ms": {k: round(med[k], 4) for k in ("t_csr2tile_ms", "t_step1_ms", "t_step2_ms",

@@ -77,12 +77,12 @@ typedef struct tsg_stats {
                                                       for the count units; CSR path only) */
     long long tile_products; /* tile-level intermediate products (step-1 work)  */
     double t_step3_kernel_ms;  /* the step-3 numeric kernel alone (dominant kernel) */
-    long long path;            /* the CSR path that ran: TSG_PATH_TILES / _FUSED / _BAND / _ROWS */
+    long long path;            /* the CSR path that ran: TSG_PATH_TILES / _BAND / _ROWS */
 } tsg_stats;
 
 /* tsg_stats.path (the CSR-in -> CSR-out routing) */
 #define TSG_PATH_TILES 0  /* staged tile pipeline: csr2tile structure, steps 1-3, tile2csr */
-#define TSG_PATH_FUSED 1  /* short rows: one persistent kernel over row units */
+/* 1: retired (the fused element path of rounds 1-3; the row-merge path is faster on short rows too) */
 #define TSG_PATH_BAND 2   /* banded rows: dense LDS window per row */
 #define TSG_PATH_ROWS 3   /* row merge: rows binned by products, B runs merged in LDS */
 

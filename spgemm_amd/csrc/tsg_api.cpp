@@ -855,23 +855,22 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
     //    least as many products as columns (FEM-like: cant); its check is a
     //    statistics kernel + one host round trip;
     //  * otherwise the row-merge setup (entry table, classes) + one round trip:
-    //    the row-merge path (tsg_rows.hip) unless hub rows without a dominant
-    //    run carry the product (dev_rows_accept: R-MAT).  (The fused path,
-    //    tsg_fused.hip, is no longer a default: since the merge classes' value
-    //    preload the row-merge path is faster on short rows too -- mc2depi
-    //    A*A^T 0.25 vs 0.35 ms; TSG_PATH=fused still runs it.)
-    //  * the staged tile pipeline below for the rest and for unsorted B rows.
-    // TSG_PATH=fused / band / rows / tiles forces a path (band when its check
-    // passes).
+    //    the row-merge path (tsg_rows.hip) for every product whose B rows are
+    //    strictly column-sorted, hub rows included (dominant-run / windowed
+    //    kernels), unless a row holds more than 2^31 - 1 products
+    //    (dev_rows_accept);
+    //  * the staged tile pipeline below for the rest and for unsorted B rows
+    //    (or rows repeating a column).
+    // TSG_PATH=band / rows / tiles forces a path (band when its check passes).
     const char *path = getenv("TSG_PATH");
-    const bool force_fused = path && !strcmp(path, "fused"), force_tiles = path && !strcmp(path, "tiles");
+    const bool force_tiles = path && !strcmp(path, "tiles");
     const bool force_band = path && !strcmp(path, "band"), force_rows = path && !strcmp(path, "rows");
     if (!force_tiles) {
         bool band = false;
         BandWin bw;
         // band candidates first (A rows of >= 8 entries on average): the window
         // check's read-back also brings the sortedness flag
-        if (!force_fused && !force_rows && (force_band || (A->m > 0 && A->nnz >= 8LL * A->m)))
+        if (!force_rows && (force_band || (A->m > 0 && A->nnz >= 8LL * A->m)))
             TSG_TRY(dev_band_check(cx, *A, *B, force_band, &band, &bw, s));
         if (band && cx.pinned[1] != 0) {  // unsorted B rows: the windows mean nothing
             cx.put(bw.win);
@@ -887,21 +886,15 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
             TSG_TRY(rc);
             path_id = TSG_PATH_BAND;
         } else {
-            // the row-merge setup (its entry table is the fused path's too) and the
-            // sortedness flag: one host round trip decides fused / rows / tiles
+            // the row-merge setup and the sortedness flag: one host round trip
+            // decides rows / tiles
             TSG_HIP(hipEventRecord(cx.ev[0], s));
             RowsPlan plan;
             TSG_TRY(dev_rows_setup_async(cx, *A, *B, plan, s));
             TSG_TRY(stream_wait(s));
             dev_rows_setup_read(cx, plan);
             const bool bsorted0 = cx.pinned[1] == 0;
-            const bool fused_fits = (long long)B->n < kFusedMaxCols;  // (else the fused path is UNSUPPORTED)
-            if (bsorted0 && !force_band && fused_fits && force_fused) {
-                const int rc = dev_spgemm_fused(cx, *A, *B, *C, &st, s, cx.ev, plan.ebnd, plan.E);
-                dev_rows_release(cx, plan);
-                TSG_TRY(rc);
-                path_id = TSG_PATH_FUSED;
-            } else if (bsorted0 && !force_band && (force_rows || dev_rows_accept(plan))) {
+            if (bsorted0 && !force_band && (force_rows || dev_rows_accept(plan))) {
                 TSG_TRY(dev_rows_run(cx, *A, *B, plan, *C, &st, s, cx.ev));
                 path_id = TSG_PATH_ROWS;
             } else {

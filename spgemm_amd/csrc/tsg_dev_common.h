@@ -1,6 +1,6 @@
 // tsg_dev_common.h -- wave64 / workgroup primitives shared by the gfx950 kernels
-// (tsg_device.hip: csr2tile, the tiled steps, tile2csr; tsg_fused.hip: the fused
-// element-path SpGEMM).  Device code only; include after tsg_internal.h.
+// (tsg_device.hip: csr2tile, the tiled steps, tile2csr; tsg_rows.hip, tsg_band.hip:
+// the row-merge and banded CSR paths).  Device code only; include after tsg_internal.h.
 #pragma once
 
 #include <climits>

@@ -1306,8 +1306,9 @@ __global__ __launch_bounds__(WG) void k_entry_bounds(const int *ciA, long nnzA, 
 // row starts as a bitmap over entry positions (bit p set: some non-empty row starts at p)
 // Row sortedness in one pass, a workgroup per SRT_TILE entries: the rows
 // starting in the tile (a binary search of its bounds in the row pointers)
-// mark their first entries in an LDS bitmap, then a descent ci[p] < ci[p-1]
-// that is not at a row start means some row is not column-sorted -- reported
+// mark their first entries in an LDS bitmap, then a non-ascent ci[p] <= ci[p-1]
+// (a descent, or a column repeated inside the row) that is not at a row start
+// means some row is not strictly column-sorted -- reported
 // by a system-scope store into the caller's host-mapped flag (no device flag,
 // no memset, no copy back).
 constexpr int SRT_TILE = 4096;
@@ -1350,7 +1351,7 @@ __global__ __launch_bounds__(WG) void k_rows_sorted_tiles(const int *rp, const i
     __syncthreads();
     bool bad = false;
     for (int p = max(1, p0) + tid; p < p1; p += WG)
-        bad |= ci[p] < ci[p - 1] && !((st[(p - p0) >> 5] >> ((p - p0) & 31)) & 1u);
+        bad |= ci[p] <= ci[p - 1] && !((st[(p - p0) >> 5] >> ((p - p0) & 31)) & 1u);
     if (__ballot(bad) && lane_id() == 0) __hip_atomic_store(hflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 

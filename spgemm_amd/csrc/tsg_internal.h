@@ -116,16 +116,6 @@ int dev_tile_masks(Context &cx, const tsg_dev_csr &M, tsg_dev_tiles &t, uint16_t
 int dev_rows_sorted(Context &cx, const tsg_dev_csr &M, bool *sorted, hipStream_t s);
 int dev_rows_sorted_async(Context &cx, const tsg_dev_csr &M, int *host_flag, hipStream_t s);
 int dev_tile2csr(Context &cx, const tsg_dev_tiles &C, tsg_dev_csr &out, hipStream_t s);
-// fused element path (tsg_fused.hip): CSR in -> CSR out, B rows column-sorted.
-// ev (optional): 0 start | 1 units built | 4, 5 around the unit kernel | 3 end
-// longest row of M, copied (stream-ordered) into *host_out
-int dev_row_maxlen_async(Context &cx, const tsg_dev_csr &M, int *host_out, hipStream_t s);
-// the fused path's segment keys hold a tile column below 2^24: B.n below this
-constexpr long long kFusedMaxCols = (1LL << 28) - 16;
-// ebnd / cum (optional): the entry table of a row-merge setup (same layout), reused
-int dev_spgemm_fused(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, tsg_dev_csr &C, tsg_stats *st,
-                     hipStream_t s, hipEvent_t *ev, int2 *ebnd_pre = nullptr, long long *cum_pre = nullptr);
-
 // banded path (tsg_band.hip): every C row's reachable columns within one
 // window of <= 2,048 columns, the windows holding at least as many products as
 // columns in all (FEM-like operands; force: any density).  BandWin holds the
@@ -143,8 +133,8 @@ int dev_spgemm_band(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, Ban
 // row-merge path (tsg_rows.hip): CSR in -> CSR out, B's rows column-sorted;
 // rows binned by element products, each row's B rows merged (or, for the
 // longest rows, marked in an LDS column bitmap).  Two halves around the
-// caller's one host round trip: the setup (entry table = the fused path's
-// too, classes, routing statistics), then the run.
+// caller's one host round trip: the setup (entry table, classes, routing
+// statistics), then the run.
 struct RowsPlan {
     int2 *ebnd = nullptr;      // per A entry: its B row's [start, end)
     long long *E = nullptr;    // per A entry: prefix of the element products
@@ -157,18 +147,7 @@ struct RowsPlan {
     long long hubprod = 0;     // hub rows' products (past kRowsHubProducts)
     long long hk = 0;          // class-H rows with more runs than the one-walk kernel takes
     long long hbig = 0;        // class-H rows' products past the one-walk register share (their scratch)
-    // ordered batches (k_rows_ob): per row (first A entry, entries, products, class),
-    // its class byte, the packing segments' batch lists, their counts, the batches' first rows
-    int4 *rinfo = nullptr;
-    signed char *rcls = nullptr;
-    int *lstart = nullptr, *nbs = nullptr, *bstart = nullptr;
-    int nseg = 0, nb = 0;
-    bool ob_prep = false;
 };
-// the ordered-batch kernel packs each row's keys as (column - the row's first
-// column, position) in 32 bits with up to 12 position bits: B's columns must
-// span less than 2^20 - 1
-constexpr long long kObMaxCols = (1LL << 20) - 2;
 // Class-H rows past kRowsHubProducts products are hub rows: one run holding all
 // but 4,096 of them -> the dominant-run kernels (k_rows_dr_*); the other hub
 // rows and the rows past the one-walk kernel's runs or column span -> the

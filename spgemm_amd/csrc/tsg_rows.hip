@@ -109,7 +109,6 @@ struct RowsArgs {
     int *rnnz;             // nnz of each row (the row pointers after a scan)
     int *Scol;             // staging: row r's nonzeros from E[rpA[r]]
     double *Sval;
-    const int *Crp;        // direct output (non-null): row r's nonzeros at Scol/Sval + Crp[r]
 };
 
 // per A entry: its B row's range and products (the latter scanned into E)
@@ -152,7 +151,7 @@ __device__ __forceinline__ int row_class(long long P, int k) {
 // order into the reserved slots.
 __global__ __launch_bounds__(WG) void k_rows_bin(const int *rpA, int m, const long long *E, const long long *Etot,
                                                  int *rnnz, int4 *lists, int *cls, long long *soff,
-                                                 unsigned long long *hst, int4 *rinfo, signed char *rcls) {
+                                                 unsigned long long *hst) {
     __shared__ int wc[NCLS][WAVES];
     __shared__ int gb[NCLS];
     __shared__ long long red64[WAVES];
@@ -187,10 +186,6 @@ __global__ __launch_bounds__(WG) void k_rows_bin(const int *rpA, int m, const lo
         const int c = row_class(P, ra1[u] - ra0[u]);
         soff[r] = e0[u];  // the row's staging offset
         rc[r - r0] = (signed char)c;
-        if (rinfo) {  // (the ordered batches' row table and the packer's classes)
-            rinfo[r] = make_int4(ra0[u], ra1[u] - ra0[u], (int)min(P, (long long)INT_MAX), c);
-            rcls[r] = (signed char)c;
-        }
         if (c < 0) rnnz[r] = 0;
 #pragma unroll
         for (int t = 0; t < NCLS; ++t) n[t] += c == t;
@@ -317,7 +312,7 @@ __global__ __launch_bounds__(WG) void k_rows_small(RowsArgs g) {
         r = e.x;
         a0 = e.y;
         k = e.z;
-        base = g.Crp ? g.Crp[r] : g.E[a0];  // (the output offset: not waited for until the output)
+        base = g.E[a0];  // (the output offset: not waited for until the output)
     }
     // lane sl < k: run sl's B range and A value; the runs' offsets in the row
     // by a scan of their lengths over the group
@@ -391,7 +386,7 @@ __global__ __launch_bounds__(WG) void k_rows_small(RowsArgs g) {
         g.Scol[o] = col;
         g.Sval[o] = s;
     }
-    if (live && sl == 0 && !g.Crp) g.rnnz[r] = __popcll(hb);
+    if (live && sl == 0) g.rnnz[r] = __popcll(hb);
 }
 
 // U independent searches in lockstep (U LDS reads in flight per step): first
@@ -512,7 +507,7 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 8 : 1) void k_rows_merge(RowsArgs 
         be = g.ebnd[le.y + tid];
         av = g.vA[le.y + tid];
     }
-    const long long base = g.Crp ? g.Crp[le.x] : g.E[le.y];  // (the output offset: not waited for until the output)
+    const long long base = g.E[le.y];  // (the output offset: not waited for until the output)
     double *const V = reinterpret_cast<double *>(kp[1][0]);
     {
         const int r = le.x;
@@ -748,7 +743,7 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 8 : 1) void k_rows_merge(RowsArgs 
             o += w < wv ? red[w] : 0;
             tot += red[w];
         }
-        if (tid == 0 && !g.Crp) g.rnnz[r] = tot;  // (direct output: counted before)
+        if (tid == 0) g.rnnz[r] = tot;
         if (packed) {
 #pragma unroll
             for (int u = 0; u < 4; ++u)
@@ -1214,8 +1209,6 @@ constexpr int W_NBLK = W_WORDS / W_BLK;
 constexpr int W_VCAP = 4096;                  // a unit's values per LDS pass
 constexpr int W_RPT = 8;                      // a unit's products per thread held in registers
 constexpr int W_SPANK = 8192;                 // plan: rows past so many runs span all of B's columns
-constexpr int W_SBW = 1024;                   // scatter: windows of a row binned in LDS per sub-batch
-constexpr int W_SB = 4 * W_NT;                // scatter: products per sub-batch (one walk step)
 
 __device__ __forceinline__ int ceil_log2_ll(long long v) {
     int l = 0;
@@ -1301,7 +1294,7 @@ __global__ __launch_bounds__(W_NT) void k_rows_wplan(RowsArgs g, int bn, long lo
             const int lg = ceil_log2_ll(span);
             wb = ceil_log2_ll((span * unit + P - 1) / P);
             wb = max(wb, lg - 13);                // (at most W_MAXW windows)
-            wb = max(wb, min(lg - 10, W_WBMAX));  // (at most W_SBW where the widest window allows)
+            wb = max(wb, min(lg - 10, W_WBMAX));  // (at most 1,024 windows where the widest window allows)
             wb = min(max(wb, W_WBMIN), W_WBMAX);
             nw = (int)((span + (1ll << wb) - 1) >> wb);
             lo = l;
@@ -1397,7 +1390,7 @@ __device__ __forceinline__ void w_chunk_hist(const RowsArgs &g, int4 ch, int lo,
 
 __global__ __launch_bounds__(W_NT) void k_rows_wcount(RowsArgs g, const int4 *chunks, const long long *cmoff,
                                                      const int *wlo, const int *wwb, const int *ubase, int *ucnt,
-                                                     int *cbo, int runmap) {
+                                                     int *cbo) {
     __shared__ int hist[W_MAXW];
     __shared__ WalkTab wt;
     __shared__ __align__(16) unsigned short rmap[4 * RH_NT];
@@ -1405,7 +1398,7 @@ __global__ __launch_bounds__(W_NT) void k_rows_wcount(RowsArgs g, const int4 *ch
     const int4 ch = chunks[blockIdx.x];
     const int u0 = ubase[ch.x], nw = ubase[ch.x + 1] - u0;
     for (int w = threadIdx.x; w < nw; w += W_NT) hist[w] = 0;
-    w_chunk_hist(g, ch, wlo[ch.x], wwb[ch.x], hist, wt, runmap ? rmap : nullptr, red);
+    w_chunk_hist(g, ch, wlo[ch.x], wwb[ch.x], hist, wt, rmap, red);
     int *const cb = cbo + cmoff[blockIdx.x];  // the chunk's place in each window's bucket
     for (int w = threadIdx.x; w < nw; w += W_NT)
         if (hist[w]) cb[w] = atomicAdd(&ucnt[u0 + w], hist[w]);
@@ -1447,23 +1440,19 @@ __global__ __launch_bounds__(W_NT) void k_rows_wscan(RowsArgs g, const int *ubas
 
 // the chunk's products to their windows' buckets in the row's staging slots
 // (bucket u at E[a0] + ubo[u]; the chunk's place in it from k_rows_wcount).
-// Each product is stored at its window's LDS cursor.  With binned
-// (TSG_W_SCATTER=1) rows of at most W_SBW windows bin each sub-batch of W_SB
-// products by window in LDS first (counts, a scan, the products placed), then
-// write it out in window order (runs of consecutive slots per window): measured
-// no faster, so not the default.
+// Each product is stored at its window's LDS cursor.  (Binning each sub-batch
+// by window in LDS first, then writing it out in window order, measured no
+// faster on the LiveJournal block: 2.744 vs 2.746 ms; removed.)
 __global__ __launch_bounds__(W_NT) void k_rows_wscatter(RowsArgs g, const int4 *chunks, const long long *cmoff,
                                                        const int *wlo, const int *wwb, const int *ubase,
-                                                       const int *ubo, const int *cbo, int binned, int runmap) {
-    constexpr int NW = W_NT / 64;
-    // direct: cursors of up to W_MAXW windows; binned: W_SBW cursors, W_SBW
-    // sub-batch counts / offsets, the sub-batch's columns and values
-    constexpr int LDSB = W_MAXW * 4 > W_SBW * 8 + W_SB * 12 ? W_MAXW * 4 : W_SBW * 8 + W_SB * 12;
-    __shared__ __align__(16) unsigned char lds[LDSB];
+                                                       const int *ubo, const int *cbo) {
+    // cursors of up to W_MAXW windows, the run map above them
+    __shared__ __align__(16) unsigned char lds[W_MAXW * 4 + 4 * RH_NT * 2];
     __shared__ WalkTab wt;
-    __shared__ int red[NW];
+    __shared__ int red[W_NT / 64];
     int *const cur = reinterpret_cast<int *>(lds);  // row-relative slots (windows not reached: unused)
-    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    unsigned short *const rm = reinterpret_cast<unsigned short *>(lds + W_MAXW * 4);
+    const int tid = threadIdx.x;
     const int4 ch = chunks[blockIdx.x];
     const int u0 = ubase[ch.x], nw = ubase[ch.x + 1] - u0;
     const int lo = wlo[ch.x], wb = wwb[ch.x];
@@ -1474,103 +1463,23 @@ __global__ __launch_bounds__(W_NT) void k_rows_wscatter(RowsArgs g, const int4 *
     rows_batch(g, a0, k, b0, wt);  // (its barriers also order the cursors above)
     const long long base = g.E[a0];
     const int q0 = ch.z * W_CH, q1 = min(wt.tot, q0 + W_CH), nb = min(RH_NT, k - b0);
-    if (!binned || nw > W_SBW) {  // (workgroup-uniform)
-        // (the run map above the cursors: W_MAXW * 4 + 8 KB within the union)
-        unsigned short *const rm = reinterpret_cast<unsigned short *>(lds + W_MAXW * 4);
-        // a run of equal windows in a wave takes its slots with one LDS add (its
-        // first lane's), so neighbouring lanes store to neighbouring slots
-        batch_walk<true>(g, nb, q0, q1, wt, [&](int c, double x, bool v) {
-            const int lane = lane_id();
-            const int w = v ? (c - lo) >> wb : -1;
-            int len;
-            const u64 bm = wave_runs(w, &len);
-            int b = 0;
-            if (v && (bm >> lane & 1ull)) b = atomicAdd(&cur[w], len);
-            const int hl = 63 - __builtin_clzll(bm & ((2ull << lane) - 1ull));  // this lane's run start
-            const int hb = __shfl(b, hl, 64);
-            if (v) {
-                const long long o = base + hb + (lane - hl);
-                g.Scol[o] = c;
-                g.Sval[o] = x;
-            }
-        }, runmap ? rm : nullptr, red);
-        return;
-    }
-    int *const lcnt = cur + W_SBW;  // the sub-batch's counts, then offsets
-    int *const scol = lcnt + W_SBW;
-    double *const sval = reinterpret_cast<double *>(scol + W_SB);
-    // the run map in the columns' space (read before the columns are placed)
-    unsigned short *const rm = reinterpret_cast<unsigned short *>(scol);
-    for (int qb = q0; qb < q1; qb += W_SB) {  // (workgroup-uniform)
-        const int n = min(W_SB, q1 - qb);
-        if (tid < W_SBW) lcnt[tid] = 0;
-        __syncthreads();
-        int c[4], wq[4], rq[4];
-        double x[4];
-        {
-            int b[4], len2[4], q[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                q[u] = qb + u * W_NT + tid;
-                b[u] = 0;
-                len2[u] = q[u] < q1 ? nb : 0;
-                c[u] = 0;
-                x[u] = 0.0;
-            }
-            if (runmap) {
-                batch_runmap(wt, nb, qb, rm, red);
-#pragma unroll
-                for (int u = 0; u < 4; ++u) b[u] = q[u] < q1 ? rm[q[u] - qb] + 1 : 1;
-            } else {
-                const bool ub[4] = {true, true, true, true};
-                search_ilp(wt.pre, b, len2, q, ub);
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (q[u] < q1) {
-                    const int pp = wt.bs[b[u] - 1] + q[u] - wt.pre[b[u] - 1];
-                    c[u] = g.Bcol[pp];
-                    x[u] = wt.av[b[u] - 1] * g.Bval[pp];
-                }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                wq[u] = q[u] < q1 ? (c[u] - lo) >> wb : -1;
-                rq[u] = wq[u] >= 0 ? atomicAdd(&lcnt[wq[u]], 1) : 0;
-            }
+    // a run of equal windows in a wave takes its slots with one LDS add (its
+    // first lane's), so neighbouring lanes store to neighbouring slots
+    batch_walk<true>(g, nb, q0, q1, wt, [&](int c, double x, bool v) {
+        const int lane = lane_id();
+        const int w = v ? (c - lo) >> wb : -1;
+        int len;
+        const u64 bm = wave_runs(w, &len);
+        int b = 0;
+        if (v && (bm >> lane & 1ull)) b = atomicAdd(&cur[w], len);
+        const int hl = 63 - __builtin_clzll(bm & ((2ull << lane) - 1ull));  // this lane's run start
+        const int hb = __shfl(b, hl, 64);
+        if (v) {
+            const long long o = base + hb + (lane - hl);
+            g.Scol[o] = c;
+            g.Sval[o] = x;
         }
-        __syncthreads();
-        // exclusive scan of the W_SBW counts (a thread each)
-        {
-            const int v = tid < W_SBW ? lcnt[tid] : 0;
-            const int inc = wave_incl_scan_dpp(v);
-            if (lane == 63) red[wv] = inc;
-            __syncthreads();
-            int off = inc - v;
-#pragma unroll
-            for (int w = 0; w < NW; ++w) off += w < wv ? red[w] : 0;
-            if (tid < W_SBW) lcnt[tid] = off;
-            __syncthreads();
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (wq[u] >= 0) {
-                const int d = lcnt[wq[u]] + rq[u];
-                scol[d] = c[u];
-                sval[d] = x[u];
-            }
-        __syncthreads();
-        // out in window order: slot i of window w at cur[w] + (i - its offset)
-        for (int i = tid; i < n; i += W_NT) {
-            const int cc = scol[i], w = (cc - lo) >> wb;
-            const long long o = base + cur[w] + (i - lcnt[w]);
-            g.Scol[o] = cc;
-            g.Sval[o] = sval[i];
-        }
-        __syncthreads();
-        // the windows' cursors past this sub-batch (next offset - this one)
-        if (tid < nw) cur[tid] += (tid + 1 < nw ? lcnt[tid + 1] : n) - lcnt[tid];
-        __syncthreads();
-    }
+    }, rm, red);
 }
 
 // rank of column c inside a unit's window (bitmap bm, block and group prefixes)
@@ -1935,162 +1844,6 @@ __global__ __launch_bounds__(DR_NT) void k_rows_dr_fill(RowsArgs g, const int *C
         }
 }
 
-// ---- direct output: every row's exact nnz before any class writes, so the
-// classes S16..M4 write C at its final CSR offsets (no staging, no second pass
-// over C).  A row's nnz is the number of distinct columns among its products:
-// each product's column inserted into an LDS hash set (Fibonacci hash, linear
-// probing, twice the class's products in slots), the successful inserts counted.
-// Only B's columns are read (4 B per product), no values, no sort.
-__device__ __forceinline__ bool hset_insert(u32 *ht, int hb, u32 c) {
-    u32 h = (c * 0x9E3779B1u) >> (32 - hb);
-    const u32 msk = (1u << hb) - 1u;
-    for (;;) {
-        const u32 old = atomicCAS(&ht[h], ~0u, c);  // (columns < 2^31: never the empty mark)
-        if (old == ~0u) return true;
-        if (old == c) return false;
-        h = (h + 1u) & msk;
-    }
-}
-
-// classes M0..M4: NT threads per row, four products per thread (the merge
-// kernels' run table and expansion, columns only)
-template <int NT, int CAP, int RUNS>
-__global__ __launch_bounds__(NT) void k_rows_count(RowsArgs g) {
-    constexpr int NW = NT / 64, HS = 2 * CAP;
-    constexpr int HB = CAP == 256 ? 9 : CAP == 512 ? 10 : CAP == 1024 ? 11 : CAP == 2048 ? 12 : 13;
-    static_assert((1 << HB) == HS && CAP == 4 * NT && RUNS <= NT, "count: table and thread shapes");
-    __shared__ u32 ht[HS];
-    __shared__ int roff[RUNS + 1];
-    __shared__ int rbs[RUNS];
-    __shared__ int red[2 * NW];
-    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
-    const int4 le = g.list[blockIdx.x];
-    int2 be = make_int2(0, 0);
-    if (tid < le.z) be = g.ebnd[le.y + tid];
-#pragma unroll
-    for (int u = 0; u < HS / NT; ++u) ht[u * NT + tid] = ~0u;
-    int k = 0, P = 0;
-    {
-        const int len = be.y - be.x;
-        const u64 b = __ballot(len > 0);
-        const int inc = wave_incl_scan_dpp(len);
-        if (lane == 63) {
-            red[wv] = __popcll(b);
-            red[NW + wv] = inc;
-        }
-        __syncthreads();
-        int off = 0, loff = 0;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) {
-            off += w < wv ? red[w] : 0;
-            k += red[w];
-            loff += w < wv ? red[NW + w] : 0;
-            P += red[NW + w];
-        }
-        if (len > 0) {
-            const int d = off + lanes_below(b);
-            roff[d] = loff + inc - len;
-            rbs[d] = be.x;
-        }
-        if (tid == 0) roff[k] = P;
-        __syncthreads();
-    }
-    const int e0 = 4 * tid, ne = max(0, min(4, P - e0));
-    int c[4] = {0, 0, 0, 0};
-    {
-        int j = 0, pa[4] = {0, 0, 0, 0};
-        if (ne > 0) j = lower_bound_dev(roff, 0, k + 1, e0 + 1) - 1;
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (u < ne) {
-                const int q = e0 + u;
-                while (roff[j + 1] <= q) ++j;
-                pa[u] = rbs[j] + q - roff[j];
-            }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (u < ne) c[u] = g.Bcol[pa[u]];
-    }
-    int cnt = 0;
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-        if (u < ne) cnt += hset_insert(ht, HB, (u32)c[u]);
-    cnt = wave_sum(cnt);
-    __syncthreads();  // (red's run counts read by every thread above)
-    if (lane == 0) red[wv] = cnt;
-    __syncthreads();
-    if (tid == 0) {
-        int tot = 0;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) tot += red[w];
-        g.rnnz[le.x] = tot;
-    }
-}
-
-// classes S16 / S64: G lanes per row (as k_rows_small), a 2G-slot set per row
-template <int G>
-__global__ __launch_bounds__(WG) void k_rows_count_small(RowsArgs g) {
-    constexpr int RPW = 64 / G, HB = G == 16 ? 5 : 7;
-    __shared__ u32 ht[WAVES][128];
-    const int lane = lane_id(), wv = wave_id(), sl = lane % G, gb = lane - sl;
-    const int i = (blockIdx.x * WAVES + wv) * RPW + lane / G;
-    if ((blockIdx.x * WAVES + wv) * RPW >= g.nrows) return;  // wave-uniform
-    ht[wv][lane] = ~0u;
-    ht[wv][lane + 64] = ~0u;
-    const bool live = i < g.nrows;
-    int r = 0, a0 = 0, k = 0;
-    if (live) {
-        const int4 e = g.list[i];
-        r = e.x;
-        a0 = e.y;
-        k = e.z;
-    }
-    int2 be = make_int2(0, 0);
-    if (sl < k) be = g.ebnd[a0 + sl];
-    const int len = be.y - be.x, bs = be.x;
-    int inc = len;
-    inc += dpp_mov<0x111, 0xf>(0, inc);
-    inc += dpp_mov<0x112, 0xf>(0, inc);
-    inc += dpp_mov<0x114, 0xf>(0, inc);
-    inc += dpp_mov<0x118, 0xf>(0, inc);
-    if constexpr (G == 64) {
-        inc += dpp_mov<0x142, 0xa>(0, inc);
-        inc += dpp_mov<0x143, 0xc>(0, inc);
-    }
-    const int roff = sl < k ? inc - len : INT_MAX;
-    const int P = __shfl(inc, G - 1, G);
-    int run = 0;
-    if constexpr (G == 64) {
-        for (int j = 1; j < k; ++j) run = (__builtin_amdgcn_readlane(roff, j) <= sl) ? j : run;
-    } else {
-#pragma unroll
-        for (int j = 1; j < G; ++j) run = __shfl(roff, j, G) <= sl ? j : run;
-    }
-    const int rs = __shfl(roff, run, G), rb = __shfl(bs, run, G);
-    bool fresh = false;
-    wave_lds_sync();  // (the sets' empty marks before any insert)
-    if (sl < P) fresh = hset_insert(&ht[wv][(lane / G) * 2 * G], HB, (u32)g.Bcol[rb + sl - rs]);
-    const u64 gm = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << gb;
-    const int n = __popcll(__ballot(fresh) & gm);
-    if (live && sl == 0) g.rnnz[r] = n;
-}
-
-// class H rows from the staging (at soff[r]) to their CSR place: a workgroup per row
-__global__ __launch_bounds__(WG) void k_rows_hcopy(const int4 *list, int n, const long long *soff, const int *Crp,
-                                                   const int *Scol, const double *Sval, int *Ccol, double *Cval) {
-    for (int i = blockIdx.x; i < n; i += gridDim.x) {
-        const int r = list[i].x;
-        const long long s = soff[r];
-        if (s < 0) continue;  // (a windowed row: k_rows_wgather writes it)
-        const int d = Crp[r], cnt = Crp[r + 1] - d;
-        for (int j = threadIdx.x; j < cnt; j += WG) {
-            __builtin_nontemporal_store(__builtin_nontemporal_load(Scol + s + j), Ccol + d + j);
-            __builtin_nontemporal_store(__builtin_nontemporal_load(Sval + s + j), Cval + d + j);
-        }
-    }
-}
-
-// every row's run from the staging area (at soff[r]) to its CSR place, by
 // chunks of CP_CH output positions (a workgroup each, consecutive lanes on
 // consecutive positions): the chunk's rows from cfirst (the row holding each
 // chunk's first position), each nonempty row marks its first position in LDS, a
@@ -2172,568 +1925,6 @@ __global__ __launch_bounds__(WG) void k_rows_compact(int m, const int *cfirst, c
         }
 }
 
-// ---- ordered batches (OB): the S16..M4 rows in row order, C written once ----
-//
-// The staging + compaction above writes C twice and reads it once (webbase:
-// 1.64 GB, the largest kernel of the pass).  Here the rows are cut, in row
-// order, into BATCHES that fit one 1,024-thread workgroup's sort slots (16
-// waves): class-S16 rows a quarter wave each (16 lanes, one product per lane),
-// S64 and M0 rows a wave, M1..M3 rows 2/4/8 waves (four products per lane), an
-// M4 row a batch of its own (16 waves), a class-H row a batch of its own (its
-// nonzeros computed before by k_rows_bitmap into the staging, copied here).
-// A workgroup takes batches in row order (a ticket), sorts its rows with the
-// merge classes' machinery (S: ranks by counting, M: wave bitonic sorts in
-// registers + cross-wave bitonic stages through LDS), publishes the batch's
-// nnz, learns its offset in C by a decoupled look-back over the batches, and
-// writes its nonzeros and row pointers straight into C: no staging, no
-// compaction, no scan of the row counts.
-//
-// Batches are packed greedily (next fit) inside segments of OB_SEG rows (one
-// wave per segment, k_rows_obpack): a batch never crosses a segment, so it
-// covers <= OB_SEG rows, and its slots are well filled (~90 % of the waves).
-constexpr int OB_NT = 1024, OB_NW = OB_NT / 64, OB_SLOTS = 4 * OB_NT;
-constexpr int OB_ROWS = 4 * OB_NW;  // nonempty rows per batch: one per quarter wave at most
-constexpr int OB_RUNS = OB_NT;      // A entries per batch (every class keeps <= 64 per wave)
-constexpr int OB_SEG = 512;         // rows per packing segment
-constexpr unsigned long long OB_AGG = 1ull << 62, OB_INC = 2ull << 62, OB_VAL = (1ull << 62) - 1;
-
-// waves of a class's row (S16: 0 -- quarter waves, counted apart)
-__device__ __forceinline__ int ob_waves(int c) {
-    return c <= 0 ? 0 : c <= 2 ? 1 : c == 3 ? 2 : c == 4 ? 4 : c == 5 ? 8 : 16;
-}
-
-// one wave per segment of OB_SEG rows: next-fit packing of its nonempty rows
-// into batches (16 waves: ceil(S16 rows / 4) + the other rows' waves); M4 and
-// H rows (classes 6, 7) each a batch of their own.  A segment's first batch
-// starts at its first row (empty rows go with the batch before them).
-// lstart[seg * (OB_SEG + 1) + j] = first row of the segment's batch j; nbs[seg] = batches.
-__global__ __launch_bounds__(WG) void k_rows_obpack(const signed char *rcls, int m, int nseg, int *lstart, int *nbs) {
-    const int lane = lane_id();
-    const int seg = blockIdx.x * WAVES + wave_id();
-    if (seg >= nseg) return;  // (wave-uniform)
-    const int r0 = seg * OB_SEG, r1 = min(m, r0 + OB_SEG);
-    int *const out = lstart + (long)seg * (OB_SEG + 1);
-    int nb = 0, q16 = 0, wf = 0;  // batches so far, the open batch's S16 rows and other waves
-    bool open = false;            // the open batch holds a row
-    if (lane == 0) out[0] = r0;
-    nb = 1;
-    for (int rb = r0; rb < r1; rb += 64) {  // (wave-uniform)
-        const int r = rb + lane;
-        const int c = r < r1 ? (int)rcls[r] : -1;
-        u64 live = __ballot(c >= 0);
-        while (live) {  // (uniform: one nonempty row at a time, in order)
-            const int l = __ffsll((long long)live) - 1;
-            live &= live - 1;
-            const int cl = __builtin_amdgcn_readlane(c, l);
-            const int row = rb + l;
-            bool cut;
-            if (cl >= 6) {  // a batch of its own, and the next row starts a new one
-                cut = open;
-                if (cut && lane == 0) out[nb] = row;
-                nb += cut;
-                open = true;
-                q16 = 0;
-                wf = OB_NW;  // (full: the next nonempty row cuts)
-                continue;
-            }
-            const int nq = q16 + (cl == 0), nw = wf + ob_waves(cl);
-            cut = open && (nq + 3) / 4 + nw > OB_NW;
-            if (cut) {
-                if (lane == 0) out[nb] = row;
-                ++nb;
-                q16 = cl == 0;
-                wf = ob_waves(cl);
-            } else {
-                q16 = nq;
-                wf = nw;
-            }
-            open = true;
-        }
-    }
-    if (lane == 0) nbs[seg] = nb;
-}
-
-// the segments' batch lists concatenated (boff = nbs scanned): bstart[b] = first
-// row of batch b, bstart[nb] = m; nb into *nbo
-__global__ __launch_bounds__(WG) void k_rows_obgather(const int *lstart, const int *boff, int nseg, int m,
-                                                      int *bstart, int *nbo) {
-    const int lane = lane_id();
-    const int seg = blockIdx.x * WAVES + wave_id();
-    if (seg > nseg) return;
-    if (seg == nseg) {
-        if (lane == 0) {
-            bstart[boff[nseg]] = m;
-            *nbo = boff[nseg];
-        }
-        return;
-    }
-    const int b0 = boff[seg], n = boff[seg + 1] - b0;
-    for (int j = lane; j < n; j += 64) bstart[b0 + j] = lstart[(long)seg * (OB_SEG + 1) + j];
-}
-
-__device__ __forceinline__ unsigned long long ob_ld(unsigned long long *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void ob_st(unsigned long long *p, unsigned long long v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// decoupled look-back over the batches (wave 0): publish the batch's count,
-// sum the predecessors' until one has its inclusive prefix (64 at a time),
-// publish the inclusive prefix, return the exclusive one.  A predecessor holds
-// a ticket taken before this one, so it is running; one that never publishes
-// within 2 s of wall clock (a fault, not a slow batch) fails the call instead
-// of hanging it.
-__device__ long long ob_lookback(unsigned long long *status, int b, long long n, int *fail) {
-    const int lane = lane_id();
-    if (b == 0) {
-        if (lane == 0) ob_st(&status[0], OB_INC | (unsigned long long)n);
-        return 0;
-    }
-    if (lane == 0) ob_st(&status[b], OB_AGG | (unsigned long long)n);
-    long long excl = 0;
-    int j0 = b - 1;
-    while (true) {
-        const int j = j0 - lane;
-        unsigned long long st = j >= 0 ? ob_ld(&status[j]) : OB_INC;
-        const unsigned long long w0 = wall_clock64();
-        while ((st >> 62) == 0) {
-            __builtin_amdgcn_s_sleep(1);
-            st = ob_ld(&status[j]);
-            if ((st >> 62) == 0 && wall_clock64() - w0 > 200000000ull) {  // (100 MHz wall clock: 2 s)
-                atomicExch(fail, 2);
-                st = OB_INC;
-            }
-        }
-        const u64 inc = __ballot((st >> 62) == 2);
-        const long long val = (long long)(st & OB_VAL);
-        if (inc) {
-            const int nearest = __ffsll((long long)inc) - 1;  // the nearest predecessor with its inclusive prefix
-            excl += wave_sum(lane <= nearest ? val : 0ll);
-            break;
-        }
-        excl += wave_sum(val);
-        j0 -= 64;
-    }
-    if (lane == 0) ob_st(&status[b], OB_INC | (unsigned long long)(excl + n));
-    return excl;
-}
-
-struct ObArgs {
-    const int *bstart;
-    int nb, m;
-    const int4 *rinfo;     // per row: (first A entry, A entries, products, class)
-    const int2 *ebnd;      // per A entry: its B row's [start, end)
-    const double *vA;
-    const long long *E;    // per A entry: prefix of the products (class H's staging offsets)
-    const int *Bcol;
-    const double *Bval;
-    const int *Hcol;       // class H's rows: nonzeros in the staging at E[first entry],
-    const double *Hval;    //   their counts in Crp[row] (k_rows_bitmap)
-    int *Crp;
-    int *Ccol;
-    double *Cval;
-    unsigned long long *status;
-    int *ticket;
-    int *fail;
-};
-
-__global__ __launch_bounds__(OB_NT, 8) void k_rows_ob(ObArgs g) {
-    // keys: kp[0][0] / kp[0][1] in turn (kp[0][1] holds the run table until the
-    // expansion is done); values in expansion order: kp[1] as OB_SLOTS doubles
-    // (an S wave's 256-double slice: its keys and values by rank)
-    __shared__ __align__(16) u32 kp[2][2][OB_SLOTS];
-    __shared__ int rrow[OB_ROWS], ra0[OB_ROWS], rk[OB_ROWS], rP[OB_ROWS], rcl[OB_ROWS];
-    __shared__ int rrun[OB_ROWS + 1], rwv[OB_ROWS], rcnt[OB_ROWS + 1];
-    __shared__ signed char wrow[OB_NW], qrow[OB_ROWS];
-    __shared__ int wred[3][OB_NW];
-    __shared__ int s_b, s_r0, s_r1, s_n, s_nr, s_kmax, s_tot;
-    __shared__ long long s_base;
-    RP_INIT
-    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
-    // run table: each run's inclusive batch-global product prefix, B start, A value
-    int *const incl = reinterpret_cast<int *>(kp[0][1]);
-    int *const rbs = incl + OB_RUNS;
-    double *const rav = reinterpret_cast<double *>(kp[0][1]) + OB_RUNS;
-    static_assert(OB_RUNS * (4 + 4 + 8) <= OB_SLOTS * 4, "run table fits the second key buffer");
-    double *const V = reinterpret_cast<double *>(kp[1]);
-
-    // ---- the batch and its nonempty rows (in row order)
-    if (tid == 0) {
-        const int b = atomicAdd(g.ticket, 1);  // (tickets in row order: the look-back's progress)
-        s_b = b;
-        s_r0 = g.bstart[b];
-        s_r1 = g.bstart[b + 1];
-    }
-    if (tid < OB_NW) wrow[tid] = -1;
-    if (tid < OB_ROWS) qrow[tid] = -1;
-    __syncthreads();
-    RP(0);
-    const int b = s_b, r0 = s_r0, r1 = s_r1;
-    {
-        const int r = r0 + tid;
-        int4 ri = make_int4(0, 0, 0, -1);
-        if (r < r1) ri = g.rinfo[r];  // (r1 - r0 <= OB_SEG < OB_NT)
-        const bool ne = ri.w >= 0;
-        const u64 bt = __ballot(ne);
-        if (lane == 0) wred[0][wv] = __popcll(bt);
-        __syncthreads();
-        int pre = 0, tot = 0;
-#pragma unroll
-        for (int w = 0; w < OB_NW; ++w) {
-            pre += w < wv ? wred[0][w] : 0;
-            tot += wred[0][w];
-        }
-        if (ne) {
-            const int i = pre + lanes_below(bt);
-            rrow[i] = r;
-            ra0[i] = ri.x;
-            rk[i] = ri.y;
-            rP[i] = ri.z;
-            rcl[i] = ri.w;
-            if (ri.w == NCLS - 1) rcnt[i] = g.Crp[r];  // (class H: counted by k_rows_bitmap)
-        }
-        if (tid == 0) s_n = tot;
-        __syncthreads();
-    }
-    const int nrows = s_n;
-    RP(1);
-    // ---- layout (wave 0): S16 rows on quarter waves first, then the others' waves;
-    // each row's first run in the batch's run table
-    if (wv == 0) {
-        const int c = lane < nrows ? rcl[lane] : -1;
-        const bool h = c == NCLS - 1;
-        const u64 b16 = __ballot(c == 0);
-        const int nq = __popcll(b16), w0 = (nq + 3) / 4;
-        const int nwv = c > 0 && !h ? ob_waves(c) : 0;
-        const int winc = wave_incl_scan_dpp(nwv);
-        const int kk = lane < nrows && !h ? rk[lane] : 0;
-        const int kinc = wave_incl_scan_dpp(kk);
-        int kmax = 0;
-        if (lane < nrows) {
-            rrun[lane] = kinc - kk;
-            if (c == 0) {
-                const int q = lanes_below(b16);
-                rwv[lane] = q;
-                qrow[q] = (signed char)lane;
-            } else if (!h) {
-                const int f = w0 + winc - nwv;
-                rwv[lane] = f;
-                for (int w = f; w < f + nwv; ++w) wrow[w] = (signed char)lane;
-                if (c >= 2) {
-                    int np = 256;
-                    while (np < rP[lane]) np <<= 1;
-                    kmax = np;
-                }
-            }
-        }
-        kmax = wave_last(wave_incl_dpp(kmax, 0, OpMax{}));
-        if (lane == 63) {
-            rrun[nrows] = kinc;  // (lane 63's inclusive = all runs; nrows <= 64)
-            s_nr = kinc;
-            s_kmax = kmax;
-        }
-    }
-    __syncthreads();
-    const int nruns = s_nr, kmax = s_kmax;
-    RP(2);
-    // ---- run table: a thread per run; products scanned over the batch
-    {
-        int len = 0, bs = 0;
-        double av = 0.0;
-        if (tid < nruns) {
-            const int i = owner_search(rrun, nrows, tid);
-            const int a = ra0[i] + tid - rrun[i];
-            const int2 be = g.ebnd[a];
-            av = g.vA[a];
-            len = be.y - be.x;
-            bs = be.x;
-        }
-        const int inc = wave_incl_scan_dpp(len);
-        if (lane == 63) wred[0][wv] = inc;
-        __syncthreads();
-        int pre = 0;
-#pragma unroll
-        for (int w = 0; w < OB_NW; ++w) pre += w < wv ? wred[0][w] : 0;
-        if (tid < nruns) {
-            incl[tid] = pre + inc;
-            rbs[tid] = bs;
-            rav[tid] = av;
-        }
-        __syncthreads();
-    }
-    RP(3);
-    // ---- each wave's role: part of an M row's group (wave sort + cross-wave
-    // stages), an S64 row, four S16 rows, or idle
-    const bool s16w = (wv << 2) < OB_ROWS && qrow[wv << 2] >= 0;
-    const int mi = s16w ? -1 : wrow[wv];  // (M or S64 row)
-    const int mc = mi >= 0 ? rcl[mi] : -1;
-    const bool mrow = mc >= 2;
-    const int g0 = mi >= 0 ? rwv[mi] : 0;
-    const int P = mi >= 0 ? rP[mi] : 0;
-    int npow = 256;
-    while (npow < P) npow <<= 1;
-    const int IB = 31 - __builtin_clz(npow);
-    const int ew = (wv - g0) << 8, er = ew + 4 * lane;  // (M) the wave's / this lane's first position in the row
-    // M: the lane's four positions -> column, a*b (values to V in expansion order)
-    int c[4] = {0, 0, 0, 0};
-    int clo = INT_MAX, chi = -1;
-    // S: one product per lane (S64: the wave's row; S16: the 16-lane group's row)
-    const int G = s16w ? 16 : 64, sl = lane & (G - 1), gb = lane - sl;
-    const int si = s16w ? qrow[(wv << 2) + (lane >> 4)] : (mc == 1 ? mi : -1);
-    const int SP = si >= 0 ? rP[si] : 0;
-    int scol = 0;
-    double sx = 0.0;
-    if (mrow) {
-        const int ne = max(0, min(4, P - er));
-        if (ne > 0) {
-            const int f = rrun[mi], l = f + rk[mi];
-            const int q0 = (f ? incl[f - 1] : 0) + er;  // batch-global product index of position er
-            int j = lower_bound_dev(incl, f, l, q0 + 1);  // the run holding it: first inclusive prefix past it
-            int pa[4];
-            double ra[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (u < ne) {
-                    while (incl[j] <= q0 + u) ++j;
-                    pa[u] = rbs[j] + q0 + u - (j ? incl[j - 1] : 0);
-                    ra[u] = rav[j];
-                }
-            double bv[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (u < ne) {
-                    c[u] = g.Bcol[pa[u]];
-                    bv[u] = g.Bval[pa[u]];
-                }
-            double xv[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                xv[u] = u < ne ? ra[u] * bv[u] : 0.0;
-                if (u < ne) {
-                    clo = min(clo, c[u]);
-                    chi = max(chi, c[u]);
-                }
-            }
-            reinterpret_cast<double4 *>(V + (g0 << 8))[er >> 2] = make_double4(xv[0], xv[1], xv[2], xv[3]);
-        }
-        clo = wave_last(wave_incl_dpp(clo, INT_MAX, OpMin{}));
-        chi = wave_last(wave_incl_dpp(chi, INT_MIN, OpMax{}));
-        if (lane == 0) {
-            wred[0][wv] = clo;
-            wred[1][wv] = chi;
-        }
-    } else if (si >= 0 && sl < SP) {
-        const int f = rrun[si], l = f + rk[si];
-        const int q = (f ? incl[f - 1] : 0) + sl;
-        const int j = lower_bound_dev(incl, f, l, q + 1);
-        const int pa = rbs[j] + q - (j ? incl[j - 1] : 0);
-        const double ra = rav[j];
-        scol = g.Bcol[pa];
-        sx = ra * g.Bval[pa];
-    }
-    __syncthreads();  // (the run table is read; the groups' column spans are in wred)
-    RP(4);
-    // ---- sorts
-    u32 x[4] = {~0u, ~0u, ~0u, ~0u};
-    const bool mact = mrow && ew < npow;  // (wave-uniform: a wave of the row's sort)
-    if (mrow) {
-        const int gw = ob_waves(mc);
-        clo = INT_MAX;
-        chi = -1;
-        for (int w = g0; w < g0 + gw; ++w) {
-            clo = min(clo, wred[0][w]);
-            chi = max(chi, wred[1][w]);
-        }
-        // (B's columns span < 2^20 - 1 on this path: every row's keys pack into
-        // (column - clo, position) with position bits IB <= 12)
-        if ((u32)(chi - clo) >= (1u << (32 - IB)) - 1u && lane == 0 && P > 0) atomicExch(g.fail, 3);
-        const int ne = max(0, min(4, P - er));
-#pragma unroll
-        for (int u = 0; u < 4; ++u) x[u] = u < ne ? ((u32)(c[u] - clo) << IB) | (u32)(er + u) : ~0u;
-        if (ew < P) wave_sort256(x, lane);  // (wave-uniform)
-        if (mact) *reinterpret_cast<uint4 *>(kp[0][0] + (g0 << 8) + er) = make_uint4(x[0], x[1], x[2], x[3]);
-    }
-    // S rows: ranks by counting the group's smaller (column, lane) keys; keys
-    // and values by rank into the wave's slice of kp[1]
-    u64 *const sk = reinterpret_cast<u64 *>(V + (wv << 8));
-    double *const sv = V + (wv << 8) + 64;
-    bool shead = false;
-    double ssum = 0.0;
-    int sord = 0, scnt = 0;
-    if (si >= 0 || s16w) {
-        const u64 key = sl < SP ? ((u64)(u32)scol << 32) | (u32)sl : ~0ull;
-        const u32 khi = (u32)(key >> 32), klo = (u32)key;
-        int rank = 0;
-        if (!s16w) {  // (S64: one row per wave, SP wave-uniform)
-            for (int f = 0; f < SP; ++f) {
-                const u64 kf = ((u64)(u32)__builtin_amdgcn_readlane((int)khi, f) << 32) |
-                               (u32)__builtin_amdgcn_readlane((int)klo, f);
-                rank += kf < key;
-            }
-        } else {
-#pragma unroll
-            for (int f = 0; f < 16; ++f) {
-                const u64 kf = ((u64)(u32)__shfl((int)khi, f, 16) << 32) | (u32)__shfl((int)klo, f, 16);
-                rank += kf < key;  // (lanes past SP hold ~0: never below a product)
-            }
-        }
-        if (sl < SP) {
-            sk[gb + rank] = key;
-            sv[gb + rank] = sx;
-        }
-        wave_lds_sync();
-        int col = -1;
-        if (sl < SP) {
-            col = key_col(sk[gb + sl]);
-            shead = sl == 0 || key_col(sk[gb + sl - 1]) != col;
-        }
-        const u64 gm = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << gb;
-        const u64 hb = __ballot(shead) & gm;
-        if (shead) {
-            ssum = sv[gb + sl];
-            for (int j = sl + 1; j < SP && key_col(sk[gb + j]) == col; ++j) ssum += sv[gb + j];
-            scol = col;
-        }
-        sord = (int)lanes_below(hb);
-        scnt = __popcll(hb);
-        if (si >= 0 && sl == 0) rcnt[si] = scnt;
-    }
-    __syncthreads();
-    RP(5);
-    // ---- the M rows' cross-wave bitonic stages (every wave runs the loop: one
-    // barrier per stage; only the rows' sort groups work)
-    int src = 0;
-    for (int K = 512; K <= kmax; K <<= 1) {
-        const bool act = mact && npow >= K;
-        auto cmpx = [&](const uint4 y, bool rev, bool keep_min) {
-            const u32 yy[4] = {rev ? y.w : y.x, rev ? y.z : y.y, rev ? y.y : y.z, rev ? y.x : y.w};
-#pragma unroll
-            for (int u = 0; u < 4; ++u) x[u] = keep_min ? min(x[u], yy[u]) : max(x[u], yy[u]);
-        };
-        u32 *const kb0 = kp[0][0] + (g0 << 8), *const kb1 = kp[0][1] + (g0 << 8);
-        if (act) cmpx(*reinterpret_cast<const uint4 *>((src ? kb1 : kb0) + (er ^ (K - 4))), true, (er & (K >> 1)) == 0);
-        for (int J = K >> 2; J >= 256; J >>= 1) {
-            if (act) {
-                src ^= 1;
-                *reinterpret_cast<uint4 *>((src ? kb1 : kb0) + er) = make_uint4(x[0], x[1], x[2], x[3]);
-            }
-            __syncthreads();
-            if (act) cmpx(*reinterpret_cast<const uint4 *>((src ? kb1 : kb0) + (er ^ J)), false, (er & J) == 0);
-        }
-        if (act) {
-            bitonic_merge<256, 128>(x, lane);
-            src ^= 1;
-            *reinterpret_cast<uint4 *>((src ? kb1 : kb0) + er) = make_uint4(x[0], x[1], x[2], x[3]);
-        }
-        __syncthreads();
-    }
-    RP(6);
-    // ---- M rows: heads, sums (in the sorted order: deterministic), the row's count
-    u32 hd = 0;
-    double xs[4] = {0.0, 0.0, 0.0, 0.0};
-    int mo = 0;
-    if (mrow) {
-        const u32 *const skm = (src ? kp[0][1] : kp[0][0]) + (g0 << 8);
-        const double *const Vg = V + (g0 << 8);
-        const int np = max(0, min(4, P - er));
-        const u32 prev = er > 0 && np > 0 ? skm[er - 1] : ~0u;
-        const u32 pm = (u32)npow - 1u;
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (u < np) {
-                xs[u] = Vg[x[u] & pm];
-                const u32 pk = u ? x[u - 1] : prev;
-                hd |= (er + u == 0 || (x[u] >> IB) != (pk >> IB)) ? 1u << u : 0u;
-            }
-        // sums over each head's equal columns, ascending (the later positions of
-        // a column continuing past this lane's four read from LDS)
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (hd >> u & 1u) {
-                const u32 col = x[u] >> IB;
-                double sum = xs[u];
-                int j = u + 1;
-#pragma unroll
-                for (int v = u + 1; v < 4; ++v)
-                    if (j == v && v < np && (x[v] >> IB) == col) {
-                        sum += xs[v];
-                        ++j;
-                    }
-                if (j == 4)
-                    for (int q = er + 4; q < P && (skm[q] >> IB) == col; ++q) sum += Vg[skm[q] & pm];
-                xs[u] = sum;
-            }
-        const int nh = __popc(hd);
-        const int inc = wave_incl_scan_dpp(nh);
-        if (lane == 63) wred[2][wv] = inc;
-        mo = inc - nh;
-    }
-    __syncthreads();
-    if (mrow) {  // the row's count and this lane's first output: the group's wave totals
-        const int gw = ob_waves(mc);
-        int tot = 0;
-        for (int w = g0; w < g0 + gw; ++w) {
-            mo += w < wv ? wred[2][w] : 0;
-            tot += wred[2][w];
-        }
-        if (wv == g0 && lane == 0) rcnt[mi] = tot;
-    }
-    __syncthreads();
-    RP(7);
-    // ---- the batch's count, its offset in C (wave 0: scan of the row counts, look-back)
-    if (wv == 0) {
-        const int v = lane < nrows ? rcnt[lane] : 0;
-        const int inc = wave_incl_scan_dpp(v);
-        if (lane < nrows) rcnt[lane] = inc - v;
-        const int tot = wave_last(inc);
-#ifdef TSG_OB_NOWAIT
-        const long long base = 0;  // (timing experiment only: no look-back, wrong output)
-#else
-        const long long base = ob_lookback(g.status, b, tot, g.fail);
-#endif
-        if (lane == 0) {
-            s_base = base;
-            s_tot = tot;
-            rcnt[nrows] = tot;
-        }
-    }
-    __syncthreads();
-    RP(8);
-    const long long base = s_base;
-    // ---- the nonzeros straight into C
-    if (mrow) {
-        long long o = base + rcnt[mi] + mo;
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (hd >> u & 1u) {
-                g.Ccol[o] = (int)(x[u] >> IB) + clo;
-                g.Cval[o] = xs[u];
-                ++o;
-            }
-    } else if (shead) {
-        const long long o = base + rcnt[si] + sord;
-        g.Ccol[o] = scol;
-        g.Cval[o] = ssum;
-    }
-    if (nrows == 1 && rcl[0] == NCLS - 1) {  // a class-H row: its nonzeros from the staging
-        const long long src0 = g.E[ra0[0]];
-        const int n = s_tot;
-        for (int i = tid; i < n; i += OB_NT) {
-            g.Ccol[base + i] = __builtin_nontemporal_load(g.Hcol + src0 + i);
-            g.Cval[base + i] = __builtin_nontemporal_load(g.Hval + src0 + i);
-        }
-    }
-    // row pointers of every row of the batch (empty rows: the next nonempty row's offset)
-    for (int r = r0 + tid; r < r1; r += OB_NT) {
-        const int j = lower_bound_dev(rrow, 0, nrows, r);
-        g.Crp[r] = (int)(base + rcnt[j]);
-    }
-    if (b == g.nb - 1 && tid == 0) g.Crp[g.m] = (int)(base + s_tot);
-    RP(9);
-    RP_DONE(1);
-}
-
 // Setup (stream-ordered, no host round trip): the entry table, its scan and the
 // classes; counts and statistics land in cx.pinned64[0..7) once the stream is synced.
 int dev_rows_setup_async(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPlan &p, hipStream_t s) {
@@ -2748,16 +1939,6 @@ int dev_rows_setup_async(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B
     // rows' scratch products (u64) [24..26) and its cursor [26..28)
     TSG_TRY(cx.get(&p.cls, 32));
     TSG_TRY(cx.get(&p.rowpointer, (size_t)m + 1));
-    // the ordered batches' tables (B narrow enough for their packed keys)
-    p.ob_prep = m > 0 && (long long)B.n <= kObMaxCols;
-    if (p.ob_prep) {
-        p.nseg = (m + OB_SEG - 1) / OB_SEG;
-        TSG_TRY(cx.get(&p.rinfo, (size_t)m));
-        TSG_TRY(cx.get(&p.rcls, (size_t)m));
-        TSG_TRY(cx.get(&p.lstart, (size_t)p.nseg * (OB_SEG + 1)));
-        TSG_TRY(cx.get(&p.nbs, (size_t)p.nseg + 1));
-        TSG_TRY(cx.get(&p.bstart, (size_t)m + p.nseg + 1));
-    }
     unsigned long long *hst = reinterpret_cast<unsigned long long *>(p.cls + 8);
     k_rows_entries<<<grid_for((long)A.nnz + 1, WG, 16384), WG, 0, s>>>(A.columnindex, A.nnz, B.rowpointer, p.ebnd,
                                                                       p.E, p.cls);
@@ -2765,18 +1946,9 @@ int dev_rows_setup_async(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B
     TSG_TRY(scan_exclusive_i64(cx, p.E, (long)A.nnz + 1, s));
     // (one workgroup at least: it writes the statistics and rowpointer[m])
     k_rows_bin<<<max(1, (m + BIN_ROWS - 1) / BIN_ROWS), WG, 0, s>>>(A.rowpointer, m, p.E, p.E + A.nnz, p.rowpointer,
-                                                                    p.lists, p.cls, p.soff, hst, p.rinfo, p.rcls);
+                                                                    p.lists, p.cls, p.soff, hst);
     TSG_HIP(hipGetLastError());
-    if (p.ob_prep) {  // batches packed per segment, concatenated; their number -> cls[28]
-        k_rows_obpack<<<(p.nseg + WAVES - 1) / WAVES, WG, 0, s>>>(p.rcls, m, p.nseg, p.lstart, p.nbs);
-        TSG_HIP(hipGetLastError());
-        TSG_HIP(hipMemsetAsync(p.nbs + p.nseg, 0, sizeof(int), s));
-        TSG_TRY(scan_exclusive_i32(cx, p.nbs, (long)p.nseg + 1, s));
-        k_rows_obgather<<<(p.nseg + 1 + WAVES - 1) / WAVES, WG, 0, s>>>(p.lstart, p.nbs, p.nseg, m, p.bstart,
-                                                                        p.cls + 28);
-        TSG_HIP(hipGetLastError());
-    }
-    TSG_HIP(hipMemcpyAsync(cx.pinned64, p.cls, 30 * sizeof(int), hipMemcpyDeviceToHost, s));
+    TSG_HIP(hipMemcpyAsync(cx.pinned64, p.cls, 26 * sizeof(int), hipMemcpyDeviceToHost, s));
     return TSG_OK;
 }
 
@@ -2788,97 +1960,19 @@ void dev_rows_setup_read(Context &cx, RowsPlan &p) {
     p.hubprod = cx.pinned64[7];
     p.hk = cx.pinned64[8];
     p.hbig = cx.pinned64[12];
-    p.nb = p.ob_prep ? reinterpret_cast<const int *>(cx.pinned64)[28] : 0;
 }
 
-// routing: every product whose B rows are column-sorted (class H's rows take
-// the one-walk bitmap, dominant-run or windowed kernels)
-bool dev_rows_accept(const RowsPlan &p) {
-    (void)p;
-    return true;
-}
+// routing: every product whose B rows are strictly column-sorted (class H's
+// rows take the one-walk bitmap, dominant-run or windowed kernels) -- unless a
+// row holds more than 2^31 - 1 products (the class-H kernels count a row's
+// products in int): such products go to the staged tile pipeline instead of
+// failing (a forced TSG_PATH=rows still returns TSG_ERR_UNSUPPORTED for them)
+bool dev_rows_accept(const RowsPlan &p) { return p.pmax <= 0x7fffffffLL; }
 
 void dev_rows_release(Context &cx, RowsPlan &p) {
-    void *ps[] = {p.ebnd, p.E, p.lists, p.soff, p.cls, p.rowpointer, p.rinfo, p.rcls, p.lstart, p.nbs, p.bstart};
+    void *ps[] = {p.ebnd, p.E, p.lists, p.soff, p.cls, p.rowpointer};
     for (void *q : ps) cx.put(q);
     p = RowsPlan{};
-}
-
-// the ordered-batch route of dev_rows_run (C.rowpointer taken from the plan):
-// class H's rows into the staging (k_rows_bitmap, their counts in C's row
-// pointers), then every batch in row order, C written once (k_rows_ob)
-static int dev_rows_run_ob(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPlan &p, tsg_dev_csr &C,
-                           tsg_stats *st, hipStream_t s, hipEvent_t *ev) {
-    const int m = A.m;
-    const long long products = p.products;
-    int *Scol = nullptr, *Oc = nullptr, *Or = nullptr;
-    double *Sval = nullptr, *Ox = nullptr;
-    unsigned long long *status = nullptr;
-    if (p.ncls[7] > 0) {
-        TSG_TRY(cx.get(&Scol, (size_t)products + 1));
-        TSG_TRY(cx.get(&Sval, (size_t)products + 1));
-        if (p.hbig > 0) {  // one-walk rows past OW_CH products: their scratch
-            TSG_TRY(cx.get(&Oc, (size_t)p.hbig));
-            TSG_TRY(cx.get(&Ox, (size_t)p.hbig));
-            TSG_TRY(cx.get(&Or, (size_t)p.hbig));
-        }
-    }
-    TSG_TRY(cx.get(&C.columnindex, (size_t)products + 1));
-    TSG_TRY(cx.get(&C.value, (size_t)products + 1));
-    TSG_TRY(cx.get(&status, (size_t)p.nb));
-    TSG_HIP(hipMemsetAsync(status, 0, (size_t)p.nb * sizeof(unsigned long long), s));
-    if (ev) TSG_HIP(hipEventRecord(ev[1], s));
-    if (ev) TSG_HIP(hipEventRecord(ev[4], s));
-#ifdef TSG_ROWS_PROF
-    unsigned long long *dprof = nullptr;
-    TSG_HIP(hipGetSymbolAddress((void **)&dprof, HIP_SYMBOL(g_rows_prof)));
-    TSG_HIP(hipMemsetAsync(dprof, 0, sizeof(unsigned long long) * 3 * 256 * 12, s));
-#endif
-    if (p.ncls[7] > 0) {
-        RowsArgs g{A.rowpointer, A.value, p.ebnd, p.E, B.columnindex, B.value, p.lists + (long)(NCLS - 1) * m,
-                   p.ncls[7], C.rowpointer, Scol, Sval, nullptr};
-        if (p.ncls[7] >= 2 && p.ncls[7] <= OH_MAX) {
-            k_rows_order_h<<<1, OH_NT, 0, s>>>(p.E, p.cls, p.lists + (long)(NCLS - 1) * m);
-            TSG_HIP(hipGetLastError());
-        }
-        k_rows_bitmap<<<p.ncls[7], RH_NT, 0, s>>>(g, Oc, Ox, Or, reinterpret_cast<unsigned long long *>(p.cls + 26));
-        TSG_HIP(hipGetLastError());
-    }
-    ObArgs og{p.bstart, p.nb, m, p.rinfo, p.ebnd, A.value, p.E, B.columnindex, B.value, Scol, Sval,
-              C.rowpointer, C.columnindex, C.value, status, p.cls + 29, p.cls + 30};
-    k_rows_ob<<<p.nb, OB_NT, 0, s>>>(og);
-    TSG_HIP(hipGetLastError());
-    if (ev) TSG_HIP(hipEventRecord(ev[5], s));
-    int *const pn = reinterpret_cast<int *>(cx.pinned64 + 15);
-    TSG_HIP(hipMemcpyAsync(pn, C.rowpointer + m, sizeof(int), hipMemcpyDeviceToHost, s));
-    TSG_HIP(hipMemcpyAsync(pn + 1, p.cls + 30, sizeof(int), hipMemcpyDeviceToHost, s));
-    if (ev) TSG_HIP(hipEventRecord(ev[3], s));
-    TSG_TRY(stream_wait(s));
-    const int fail = pn[1];
-    C.nnz = pn[0];
-#ifdef TSG_ROWS_PROF
-    {
-        static unsigned long long raw[3 * 256 * 12];
-        unsigned long long pr[12] = {};
-        TSG_HIP(hipMemcpy(raw, dprof, sizeof(raw), hipMemcpyDeviceToHost));
-        for (int b = 0; b < 256; ++b)
-            for (int k = 0; k < 12; ++k) pr[k] += raw[(256 + b) * 12 + k];
-        fprintf(stderr, "ob (%d batches) us/batch:", p.nb);
-        for (int k = 0; k < 10; ++k) fprintf(stderr, " %.2f", pr[k] / 100.0 / p.nb);
-        fprintf(stderr, "\n");
-    }
-#endif
-    void *ws[] = {Scol, Sval, Oc, Ox, Or, status};
-    for (void *q : ws) cx.put(q);
-    dev_rows_release(cx, p);
-    // a look-back that never resolved (2) or a row span past the packed keys (3): never expected
-    if (fail != 0) return TSG_ERR_HIP;
-    if (st) {
-        st->nnzC = C.nnz;
-        st->tile_products = products;
-        st->numblkC = -1;
-    }
-    return TSG_OK;
 }
 
 // CSR in -> CSR out from a setup (B's rows column-sorted; the caller checked);
@@ -2897,30 +1991,19 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
     C.n = B.n;
     C.rowpointer = p.rowpointer;
     p.rowpointer = nullptr;  // (now C's)
-#ifndef TSG_NO_OB
-    if (p.ob_prep && p.nb > 0 && p.hubprod == 0 && p.hk == 0 && p.products <= 0x7fffffffLL &&
-        p.products * 12 <= kRowsProductSizedC)
-        return dev_rows_run_ob(cx, A, B, p, C, st, s, ev);
-#endif
     int2 *ebnd = p.ebnd;
     long long *E = p.E, *soff = p.soff;
     int4 *lists = p.lists;
     const long long products = p.products;
     int ncls[NCLS];
     for (int t = 0; t < NCLS; ++t) ncls[t] = p.ncls[t];
-    // TSG_ROWS_DIRECT=1: exact row counts first (k_rows_count*), the classes
-    // S16..M4 write C in place, only class H's rows go through the staging (and
-    // a copy): no products-sized staging for the other rows (less device
-    // memory), but on webbase the count kernels (318 us, latency-bound: three
-    // dependent loads per row) cost more than the compaction they save (e2e
-    // 1.40 vs 1.30 ms), so the default stages every row and compacts.
-    const bool direct = getenv("TSG_ROWS_DIRECT") && atoi(getenv("TSG_ROWS_DIRECT")) != 0;
+    // (exact row counts first, so that the classes write C in place, measured
+    // slower on webbase in round 3: the count kernels took 318 us against the
+    // 300 us compaction they save; the staging + compaction stays)
     int *Scol = nullptr;
     double *Sval = nullptr;
-    if (!direct || ncls[7] > 0) {
-        TSG_TRY(cx.get(&Scol, (size_t)products + 1));
-        TSG_TRY(cx.get(&Sval, (size_t)products + 1));
-    }
+    TSG_TRY(cx.get(&Scol, (size_t)products + 1));
+    TSG_TRY(cx.get(&Sval, (size_t)products + 1));
     if (ev) TSG_HIP(hipEventRecord(ev[1], s));
     if (ev) TSG_HIP(hipEventRecord(ev[4], s));
 #ifdef TSG_ROWS_PROF
@@ -2951,7 +2034,7 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
         return TSG_OK;
     };
     // the merge classes are persistent: one resident wave of workgroups
-    if (ncls[7] >= 2 && ncls[7] <= OH_MAX && !getenv("TSG_ROWS_H_ROWORDER")) {
+    if (ncls[7] >= 2 && ncls[7] <= OH_MAX) {
         k_rows_order_h<<<1, OH_NT, 0, s>>>(E, p.cls, lists + (long)(NCLS - 1) * m);
         TSG_HIP(hipGetLastError());
     }
@@ -2992,9 +2075,8 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
             TSG_TRY(cx.get(&wmat, (size_t)n7 + 1));
             TSG_TRY(cx.get(&wst, 4));
             TSG_HIP(hipMemsetAsync(wst, 0, 4 * sizeof(unsigned long long), s));
-            // products per unit, the target of each row's window width (TSG_W_UNIT)
-            const long long wunit = getenv("TSG_W_UNIT") ? atoll(getenv("TSG_W_UNIT")) : W_UNIT;
-            k_rows_wplan<<<n7, W_NT, 0, s>>>(g, B.n, wunit > 0 ? wunit : W_UNIT, wnw, wnch, wlo, wwb, wpre, wmat,
+            // (W_UNIT products per unit: 4,096 measured equal, 16,384 / 32,768 slower)
+            k_rows_wplan<<<n7, W_NT, 0, s>>>(g, B.n, W_UNIT, wnw, wnch, wlo, wwb, wpre, wmat,
                                              wst, soff);
             TSG_HIP(hipGetLastError());
             TSG_HIP(hipMemsetAsync(wnw + n7, 0, sizeof(int), s));
@@ -3032,19 +2114,15 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
             TSG_TRY(cx.get(&Wc, (size_t)wprod + 1));
             TSG_TRY(cx.get(&Wv, (size_t)wprod + 1));
             TSG_HIP(hipMemsetAsync(ucnt, 0, (size_t)nu * sizeof(int), s));
-            // TSG_W_SCATTER=1: the scatter bins each sub-batch by window in LDS
-            // before its stores (measured the same as the direct stores on the
-            // LiveJournal block: 2.744 vs 2.746 ms); TSG_W_RUNMAP=0: binary
-            // searches of the run table instead of the run map (3.25 vs 2.75 ms)
-            const int binned = getenv("TSG_W_SCATTER") && atoi(getenv("TSG_W_SCATTER")) != 0;
-            const int runmap = !getenv("TSG_W_RUNMAP") || atoi(getenv("TSG_W_RUNMAP")) != 0;
+            // (the run map of each walk step, not a binary search of the run table
+            // per product: 2.75 vs 3.25 ms on the LiveJournal block)
             k_rows_wchunks<<<n7, WG, 0, s>>>(g, ubase, cbase, wmat, wchunks, cmoff, umap);
             TSG_HIP(hipGetLastError());
-            k_rows_wcount<<<nc, W_NT, 0, s>>>(g, wchunks, cmoff, wlo, wwb, ubase, ucnt, cbo, runmap);
+            k_rows_wcount<<<nc, W_NT, 0, s>>>(g, wchunks, cmoff, wlo, wwb, ubase, ucnt, cbo);
             TSG_HIP(hipGetLastError());
             k_rows_wscan<<<n7, W_NT, 0, s>>>(g, ubase, ucnt, ubo, nullptr);
             TSG_HIP(hipGetLastError());
-            k_rows_wscatter<<<nc, W_NT, 0, s>>>(g, wchunks, cmoff, wlo, wwb, ubase, ubo, cbo, binned, runmap);
+            k_rows_wscatter<<<nc, W_NT, 0, s>>>(g, wchunks, cmoff, wlo, wwb, ubase, ubo, cbo);
             TSG_HIP(hipGetLastError());
             k_rows_wunit<<<nu, W_NT, 0, s>>>(g, umap, ubase, wlo, wwb, wpre, ucnt, ubo, ucount, Wc, Wv);
             TSG_HIP(hipGetLastError());
@@ -3127,28 +2205,7 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
         return TSG_OK;
     };
     int *cfirst = nullptr;
-    if (direct) {
-        // the classes' exact counts (class H's came with its rows, in the staging)
-        TSG_TRY(launch(6, k_rows_count<M4_NT, M4_CAP, M4_RUNS>, ncls[6], M4_NT, s));
-        TSG_TRY(launch(5, k_rows_count<M3_NT, M3_CAP, M3_RUNS>, ncls[5], M3_NT, s));
-        TSG_TRY(launch(4, k_rows_count<M2_NT, M2_CAP, M2_RUNS>, ncls[4], M2_NT, s));
-        TSG_TRY(launch(3, k_rows_count<M1_NT, M1_CAP, M1_RUNS>, ncls[3], M1_NT, s));
-        TSG_TRY(launch(2, k_rows_count<M0_NT, M0_CAP, M0_RUNS>, ncls[2], M0_NT, s));
-        TSG_TRY(launch(1, k_rows_count_small<64>, (ncls[1] + WAVES - 1) / WAVES, WG, s));
-        TSG_TRY(launch(0, k_rows_count_small<16>, (ncls[0] + 4 * WAVES - 1) / (4 * WAVES), WG, s));
-        TSG_TRY(scan_alloc());
-        TSG_TRY(wgather());
-        g.Crp = C.rowpointer;
-        g.Scol = C.columnindex;
-        g.Sval = C.value;
-        TSG_TRY(classes());
-        if (ncls[7] > 0) {
-            k_rows_hcopy<<<min(ncls[7], 8192), WG, 0, s>>>(lists + (long)7 * m, ncls[7], soff, C.rowpointer, Scol,
-                                                           Sval, C.columnindex, C.value);
-            TSG_HIP(hipGetLastError());
-        }
-        if (ev) TSG_HIP(hipEventRecord(ev[5], s));
-    } else {
+    {
         TSG_TRY(classes());
         // (the numeric phase: to the class kernels' end, or -- with windowed or
         // dominant-run rows, whose nonzeros go straight into C after the row

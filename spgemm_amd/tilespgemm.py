@@ -26,7 +26,7 @@ from ._lib import SMatrix, Stats, check, lib
 _CSR_FIELDS = ("rowpointer", "columnindex", "value")
 
 # stats["path"]: the CSR-in -> CSR-out route that ran (include/tsg.h TSG_PATH_*)
-PATH_TILES, PATH_FUSED, PATH_BAND, PATH_ROWS = 0, 1, 2, 3
+PATH_TILES, PATH_BAND, PATH_ROWS = 0, 2, 3  # (1: the retired fused path)
 
 
 def _view(ptr, n, dt):

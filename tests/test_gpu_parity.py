@@ -259,7 +259,7 @@ def test_step2_modes_match_oracle(mode, case, monkeypatch):
     elif case == "rand_dense":
         m, n, rp, ci, vv = synth.random_csr(600, 600, density=0.2, seed=22)
     elif case == "banded":
-        m, n, rp, ci, vv = synth.cant(n=3000, half_band=40)
+        m, n, rp, ci, vv = synth.cant(dims=(4, 4, 63))
     elif case == "rect_aat":
         m, n, rp, ci, vv = synth.random_csr(700, 2500, density=0.004, seed=23)
     else:

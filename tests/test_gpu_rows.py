@@ -209,8 +209,7 @@ def test_default_routing_hub_rows_windowed(monkeypatch):
 
 def test_default_routing_short_rows_row_merge(monkeypatch):
     """Short C rows (a 100-entry A row over 1-entry B rows, beside a 40-entry B
-    row that no long A row selects) take the row-merge path by default (the
-    fused path only when forced)."""
+    row that no long A row selects) take the row-merge path by default."""
     monkeypatch.delenv("TSG_PATH", raising=False)
     n = 200
     brows = [np.array([(3 * j) % n]) for j in range(n)]
@@ -300,12 +299,10 @@ def test_rows_mawi_prefix_hub_rows():
     _check((r, n, rp[:r + 1].copy(), ci[:rp[r]].copy(), vv[:rp[r]].copy()), (m, n, rp, ci, vv), real=True, seed=47)
 
 
-def test_default_routing_wide_b_skips_fused(monkeypatch):
-    """Short C rows (the fused path's kind) with B wider than its segment keys
-    hold (B.n >= 2^28 - 16): the default route must not send them to the fused
-    path (which is UNSUPPORTED there) but to the row-merge path.  Checked
-    against a per-row numpy product (the oracle's dense row accumulator would
-    need B.n doubles per thread)."""
+def test_default_routing_very_wide_b(monkeypatch):
+    """Short C rows with B wider than 2^28 columns take the row-merge path by
+    default (unpacked keys).  Checked against a per-row numpy product (the
+    oracle's dense row accumulator would need B.n doubles per thread)."""
     monkeypatch.delenv("TSG_PATH", raising=False)
     rng = np.random.default_rng(51)
     n = (1 << 28) + 1000
@@ -398,26 +395,19 @@ def test_rows_class_h_one_walk_rows():
     _check(A, Bc, real=True, seed=9)
 
 
-def test_rows_direct_output_mode(monkeypatch):
-    """TSG_ROWS_DIRECT=1: exact row counts (LDS hash sets, k_rows_count*) before
-    the classes, which then write C at its final offsets; class H rows through
-    the staging and k_rows_hcopy.  Every class (webbase), real values, edge
-    cases, duplicate runs."""
-    monkeypatch.setenv("TSG_ROWS_DIRECT", "1")
-    m, n, rp, ci, vv = synth.GENERATORS["webbase"]()
-    assert all((_classes(m, n, rp, ci, rp) == c).any() for c in range(H + 1))
-    _check((m, n, rp, ci, vv), real=True, seed=21)
-    test_rows_random_mixed_classes_real_values()
-    test_rows_edge_cases()
-    test_rows_duplicate_runs_sum()
-    _check(synth.GENERATORS["mc2depi"](), aat=True)
-
-
-@pytest.mark.parametrize("opt", ["TSG_W_SCATTER=1", "TSG_W_RUNMAP=0"])
-def test_rows_windowed_kernel_options(monkeypatch, opt):
-    """The windowed kernels' non-default options (the LDS-binned scatter; run
-    table binary searches instead of the run map) on the hub-row cases."""
-    k, v = opt.split("=")
-    monkeypatch.setenv(k, v)
-    test_rows_hub_rows_windowed_and_dominant_run()
-    test_default_routing_hub_rows_windowed(monkeypatch)
+def test_repeated_column_in_b_row_routes_to_tiles(monkeypatch):
+    """A B row that repeats a column (here a long hub row, the dominant-run
+    kind) is not strictly column-sorted: the sortedness check flags it and the
+    default route sends the product to the staged tile pipeline, whose C sums
+    the repeated column's products like the oracle (the dominant-run kernels
+    copy a run as it stands and would emit the column twice)."""
+    monkeypatch.delenv("TSG_PATH", raising=False)
+    rng = np.random.default_rng(61)
+    n = 5000
+    hub = np.sort(rng.choice(n, size=3000, replace=False))
+    hub = np.sort(np.concatenate([hub, hub[1500:1501]]))  # one column twice, adjacent
+    brows = [hub] + [np.sort(rng.choice(n, size=int(rng.integers(1, 8)), replace=False)) for _ in range(n - 1)]
+    B = _csr(n, n, brows)
+    arows = [np.sort(np.concatenate([[0], rng.choice(np.arange(1, n), size=3, replace=False)])) for _ in range(40)]
+    A = _csr(40, n, arows)
+    _check(A, B, real=True, seed=62, path=T.PATH_TILES)

@@ -33,6 +33,14 @@ def counters(d, counter):
     return acc
 
 
+def bench_line(log):
+    if os.path.exists(log):
+        for line in open(log):
+            if line.startswith("{\"metric\""):
+                return line
+    return None
+
+
 def main():
     src, tag = sys.argv[1], sys.argv[2]
     prof = os.path.join(REPO, "profiles")
@@ -80,24 +88,34 @@ def main():
                                       "median over the calls after the first"}
     fetch = counters(os.path.join(src, "pmc_fetch"), "FETCH_SIZE")
     write = counters(os.path.join(src, "pmc_write"), "WRITE_SIZE")
+    tot_f = tot_w = 0.0
     for k in sorted(set(dur) | set(fetch) | set(write)):
         f, w = fetch.get(k, []), write.get(k, [])
         out[k] = {
-            "dispatches": len(dur.get(k, [])),
+            "dispatches": len(dur.get(k, [])) or len(f),
             "avg_us": round(sum(dur[k]) / len(dur[k]), 2) if dur.get(k) else None,
             "fetch_bytes_per_dispatch": round(2.0 * sum(f) / len(f)) if f else None,
             "write_bytes_per_dispatch": round(sum(w) / len(w)) if w else None,
         }
+        tot_f += 2.0 * sum(f)
+        tot_w += sum(w)
         if f and w:
             out[k]["hbm_bytes_per_dispatch"] = out[k]["fetch_bytes_per_dispatch"] + out[k]["write_bytes_per_dispatch"]
+    calls = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+    if calls and (tot_f or tot_w):
+        # every kernel of the pass (the whole device pass), per call: the dispatches of
+        # the PMC runs summed, over the calls each run makes (warmup + steps)
+        out["_per_call"] = {"calls": calls, "hbm_bytes": round((tot_f + tot_w) / calls),
+                            "fetch_bytes": round(tot_f / calls), "write_bytes": round(tot_w / calls),
+                            "note": "all kernels of one call: 2*FETCH_SIZE + WRITE_SIZE summed over the "
+                                    "PMC runs' dispatches / calls per run"}
+    line = bench_line(os.path.join(src, "stats.log")) or bench_line(os.path.join(src, "pmc_fetch.log"))
+    if line:
+        out["_workload"] = json.loads(line)["config"]["workload"]
     json.dump(out, open(os.path.join(prof, f"{tag}_pmc.json"), "w"), indent=1, sort_keys=True)
-    log = os.path.join(src, "stats.log")
-    if os.path.exists(log):
-        for line in open(log):
-            if line.startswith("{\"metric\""):
-                open(os.path.join(prof, f"{tag}_bench.json"), "w").write(line)
-                out["_workload"] = json.loads(line)["config"]["workload"]
-    json.dump(out, open(os.path.join(prof, f"{tag}_pmc.json"), "w"), indent=1, sort_keys=True)
+    sl = bench_line(os.path.join(src, "stats.log"))
+    if sl:
+        open(os.path.join(prof, f"{tag}_bench.json"), "w").write(sl)
     print(f"wrote profiles/{tag}_*")
 
 

@@ -6,10 +6,11 @@ TAG=${1:-rows}; MAT=${2:-webbase}; P=${3:-rows}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
+export TSG_PATH=$P
 cd /tmp
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run -- \
-  python3 "$ROOT/tools/fz_time.py" "$MAT" --path="$P" > "$OUT/stats.log" 2>&1
+  python3 "$ROOT/bench.py" --matrix "$MAT" --steps 5 --warmup 2 --no-cpu-baseline --tiled 0 > "$OUT/stats.log" 2>&1
 cd "$ROOT"
 python3 - "$OUT" <<'PY'
 import csv, glob, sys
