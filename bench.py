@@ -7,14 +7,15 @@ step 3 + GPU tile2csr (SURVEY.md §8d t_e2e).  Inputs are resident in HBM
 (src/tilespgemm-cuda.h:2808).
 
   python bench.py                       # N=1, webbase-1M synthetic stand-in
-  python bench.py --gpus N ...          # under torch.distributed.run: the north-star
-                                        # (default, strong scaling): the fixed product
-                                        # A*B, A split by tile-row blocks of equal work,
-                                        # B replicated, C row blocks gathered to rank 0
-                                        # over RCCL inside the timed region
-  python bench.py --gpus N --scaling weak
-                                        # rank r computes row block r of [A; A; ...; A]*B
-                                        # (one full A per rank, C stays distributed)
+  python bench.py --gpus N ...          # under torch.distributed.run (default: weak
+                                        # scaling): rank r computes row block r of
+                                        # [A; A; ...; A]*B (one full A per rank, B
+                                        # replicated, C stays distributed, no collective)
+  python bench.py --gpus N --scaling strong
+                                        # north_star's exchange: the fixed product A*B,
+                                        # A's rows split into pieces of equal work, B
+                                        # replicated, C gathered to rank 0 over RCCL
+                                        # inside the timed region (gather-bound: DESIGN 5)
   python bench.py --matrix lj           # products past int32 nnz(C) (the reference's
                                         # `int nnzC`, src/tilespgemm-cuda.h:2327) run as
                                         # sequential tile-row blocks of <= 1.5e9 products
@@ -297,14 +298,16 @@ def main():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N>1 (nccl = RCCL over xGMI; gloo = host-staged "
                          "rehearsal of the multi-rank path, e.g. several ranks on one GPU)")
-    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
-                    help="N>1: strong (default) = the fixed product, A's tile rows partitioned by "
-                         "work + RCCL gather of C to rank 0; weak = every rank owns one A-sized row "
-                         "block of the stacked product (fixed work per GPU, no data-path collective)")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="N>1: weak (default) = every rank owns one A-sized row block of the stacked "
+                         "product (fixed work per GPU, C stays distributed, no data-path collective); "
+                         "strong = the fixed product, A's rows partitioned by work + the RCCL gather of C "
+                         "to rank 0 (north_star's exchange step; gather-bound, DESIGN section 5)")
     ap.add_argument("--gather-sub", type=int, default=0,
-                    help="N>1 strong: each rank computes its rows as this many sub-blocks and sends each "
-                         "to rank 0 as soon as it is done, overlapping the gather with the next one "
-                         "(dist.StreamingGather); 0 = auto: 4 when a rank holds >= 2e8 products, else 1")
+                    help="N>1 strong: the rows are cut into N x this many pieces of equal products, rank r "
+                         "computing piece (s, r) in round s; each round goes to rank 0 straight into the final "
+                         "C while the next one computes (dist.RoundGather); 0 = auto: 4 when a rank holds "
+                         ">= 2e8 products, else 1")
     ap.add_argument("--block-products", type=float, default=1.5e9,
                     help="row-block size (intermediate products) when the product exceeds int32 "
                          "nnz(C): such products run as sequential row blocks, C kept per block")
@@ -364,6 +367,15 @@ def main():
                                       f"(tiles in -> tiled C out; the reference's timed region)",
                           "m": m, "nnzA": int(len(ci)), "nnzCub": cub, "nnzC": tl["nnzC"], "path": "tiled"},
                "roofline": tl["roofline"], "tiled": tl}
+        # HBM traffic of the call from a PMC summary of the same command (tools/profile.sh
+        # --leg tiled): every kernel's bytes over the calls, which also spreads the
+        # one-time csr2tile of A and B (outside the timed region) over the calls
+        pfile = pmc_file(out["config"]["workload"], args.pmc_from)
+        _, allk = pmc_traffic([], pfile)
+        rl = out["roofline"]
+        rl["traffic_all_kernels"] = allk
+        rl["traffic_over_b_alg"] = round(allk / rl["algorithmic_bytes"], 3) if allk else None
+        rl["traffic_source"] = os.path.relpath(pfile, REPO) if pfile else None
         print(json.dumps(out), flush=True)
         return
     blen_b = np.diff(rpb.astype(np.int64))
@@ -388,25 +400,22 @@ def main():
     nnzcub_full = int(cum[-1])
     weak = world > 1 and args.scaling == "weak"
     nnzcub_total = nnzcub_full * world if weak else nnzcub_full
-    # this rank's tile rows: strong = a contiguous block of ~equal work
-    if world > 1 and not weak:
-        work = tdist.tile_row_work(rp, ci, rpb, m, tm)
-        rank_rows = [(min(m, a * tm), min(m, b * tm)) for a, b in tdist.partition_tile_rows(work, world)]
-        r_lo, r_hi = rank_rows[rank]
-    else:
-        r_lo, r_hi = 0, m
     # products past int32 nnz(C) (the reference's `int nnzC`): sequential row
     # blocks of <= block_products each, every block's C kept on the device
     blocked = nnzcub_full > args.block_products
-    blocks = tdist.product_blocks(cum, r_lo, r_hi, args.block_products, tm) if blocked else [(r_lo, r_hi)]
     gather = world > 1 and not weak and not blocked
     nsub = 1
     if gather:
-        # the overlapped gather: every rank's rows as nsub sub-blocks of ~equal products
-        nsub = args.gather_sub or (4 if max(cum[b] - cum[a] for a, b in rank_rows) >= 2e8 else 1)
-        subs = [tdist.sub_blocks(cum, a, b, nsub, tm) for a, b in rank_rows]
-        sub_rows = [[b1 - b0 for b0, b1 in sb] for sb in subs]
-        blocks = subs[rank]
+        # the overlapped gather: rows cut into world x nsub pieces of ~equal products
+        # (row granularity), rank r computing piece (s, r) in round s (dist.RoundGather)
+        nsub = args.gather_sub or (4 if nnzcub_full / world >= 2e8 else 1)
+    if world > 1 and not weak:
+        pieces = tdist.row_pieces(cum, m, world, nsub)
+        my_pieces = [pieces[s][rank] for s in range(nsub)]
+    else:
+        pieces, my_pieces = None, [(0, m)]
+    r_lo, r_hi = my_pieces[0][0], my_pieces[-1][1]  # (blocked / single: one contiguous range)
+    blocks = tdist.product_blocks(cum, r_lo, r_hi, args.block_products, tm) if blocked else my_pieces
     dA_blocks = []
     for (b0, b1) in blocks:
         mb_, rpb_, cib_, vvb_ = tdist.slice_rows(m, rp, ci, vv, b0, b1)
@@ -427,10 +436,10 @@ def main():
         sts, nnz = [], 0
         c = None
         if gather:
-            # sub-blocks in turn, each handed to the streaming gather as soon as its C
-            # is complete (the context keeps every sub-block's C until the step ends)
+            # the rounds in turn, each piece handed to the gather as soon as its C is
+            # complete (the context keeps every piece's C until the step ends)
             ctx.reset()
-            sg = tdist.StreamingGather(rank, world, sub_rows, device="cpu" if host_coll else "cuda")
+            sg = tdist.RoundGather(rank, world, pieces, nnzcub_full, device="cpu" if host_coll else "cuda")
             for s, (_, _, dAb) in enumerate(dA_blocks):
                 c, st = ctx.spgemm(dAb, dB, tm, tm)
                 sts.append(st)
@@ -444,7 +453,7 @@ def main():
             gathered[0] = sg.finish()
             if not host_coll:
                 torch.cuda.synchronize()
-            gather_ms.append((time.perf_counter() - g0) * 1e3)  # (the part not hidden behind compute)
+            gather_ms.append((time.perf_counter() - g0) * 1e3)  # (the last round's, not hidden behind compute)
         else:
             for (_, _, dAb) in dA_blocks:
                 ctx.reset()
@@ -484,10 +493,11 @@ def main():
     else:
         nnzC = nnz_rank
     work_share = None
+    my_products = float(sum(cum[b] - cum[a] for a, b in my_pieces))
     if dist:
         # each rank's share of the intermediate products (its rows' work) and the
         # max/mean imbalance of the partition
-        w = torch.tensor([float(cum[r_hi] - cum[r_lo])], dtype=torch.float64, device=red_dev)
+        w = torch.tensor([my_products], dtype=torch.float64, device=red_dev)
         allw = [torch.zeros_like(w) for _ in range(world)]
         dist.all_gather(allw, w)
         ws = [float(x.item()) for x in allw]
@@ -495,11 +505,10 @@ def main():
         work_share = {"products": [int(x) for x in ws],
                       "max_over_mean": round(max(ws) / mean, 4) if mean > 0 else None}
         if not weak and mean > 0:
-            # hub tile rows: a single tile row heavier than a rank's fair share
-            # bounds the imbalance (the partition keeps tile rows whole)
-            heavy = np.nonzero(work > mean)[0]
-            work_share["hub_tile_rows"] = [int(t) for t in heavy[:16]]
-            work_share["max_tile_row_over_mean"] = round(float(work.max()) / mean, 4)
+            # the heaviest single row against a rank's fair share (the partition cuts
+            # between rows: a row heavier than the share would bound the imbalance)
+            prow = np.diff(cum)
+            work_share["max_row_over_mean"] = round(float(prow.max()) / mean, 6) if len(prow) else 0.0
     ms_per_step = elapsed * 1e3 / args.steps
     gflops = 2.0 * nnzcub_total * args.steps / elapsed / 1e9
 
@@ -507,15 +516,15 @@ def main():
     mins = {k: float(np.min([s[k] for s in stats])) for k in ("t_e2e_ms", "t_kern_ms")}
     dev_ms = med["t_csr2tile_ms"] + med["t_step1_ms"] + med["t_step2_ms"] + med["t_step3_ms"] + med["t_tile2csr_ms"]
     # SURVEY §8d algorithmic bytes (src/external/cusparse/main.cu:205-208), this rank's share
-    mrank = r_hi - r_lo
-    nnza_rank = int(rp[r_hi] - rp[r_lo])
+    mrank = sum(b - a for a, b in my_pieces)
+    nnza_rank = int(sum(int(rp[b]) - int(rp[a]) for a, b in my_pieces))
     nb_calls = 1 if gather else len(blocks)  # (the gather's sub-blocks: B counted once, as one call)
     b_alg = (4.0 * (mrank + nb_calls) + 12.0 * nnza_rank + (4.0 * (mb + 1) + 12.0 * len(cib)) * nb_calls
              + 4.0 * (mrank + nb_calls) + 12.0 * nnz_rank)
     achieved_pipe = b_alg / (dev_ms * 1e-3) / 1e9
     # context only (never the graded figure): + one fp64 value and one u16 local column
     # per intermediate product of this rank (SURVEY §8d B_stream)
-    b_stream = b_alg + 10.0 * float(cum[r_hi] - cum[r_lo])
+    b_stream = b_alg + 10.0 * my_products
     # dominant kernel (reads the CSR operands, builds the C rows = B_alg's terms),
     # timed with HIP events on the call's stream: the staged pipeline's step-3
     # numeric kernel, or the row-merge path's numeric phase (its class kernels
@@ -555,7 +564,7 @@ def main():
             acc += [float(len(g_ci)), float(g_rp[:-1].astype(np.int64).sum() + off * (len(g_rp) - 1)),
                     float(g_ci.astype(np.int64).sum()), float(g_vv.sum())]
             off += len(g_ci)
-        rows_rank = r_hi - r_lo
+        rows_rank = mrank
         if weak:  # every rank's block of the stacked product is the same C
             chk = acc.copy()
             chk[1] += off
@@ -601,7 +610,7 @@ def main():
         elif weak:
             par = f"stacked-row-block{world} (B replicated, C distributed)"
         elif gather:
-            par = f"row-block{world} + RCCL gather"
+            par = f"row-pieces{world}x{nsub} + RCCL gather"
         else:
             par = f"row-block{world} x {len(blocks)} sequential blocks (C distributed: past one int32 CSR)"
         out = {
@@ -619,7 +628,7 @@ def main():
                                         "tile-pattern step 1 also lists empty ones, see t_kern_tiled)") if path_id == 0
                                        else "-1: this path builds no C tiles (the reference-layout tiled C: see tiled)",
                        "row_blocks": 1 if gather else len(blocks),
-                       "gather_sub": nsub if gather else None,
+                       "gather_rounds": nsub if gather else None,
                        "parallelism": par},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,

@@ -21,7 +21,7 @@
 #include "tsg_internal.h"
 
 namespace tsg {
-int dev_tiles_finalize_c(Context &cx, tsg_dev_tiles &C, hipStream_t s);
+int dev_tiles_finalize_c(Context &cx, tsg_dev_tiles &C, hipStream_t s, bool zero_empty);
 int dev_rm2csc_from_structs(Context &cx, tsg_dev_tiles &B, hipStream_t s);
 
 void report_hip_error(hipError_t e, const char *what, const char *file, int line) {
@@ -90,6 +90,10 @@ int Context::init(int dev) {
     TSG_HIP(hipSetDevice(dev));
     TSG_HIP(hipHostMalloc((void **)&pinned, 64, hipHostMallocDefault));
     TSG_HIP(hipHostMalloc((void **)&pinned64, 256, hipHostMallocDefault));
+    TSG_HIP(hipMalloc((void **)&dscratch, 256));
+    TSG_HIP(hipMemset(dscratch, 0, 256));
+    pinned[15] = 0;
+    TSG_HIP(hipHostGetDevicePointer((void **)&dfail, pinned + 15, 0));
     for (auto &e : ev) TSG_HIP(hipEventCreate(&e));
     ev_ready = true;
     return TSG_OK;
@@ -118,11 +122,22 @@ void Context::destroy() {
     pool.trim();
     if (pinned) (void)hipHostFree(pinned);
     if (pinned64) (void)hipHostFree(pinned64);
+    if (dscratch) (void)hipFree(dscratch);
+    dscratch = nullptr;
     pinned = nullptr;
     pinned64 = nullptr;
     if (ev_ready)
         for (auto &e : ev) (void)hipEventDestroy(e);
     ev_ready = false;
+}
+
+// a single-pass scan whose look-back never resolved (k_scan_lb: a fault, never
+// expected) flags pinned[15] from the device; checked after the call's sync
+static int lookback_check(Context &cx) {
+    if (cx.pinned[15] == 0) return TSG_OK;
+    cx.pinned[15] = 0;
+    fprintf(stderr, "tsg: a device-wide scan's look-back timed out\n");
+    return TSG_ERR_HIP;
 }
 
 static double ev_ms(hipEvent_t a, hipEvent_t b) {
@@ -216,6 +231,7 @@ class HostLease {
     }
     tsg_context *ctx() { return c_; }
     Context &cx() { return c_->cx; }
+    Context &cx_or(Context &other) { return c_ ? c_->cx : other; }
     hipStream_t stream() { return c_->stream; }
 
   private:
@@ -666,7 +682,48 @@ int tsg_tilespgemm(tsg_smatrix *A, tsg_smatrix *B, tsg_smatrix *C, unsigned int 
     tsg_stats st{};
     auto h0 = std::chrono::steady_clock::now();
     int rc;
-    if (sq16) {
+    int evi[4] = {0, 1, 2, 3};  // the events bracketing steps 1 | 2 | 3
+    HostLease aux;  // the CSR route's step 1: its own context and stream (outlives the download)
+    double t_s1 = -1.0;
+    if (sq16 && use_csr) {
+        // step 1: the reference's tile-pattern C structure (empty tiles included);
+        // steps 2 + 3: C's nonzeros on the device CSR route (banded / row-merge /
+        // staged) -- bit-identical to the reference's steps 2/3 +
+        // tile2csr -- then laid out as the reference's tiled C on step 1's
+        // structure (tsg_ctiles.hip): Ptr, masks, Col, Value, tile_nnz.
+        // Step 1 and the CSR product read only A and B: step 1 runs on a second
+        // stream from a host thread (each has host round trips of its own), the
+        // layout kernel joins them.
+        (void)s2e;
+        evi[0] = 12, evi[1] = 12, evi[2] = 13, evi[3] = 14;
+        dC = tsg_dev_tiles{};
+        dC.m = A->m; dC.n = B->n; dC.tile_m = 16; dC.tile_n = 16;
+        dC.tilem = dA.tilem; dC.tilen = dB.tilen;
+        TSG_TRY(aux.acquire());
+        Context &cx1 = aux.cx();
+        hipStream_t s1 = aux.stream();
+        int rc1 = TSG_OK;
+        std::thread th([&] {
+            long long tp = 0;
+            rc1 = hipSetDevice(cx.device) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
+            if (rc1 == TSG_OK) rc1 = hipEventRecord(cx1.ev[11], s1) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
+            if (rc1 == TSG_OK) rc1 = dev_step1(cx1, dA, dB, dC, &tp, s1);
+            if (rc1 == TSG_OK) rc1 = hipEventRecord(cx1.ev[12], s1) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
+            if (rc1 == TSG_OK) rc1 = hipStreamSynchronize(s1) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
+        });
+        tsg_dev_csr Cc{};
+        tsg_stats st2{};
+        rc = hipEventRecord(cx.ev[12], s) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
+        if (rc == TSG_OK) rc = dev_spgemm16(cx, &cA, &cB, s, &Cc, &st2);
+        if (rc == TSG_OK) rc = hipEventRecord(cx.ev[13], s) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
+        th.join();
+        if (rc == TSG_OK) rc = rc1;
+        if (rc == TSG_OK) t_s1 = ev_ms(cx1.ev[11], cx1.ev[12]);
+        if (rc == TSG_OK) rc = dev_ctiles_from_csr(cx, Cc, dC, s);
+        if (rc == TSG_OK) rc = hipEventRecord(cx.ev[14], s) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
+        if (rc == TSG_OK) TSG_HIP(hipStreamSynchronize(s));
+        if (rc == TSG_OK && cx.pinned[8] != 0) rc = TSG_ERR_HIP;  // (a nonzero outside step 1's tiles)
+    } else if (sq16) {
         rc = dev_tilespgemm(cx, dA, dB, dC, &st, s, cx.ev, nullptr, use_csr ? &cA : nullptr, use_csr ? &cB : nullptr,
                             s2e);
     } else {
@@ -679,8 +736,11 @@ int tsg_tilespgemm(tsg_smatrix *A, tsg_smatrix *B, tsg_smatrix *C, unsigned int 
         if (rc == TSG_OK) rc = dev_tile_steps23(cx, dA, dB, dC, s, cx.ev);
     }
     if (rc == TSG_OK) TSG_HIP(hipStreamSynchronize(s));
+    if (rc == TSG_OK) rc = lookback_check(cx);
+    if (rc == TSG_OK) rc = lookback_check(aux.cx_or(cx));
     auto h1 = std::chrono::steady_clock::now();
-    if (rc == TSG_OK) rc = dev_tiles_finalize_c(cx, dC, s);
+    // (the CSR route's layout kernel already wrote the empty tiles' Ptr and mask)
+    if (rc == TSG_OK) rc = dev_tiles_finalize_c(cx, dC, s, !(sq16 && use_csr));
     if (rc == TSG_OK) {
         memset(C, 0, sizeof(*C));
         C->m = dC.m; C->n = dC.n; C->nnz = dC.nnz;
@@ -689,7 +749,9 @@ int tsg_tilespgemm(tsg_smatrix *A, tsg_smatrix *B, tsg_smatrix *C, unsigned int 
     cx.pool.release_all_live();
     if (rc != TSG_OK) return rc;
     // the reference's steps at every tile size: step 1 | step 2 + scan | step 3
-    const double t1 = ev_ms(cx.ev[0], cx.ev[1]), t2 = ev_ms(cx.ev[1], cx.ev[2]), t3 = ev_ms(cx.ev[2], cx.ev[3]);
+    // (the CSR route: step 1 overlaps step 2, its own stream's duration)
+    const double t1 = t_s1 >= 0 ? t_s1 : ev_ms(cx.ev[evi[0]], cx.ev[evi[1]]),
+                 t2 = ev_ms(cx.ev[evi[1]], cx.ev[evi[2]]), t3 = ev_ms(cx.ev[evi[2]], cx.ev[evi[3]]);
     const double tk = std::chrono::duration<double, std::milli>(h1 - h0).count();
     if (time_step1) *time_step1 = t1;
     if (time_step2) *time_step2 = t2;
@@ -904,6 +966,7 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
         if (path_id >= 0) {
             TSG_HIP(hipEventRecord(cx.ev[10], s));
             TSG_HIP(hipEventSynchronize(cx.ev[10]));
+            TSG_TRY(lookback_check(cx));
             auto h1 = std::chrono::steady_clock::now();
             st.numtileA = -1;
             st.numtileB = -1;
@@ -971,6 +1034,7 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
                            s2elem));
     TSG_HIP(hipEventRecord(cx.ev[10], s));
     TSG_HIP(hipEventSynchronize(cx.ev[10]));
+    TSG_TRY(lookback_check(cx));
     auto h1 = std::chrono::steady_clock::now();
     st.numtileA = tA.numtile;
     st.numtileB = tB.numtile;

@@ -87,12 +87,123 @@ __global__ __launch_bounds__(WG) void k_scan_apply(T *a, long n, const P *part) 
     }
 }
 
+// Single pass (decoupled look-back) for n past one tile: each workgroup takes
+// a ticket (tiles in ticket order: every predecessor is already running),
+// scans its tile in LDS, publishes the tile's sum, then its first wave sums the
+// predecessors' published values 64 at a time until it meets an inclusive
+// prefix, and publishes its own.  One launch + the status memset instead of
+// reduce / scan of the partials / apply (three launches, the values read
+// twice).  Status words: flag in bits 62-63 (1: the tile's sum, 2: its
+// inclusive prefix), the value below -- every scan here is of non-negative
+// counts.  A predecessor that never publishes within 2 s of wall clock (a
+// fault, not a slow tile) sets the caller's host-mapped failure flag
+// (Context::dfail, checked at the end of the API call) instead of hanging.
+constexpr unsigned long long LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_VAL = (1ull << 62) - 1;
+__device__ __forceinline__ unsigned long long lb_ld(unsigned long long *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lb_st(unsigned long long *p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ long long lb_lookback(unsigned long long *status, int b, long long n, int *fail) {
+    const int lane = lane_id();
+    if (b == 0) {
+        if (lane == 0) lb_st(&status[0], LB_INC | (unsigned long long)n);
+        return 0;
+    }
+    if (lane == 0) lb_st(&status[b], LB_AGG | (unsigned long long)n);
+    long long excl = 0;
+    int j0 = b - 1;
+    for (;;) {
+        const int j = j0 - lane;
+        unsigned long long st = j >= 0 ? lb_ld(&status[j]) : LB_INC;
+        const unsigned long long w0 = wall_clock64();
+        while ((st >> 62) == 0) {
+            __builtin_amdgcn_s_sleep(1);
+            st = lb_ld(&status[j]);
+            if ((st >> 62) == 0 && wall_clock64() - w0 > 200000000ull) {  // (100 MHz wall clock: 2 s)
+                __hip_atomic_store(fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                st = LB_INC;
+            }
+        }
+        const u64 inc = __ballot((st >> 62) == 2);
+        const long long val = (long long)(st & LB_VAL);
+        if (inc) {
+            const int nearest = __ffsll((long long)inc) - 1;  // the nearest predecessor with its inclusive prefix
+            excl += wave_sum(lane <= nearest ? val : 0ll);
+            break;
+        }
+        excl += wave_sum(val);
+        j0 -= 64;
+    }
+    if (lane == 0) lb_st(&status[b], LB_INC | (unsigned long long)(excl + n));
+    return excl;
+}
+
+template <class T>
+__global__ __launch_bounds__(WG) void k_scan_lb(T *a, long n, unsigned long long *status, int *ticket, int nb,
+                                                int *fail) {
+    __shared__ T tile[SCAN_TILE + SCAN_TILE / 16];
+    __shared__ T red[WAVES];
+    __shared__ int sb;
+    __shared__ long long sx;
+    if (threadIdx.x == 0) {
+        const int b = atomicAdd(ticket, 1);
+        if (b == nb - 1) atomicExch(ticket, 0);  // (the last ticket: reset for the next scan)
+        sb = b;
+    }
+    __syncthreads();
+    const int b = sb;
+    const long base = (long)b * SCAN_TILE;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        const int li = k * WG + threadIdx.x;
+        const long i = base + li;
+        tile[scan_pad(li)] = (i < n) ? a[i] : T(0);
+    }
+    __syncthreads();
+    T sum = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) sum += tile[scan_pad(threadIdx.x * SCAN_ITEMS + k)];
+    T tot;
+    T off = block_excl_scan(sum, &tot, red);
+    if (threadIdx.x < 64) {
+        const long long x = lb_lookback(status, b, (long long)tot, fail);
+        if (threadIdx.x == 0) sx = x;
+    }
+    __syncthreads();
+    off += (T)sx;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        const int li = scan_pad(threadIdx.x * SCAN_ITEMS + k);
+        const T v = tile[li];
+        tile[li] = off;
+        off += v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        const int li = k * WG + threadIdx.x;
+        const long i = base + li;
+        if (i < n) a[i] = tile[scan_pad(li)];
+    }
+}
+
 template <class T> static int scan_exclusive(Context &cx, T *a, long n, hipStream_t s) {
     if (n <= 0) return TSG_OK;
-    long nb = (n + SCAN_TILE - 1) / SCAN_TILE;
+    const long nb = (n + SCAN_TILE - 1) / SCAN_TILE;
     if (nb == 1) {
         k_scan_apply<T><<<1, WG, 0, s>>>(a, n, (const T *)nullptr);
         TSG_HIP(hipGetLastError());
+        return TSG_OK;
+    }
+    if (nb < (1L << 31)) {
+        unsigned long long *status = nullptr;
+        TSG_TRY(cx.get(&status, (size_t)nb));
+        TSG_HIP(hipMemsetAsync(status, 0, (size_t)nb * sizeof(unsigned long long), s));
+        k_scan_lb<T><<<(unsigned)nb, WG, 0, s>>>(a, n, status, cx.dscratch + 2, (int)nb, cx.dfail);
+        TSG_HIP(hipGetLastError());
+        cx.put(status);
         return TSG_OK;
     }
     T *part = nullptr;
@@ -1303,56 +1414,53 @@ __global__ __launch_bounds__(WG) void k_entry_bounds(const int *ciA, long nnzA, 
     }
 }
 
-// row starts as a bitmap over entry positions (bit p set: some non-empty row starts at p)
-// Row sortedness in one pass, a workgroup per SRT_TILE entries: the rows
-// starting in the tile (a binary search of its bounds in the row pointers)
-// mark their first entries in an LDS bitmap, then a non-ascent ci[p] <= ci[p-1]
-// (a descent, or a column repeated inside the row) that is not at a row start
-// means some row is not strictly column-sorted -- reported
-// by a system-scope store into the caller's host-mapped flag (no device flag,
-// no memset, no copy back).
-constexpr int SRT_TILE = 4096;
-// first index in [0, n) whose element is >= key (n if none), a wave at a time:
-// 64 probes per step (ballot), so log64(n) dependent loads instead of log2(n)
-// (mawi's 226 M row pointers: 5 instead of 28)
-__device__ __forceinline__ int wave_lower_bound(const int *a, int n, int key) {
-    const int lane = lane_id();
-    long long lo = 0, hi = n;  // the answer lies in [lo, hi]
-    while (hi - lo > 64) {
-        const long long step = (hi - lo + 63) / 64;
-        const long long x = lo + lane * step;
-        const bool ge = x >= hi || a[x] >= key;  // (monotone over the lanes)
-        const u64 b = __ballot(ge);
-        const int f = b ? __builtin_ctzll(b) : 64;
-        const long long nlo = f > 0 ? lo + (long long)(f - 1) * step + 1 : lo;
-        hi = f < 64 ? min(hi, lo + (long long)f * step) : hi;
-        lo = nlo;
+// Row sortedness in one pass with no search: D = the non-ascents ci[p] <=
+// ci[p-1] over all entries (a descent, or a column repeated), R = those at the
+// first entry of a non-empty row (a thread per row).  The first entries of
+// non-empty rows are distinct positions, so D - R counts the non-ascents
+// inside rows: every row is strictly column-sorted iff D == R.  Each workgroup
+// adds its share of D - R to a device counter; the last workgroup to finish
+// (a done counter) reads it, reports a nonzero total by a system-scope store
+// into the caller's host-mapped flag, and resets both counters for the next
+// call (Context::dscratch, zeroed once at init).
+constexpr int SRT_PT = 4;  // entries (and rows) per thread, their loads issued together
+__global__ __launch_bounds__(WG) void k_rows_sorted_count(const int *rp, const int *ci, int m, int nnz, int *cnt,
+                                                          int *hflag) {
+    __shared__ int red[WAVES];
+    const int tid = threadIdx.x;
+    const long b0 = (long)blockIdx.x * WG * SRT_PT;
+    int c0[SRT_PT], c1[SRT_PT], r0[SRT_PT], r1[SRT_PT];
+#pragma unroll
+    for (int u = 0; u < SRT_PT; ++u) {
+        const long p = b0 + u * WG + tid;
+        const bool okp = p >= 1 && p < nnz, okr = p < m;
+        c0[u] = okp ? ci[p - 1] : 0;
+        c1[u] = okp ? ci[p] : 1;
+        r0[u] = okr ? rp[p] : 0;
+        r1[u] = okr ? rp[p + 1] : 0;
     }
-    const long long x = lo + lane;
-    const u64 b = __ballot(x < hi && a[x] >= key);
-    return b ? (int)(lo + __builtin_ctzll(b)) : (int)hi;
-}
-
-__global__ __launch_bounds__(WG) void k_rows_sorted_tiles(const int *rp, const int *ci, int m, int nnz, int *hflag) {
-    __shared__ u32 st[SRT_TILE / 32];
-    __shared__ int rr[2];
-    const int tid = threadIdx.x, wv = wave_id();
-    const int p0 = blockIdx.x * SRT_TILE, p1 = min(nnz, p0 + SRT_TILE);
-    for (int i = tid; i < SRT_TILE / 32; i += WG) st[i] = 0;
-    if (wv < 2) {  // rows starting in [p0, p1): waves 0 and 1 search the row pointers
-        const int r = wave_lower_bound(rp, m + 1, wv ? p1 : p0);
-        if (lane_id() == 0) rr[wv] = r;
+    int v = 0, f0[SRT_PT], f1[SRT_PT];
+#pragma unroll
+    for (int u = 0; u < SRT_PT; ++u) {
+        v += c1[u] <= c0[u];
+        const bool st = r0[u] >= 1 && r0[u] < r1[u];  // a non-empty row past the first entry
+        f0[u] = st ? ci[r0[u] - 1] : 0;
+        f1[u] = st ? ci[r0[u]] : 1;
     }
-    __syncthreads();
-    for (int r = rr[0] + tid; r < rr[1]; r += WG) {
-        const int p = rp[r];
-        if (p < rp[r + 1]) atomicOr(&st[(p - p0) >> 5], 1u << ((p - p0) & 31));
+#pragma unroll
+    for (int u = 0; u < SRT_PT; ++u) v -= f1[u] <= f0[u];
+    v = block_sum(v, red);
+    if (tid == 0) {
+        if (v) atomicAdd(&cnt[0], v);
+        __threadfence();
+        if (atomicAdd(&cnt[1], 1) == (int)gridDim.x - 1) {  // the last workgroup
+            __threadfence();
+            const int tot = atomicAdd(&cnt[0], 0);
+            if (tot != 0) __hip_atomic_store(hflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            atomicExch(&cnt[0], 0);
+            atomicExch(&cnt[1], 0);
+        }
     }
-    __syncthreads();
-    bool bad = false;
-    for (int p = max(1, p0) + tid; p < p1; p += WG)
-        bad |= ci[p] <= ci[p - 1] && !((st[(p - p0) >> 5] >> ((p - p0) & 31)) & 1u);
-    if (__ballot(bad) && lane_id() == 0) __hip_atomic_store(hflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Queued only: the flag (1: some row is not column-sorted) lands in *host_flag
@@ -1363,8 +1471,9 @@ int dev_rows_sorted_async(Context &cx, const tsg_dev_csr &M, int *host_flag, hip
     if (M.m > 0 && M.nnz > 1) {
         int *dflag = nullptr;
         TSG_HIP(hipHostGetDevicePointer((void **)&dflag, host_flag, 0));
-        k_rows_sorted_tiles<<<(M.nnz + SRT_TILE - 1) / SRT_TILE, WG, 0, s>>>(M.rowpointer, M.columnindex, M.m, M.nnz,
-                                                                             dflag);
+        const long n = std::max<long>(M.nnz, M.m);
+        k_rows_sorted_count<<<(unsigned)((n + WG * SRT_PT - 1) / (WG * SRT_PT)), WG, 0, s>>>(
+            M.rowpointer, M.columnindex, M.m, M.nnz, cx.dscratch, dflag);
     }
     TSG_HIP(hipGetLastError());
     return TSG_OK;
@@ -2699,9 +2808,10 @@ __global__ __launch_bounds__(WG) void k_zero_empty_ptr(const int *nnzoff, int nu
 
 // Reference-layout extras for the host drop-in API: zero Ptr of empty C tiles
 // and fill tile_rowidx (the device pipeline needs neither).
-int dev_tiles_finalize_c(Context &cx, tsg_dev_tiles &C, hipStream_t s) {
+int dev_tiles_finalize_c(Context &cx, tsg_dev_tiles &C, hipStream_t s, bool zero_empty) {
     if (C.numtile <= 0) return TSG_OK;
-    k_zero_empty_ptr<<<grid_for(C.numtile, WG, 16384), WG, 0, s>>>(C.tile_nnz, C.numtile, C.tile_m, C.tile_csr_Ptr,
+    if (zero_empty)
+        k_zero_empty_ptr<<<grid_for(C.numtile, WG, 16384), WG, 0, s>>>(C.tile_nnz, C.numtile, C.tile_m, C.tile_csr_Ptr,
                                                                   C.mask);
     TSG_TRY(cx.get(&C.tile_rowidx, (size_t)C.numtile + 1));
     k_crow<<<grid_for(C.tilem, WAVES, 8192), WG, 0, s>>>(C.tile_ptr, C.tilem, C.tile_rowidx);

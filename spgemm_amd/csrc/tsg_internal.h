@@ -58,6 +58,8 @@ struct Context {
     DevicePool pool;
     int *pinned = nullptr;        // host pinned scratch for size read-backs
     long long *pinned64 = nullptr;
+    int *dscratch = nullptr;      // device counters that kernels leave zeroed (k_rows_sorted_count, k_scan_lb)
+    int *dfail = nullptr;         // device view of pinned[15]: a look-back that never resolved (k_scan_lb)
     hipEvent_t ev[16];
     bool ev_ready = false;
     std::vector<void *> owned;    // outputs handed to the caller (released on reset)
@@ -102,6 +104,9 @@ int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_d
               long long *tile_products, hipStream_t s, const tsg_dev_csr *Ael = nullptr,
               const tsg_dev_csr *Bel = nullptr, int2 *ebnd = nullptr,
               long long **tbase_out = nullptr, long long *tslots_out = nullptr, bool fill_ebnd = false);
+// the reference's tiled C payload (tile_nnz, Ptr, mask, Col, Value) laid onto
+// step 1's 16 x 16 structure from a column-sorted CSR C (tsg_ctiles.hip)
+int dev_ctiles_from_csr(Context &cx, const tsg_dev_csr &Cc, tsg_dev_tiles &C, hipStream_t s);
 // steps 2 + 3 on the reference tiled layout at any tile size (tsg_tile_steps.hip):
 // C holds step 1's structure at C.tile_m x C.tile_m; ev (optional) gets ev[1..3]
 int dev_tile_steps23(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_dev_tiles &C, hipStream_t s,

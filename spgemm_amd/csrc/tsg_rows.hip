@@ -38,6 +38,7 @@ namespace {
 
 constexpr int S16_MAX = 16;           // class S16: products (and runs) per row, 4 rows per wave
 constexpr int RS_MAX = 64;            // class S64: products (and runs) per row, a wave
+constexpr int S16_U = 4, S64_U = 2;   // rows per lane group of the S16 / S64 kernels (k_rows_small)
 // merge classes M1..M4: products and runs per row, threads per row -- each
 // sized so its LDS (16 B per product + 16 B per run) keeps several rows per CU
 // (M0..M3: run tables a few runs short of a power of two, so that 32, 16, 8
@@ -295,98 +296,130 @@ __global__ __launch_bounds__(OH_NT) void k_rows_order_h(const long long *E, cons
 }
 
 // ---- classes S16 / S64: G lanes per row (64/G rows per wave), the products
-// one per lane, ranks by counting the group's smaller (column, lane) keys
-template <int G>
+// one per lane, ranks by counting the group's smaller (column, lane) keys.
+// Each lane group takes U rows: the rows' loads (list, entries, B) are issued
+// stage by stage for all U together, so a wave waits for three dependent
+// memory round trips per U rows rather than per row (the classes are bound by
+// those chains, not by bytes: 85 us for mc2depi's 0.5 M S16 rows at U = 1).
+template <int G, int U>
 __global__ __launch_bounds__(WG) void k_rows_small(RowsArgs g) {
     constexpr int RPW = 64 / G;
-    __shared__ u64 sk[WAVES][64];
-    __shared__ double sv[WAVES][64];
+    __shared__ u64 sk[WAVES][U][64];
+    __shared__ double sv[WAVES][U][64];
     const int lane = lane_id(), wv = wave_id(), sl = lane % G, gb = lane - sl;
-    const int i = (blockIdx.x * WAVES + wv) * RPW + lane / G;
-    if ((blockIdx.x * WAVES + wv) * RPW >= g.nrows) return;  // wave-uniform
-    const bool live = i < g.nrows;
-    int r = 0, a0 = 0, k = 0;
-    long long base = 0;
-    if (live) {
-        const int4 e = g.list[i];
-        r = e.x;
-        a0 = e.y;
-        k = e.z;
-        base = g.E[a0];  // (the output offset: not waited for until the output)
-    }
-    // lane sl < k: run sl's B range and A value; the runs' offsets in the row
-    // by a scan of their lengths over the group
-    int2 be = make_int2(0, 0);
-    double av = 0.0;
-    if (sl < k) {
-        be = g.ebnd[a0 + sl];
-        av = g.vA[a0 + sl];
-    }
-    const int len = be.y - be.x, bs = be.x;
-    int inc = len;  // inclusive scan over the G lanes (DPP row shifts stay inside 16-lane rows)
-    inc += dpp_mov<0x111, 0xf>(0, inc);
-    inc += dpp_mov<0x112, 0xf>(0, inc);
-    inc += dpp_mov<0x114, 0xf>(0, inc);
-    inc += dpp_mov<0x118, 0xf>(0, inc);
-    if constexpr (G == 64) {
-        inc += dpp_mov<0x142, 0xa>(0, inc);  // row_bcast:15
-        inc += dpp_mov<0x143, 0xc>(0, inc);  // row_bcast:31
-    }
-    const int roff = sl < k ? inc - len : INT_MAX;
-    const int P = __shfl(inc, G - 1, G);
-    // position sl: its run = the last run starting at or before it
-    int run = 0;
-    if constexpr (G == 64) {
-        for (int j = 1; j < k; ++j) run = (__builtin_amdgcn_readlane(roff, j) <= sl) ? j : run;
-    } else {
+    const int w0 = (blockIdx.x * WAVES + wv) * RPW * U;  // the wave's first row
+    if (w0 >= g.nrows) return;                           // wave-uniform
+    int r[U], a0[U], k[U];
+    bool live[U];
+    long long base[U];
 #pragma unroll
-        for (int j = 1; j < G; ++j) run = __shfl(roff, j, G) <= sl ? j : run;
-    }
-    const int rs = __shfl(roff, run, G), rb = __shfl(bs, run, G);
-    const double ra = __shfl(av, run, G);
-    u64 key = ~0ull;
-    double x = 0.0;
-    if (sl < P) {
-        const int p = rb + sl - rs;
-        key = ((u64)(u32)g.Bcol[p] << 32) | (u32)sl;
-        x = ra * g.Bval[p];
-    }
-    const u32 khi = (u32)(key >> 32), klo = (u32)key;
-    int rank = 0;
-    if constexpr (G == 64) {  // one row per wave: P is wave-uniform, scalar reads of each key
-        for (int f = 0; f < P; ++f) {
-            const u64 kf = ((u64)(u32)__builtin_amdgcn_readlane((int)khi, f) << 32) |
-                           (u32)__builtin_amdgcn_readlane((int)klo, f);
-            rank += kf < key;
-        }
-    } else {
-#pragma unroll
-        for (int f = 0; f < G; ++f) {
-            const u64 kf = ((u64)(u32)__shfl((int)khi, f, G) << 32) | (u32)__shfl((int)klo, f, G);
-            rank += kf < key;  // (lanes past P hold ~0: never below a product)
+    for (int u = 0; u < U; ++u) {
+        const int i = w0 + u * RPW + lane / G;
+        live[u] = i < g.nrows;
+        r[u] = 0, a0[u] = 0, k[u] = 0;
+        if (live[u]) {
+            const int4 e = g.list[i];
+            r[u] = e.x;
+            a0[u] = e.y;
+            k[u] = e.z;
         }
     }
-    if (sl < P) {
-        sk[wv][gb + rank] = key;
-        sv[wv][gb + rank] = x;
+    // lane sl < k: run sl's B range and A value (and the row's output offset)
+    int2 be[U];
+    double av[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        be[u] = make_int2(0, 0);
+        av[u] = 0.0;
+        base[u] = 0;
+        if (live[u]) base[u] = g.E[a0[u]];  // (not waited for until the output)
+        if (sl < k[u]) {
+            be[u] = g.ebnd[a0[u] + sl];
+            av[u] = g.vA[a0[u] + sl];
+        }
+    }
+    // the runs' offsets in each row by a scan of their lengths over the group;
+    // position sl's run = the last run starting at or before it; its B element
+    int P[U], pp[U];
+    double ra[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int len = be[u].y - be[u].x, bs = be[u].x;
+        int inc = len;  // inclusive scan over the G lanes (DPP row shifts stay inside 16-lane rows)
+        inc += dpp_mov<0x111, 0xf>(0, inc);
+        inc += dpp_mov<0x112, 0xf>(0, inc);
+        inc += dpp_mov<0x114, 0xf>(0, inc);
+        inc += dpp_mov<0x118, 0xf>(0, inc);
+        if constexpr (G == 64) {
+            inc += dpp_mov<0x142, 0xa>(0, inc);  // row_bcast:15
+            inc += dpp_mov<0x143, 0xc>(0, inc);  // row_bcast:31
+        }
+        const int roff = sl < k[u] ? inc - len : INT_MAX;
+        P[u] = __shfl(inc, G - 1, G);
+        int run = 0;
+        if constexpr (G == 64) {
+            for (int j = 1; j < k[u]; ++j) run = (__builtin_amdgcn_readlane(roff, j) <= sl) ? j : run;
+        } else {
+#pragma unroll
+            for (int j = 1; j < G; ++j) run = __shfl(roff, j, G) <= sl ? j : run;
+        }
+        const int rs = __shfl(roff, run, G), rb = __shfl(bs, run, G);
+        ra[u] = __shfl(av[u], run, G);
+        pp[u] = rb + sl - rs;
+    }
+    u64 key[U];
+    double x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        key[u] = ~0ull;
+        x[u] = 0.0;
+        if (sl < P[u]) {
+            key[u] = ((u64)(u32)g.Bcol[pp[u]] << 32) | (u32)sl;
+            x[u] = g.Bval[pp[u]];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const u32 khi = (u32)(key[u] >> 32), klo = (u32)key[u];
+        int rank = 0;
+        if constexpr (G == 64) {  // one row per wave: P is wave-uniform, scalar reads of each key
+            for (int f = 0; f < P[u]; ++f) {
+                const u64 kf = ((u64)(u32)__builtin_amdgcn_readlane((int)khi, f) << 32) |
+                               (u32)__builtin_amdgcn_readlane((int)klo, f);
+                rank += kf < key[u];
+            }
+        } else {
+#pragma unroll
+            for (int f = 0; f < G; ++f) {
+                const u64 kf = ((u64)(u32)__shfl((int)khi, f, G) << 32) | (u32)__shfl((int)klo, f, G);
+                rank += kf < key[u];  // (lanes past P hold ~0: never below a product)
+            }
+        }
+        if (sl < P[u]) {
+            sk[wv][u][gb + rank] = key[u];
+            sv[wv][u][gb + rank] = ra[u] * x[u];
+        }
     }
     wave_lds_sync();
-    int col = -1;
-    bool head = false;
-    if (sl < P) {
-        col = key_col(sk[wv][gb + sl]);
-        head = sl == 0 || key_col(sk[wv][gb + sl - 1]) != col;
-    }
     const u64 gm = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << gb;
-    const u64 hb = __ballot(head) & gm;
-    if (head) {
-        double s = sv[wv][gb + sl];
-        for (int j = sl + 1; j < P && key_col(sk[wv][gb + j]) == col; ++j) s += sv[wv][gb + j];
-        const long long o = base + (long long)lanes_below(hb);
-        g.Scol[o] = col;
-        g.Sval[o] = s;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        int col = -1;
+        bool head = false;
+        if (sl < P[u]) {
+            col = key_col(sk[wv][u][gb + sl]);
+            head = sl == 0 || key_col(sk[wv][u][gb + sl - 1]) != col;
+        }
+        const u64 hb = __ballot(head) & gm;
+        if (head) {
+            double sm = sv[wv][u][gb + sl];
+            for (int j = sl + 1; j < P[u] && key_col(sk[wv][u][gb + j]) == col; ++j) sm += sv[wv][u][gb + j];
+            const long long o = base[u] + (long long)lanes_below(hb);
+            g.Scol[o] = col;
+            g.Sval[o] = sm;
+        }
+        if (live[u] && sl == 0) g.rnnz[r[u]] = __popcll(hb);
     }
-    if (live && sl == 0) g.rnnz[r] = __popcll(hb);
 }
 
 // U independent searches in lockstep (U LDS reads in flight per step): first
@@ -2154,8 +2187,8 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
         TSG_TRY(launch_m(4, k_rows_merge<M2_NT, M2_CAP, M2_RUNS>, ncls[4], M2_NT, s));
         TSG_TRY(launch_m(3, k_rows_merge<M1_NT, M1_CAP, M1_RUNS>, ncls[3], M1_NT, s));
         TSG_TRY(launch_m(2, k_rows_merge<M0_NT, M0_CAP, M0_RUNS>, ncls[2], M0_NT, s));
-        TSG_TRY(launch(1, k_rows_small<64>, (ncls[1] + WAVES - 1) / WAVES, WG, s));
-        TSG_TRY(launch(0, k_rows_small<16>, (ncls[0] + 4 * WAVES - 1) / (4 * WAVES), WG, s));
+        TSG_TRY(launch(1, k_rows_small<64, S64_U>, (ncls[1] + WAVES * S64_U - 1) / (WAVES * S64_U), WG, s));
+        TSG_TRY(launch(0, k_rows_small<16, S16_U>, (ncls[0] + 4 * WAVES * S16_U - 1) / (4 * WAVES * S16_U), WG, s));
         return TSG_OK;
     };
     // row counts -> row pointers -> C's arrays, with no host round trip: nnz(C)

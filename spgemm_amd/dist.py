@@ -112,112 +112,106 @@ def gather_csr_blocks(rowptr, col, val, rank, world, device=None):
     return out_rp, out_ci, out_v
 
 
-def sub_blocks(cum, r_lo, r_hi, nsub, tile_m):
-    """Rows [r_lo, r_hi) as `nsub` consecutive tile-row-aligned sub-blocks of
-    ~equal intermediate products (cum = nnzCub of the row prefixes); some may
-    be empty.  Every rank computes every rank's split the same way."""
-    cum = np.asarray(cum, dtype=np.int64)
-    bounds = [r_lo]
-    for s in range(1, nsub):
-        tgt = cum[r_lo] + (cum[r_hi] - cum[r_lo]) * s / nsub
-        b = int(np.searchsorted(cum, tgt, side="left")) // tile_m * tile_m
-        bounds.append(min(r_hi, max(bounds[-1], b)))
-    bounds.append(r_hi)
-    return list(zip(bounds[:-1], bounds[1:]))
+def row_pieces(cum, m, world, nsub):
+    """Rows [0, m) cut into world * nsub consecutive pieces of ~equal
+    intermediate products (cum: the products of the row prefixes, length m+1;
+    +1 per row so that runs of empty rows still spread), at ROW granularity: a
+    hub tile row's 16 rows may go to different ranks (the CSR path has no tile
+    rows).  Piece j is rank j % world's piece of round j // world, so that the
+    pieces of one round are consecutive in C.  Returns pieces[round][rank] =
+    (r0, r1).  (A single row heavier than a piece stays whole: none of the
+    BASELINE configs has one -- webbase's heaviest row is 65 K of its 69 M
+    products, the mawi prefix's 10^7 of 1.5 * 10^9.)"""
+    cum = np.asarray(cum, dtype=np.float64)
+    npc = max(1, world * nsub)
+    w = cum + np.arange(m + 1, dtype=np.float64)
+    bounds = [0]
+    for j in range(1, npc):
+        b = int(np.searchsorted(w, w[-1] * j / npc, side="left"))
+        bounds.append(min(m, max(bounds[-1], b)))
+    bounds.append(m)
+    return [[(bounds[s * world + r], bounds[s * world + r + 1]) for r in range(world)] for s in range(nsub)]
 
 
-class StreamingGather:
-    """Gather of C row blocks to rank 0 overlapped with their computation.
+class RoundGather:
+    """Gather of C to rank 0 in rounds, each overlapped with the next round's
+    computation.  The rows are cut into world x nsub pieces (row_pieces): rank
+    r computes piece (s, r) in round s and hands it to push(s, ...).  After each
+    round one all_gather brings every piece's nnz to every rank (one host
+    synchronisation per round); rank 0 then posts the receives of the peers'
+    pieces straight into the final C at their exact offsets (the earlier
+    rounds' nonzeros + the round's earlier pieces) and copies its own piece
+    there, while the peers post non-blocking sends and go on computing the next
+    round.  No concatenation: C's columns and values are written once on rank
+    0, into arrays sized by the product bound (`products`, fixed before the
+    first round; the returned arrays are views of their first nnz(C) entries).
+    Point-to-point messages between a pair match in posting order (RCCL/NCCL
+    P2P have no tags): every pair posts rounds in order."""
 
-    Each rank computes its rows as sub-blocks (sub_blocks above) and hands
-    each one to push() as soon as it is done: a peer posts non-blocking sends
-    of its row pointers (whose last entry, nnz, sizes the rest) and then its
-    columns and values, and goes on computing the next sub-block while they
-    travel; rank 0 posts the row-pointer receive of every peer's next
-    sub-block ahead, and after each of its own sub-blocks turns the arrived
-    row pointers into the column / value receives.  Point-to-point messages
-    between a pair match in posting order (RCCL/NCCL P2P have no tags), so
-    every peer's sub-blocks are received in order.  finish() returns the
-    concatenated CSR (rank 0's sub-blocks, then rank 1's, ...) on rank 0 and
-    None elsewhere.  sub_rows[r] = the row counts of rank r's sub-blocks."""
-
-    def __init__(self, rank, world, sub_rows, device=None):
+    def __init__(self, rank, world, pieces, products, device=None):
         import torch
         import torch.distributed as dist
         self.t, self.d = torch, dist
-        self.rank, self.world, self.sub_rows = rank, world, sub_rows
+        self.rank, self.world, self.pieces = rank, world, pieces
         self.dev = device
-        self.mine = []       # rank 0: its own sub-blocks
-        self.sends = []      # peers: (work handle, tensor) kept alive until finish
-        self.rp = {}         # rank 0: (peer, s) -> row pointer tensor being received
-        self.rp_work = {}
-        self.arr = {}        # rank 0: (peer, s) -> (col, val)
-        self.arr_work = []
-        self.next_s = [0] * world  # rank 0: each peer's next sub-block to turn into array receives
+        self.off = 0            # rank 0: nonzeros of the rounds gathered so far
+        self.work = []          # (work handle(s), tensors kept alive)
+        self.fix = []           # rank 0: (received row pointers, first row, offset)
         if rank == 0:
-            for r in range(1, world):
-                self._post_rp(r, 0)
-
-    def _post_rp(self, r, s):
-        if s >= len(self.sub_rows[r]):
-            return
-        buf = self.t.empty(self.sub_rows[r][s] + 1, dtype=self.t.int32, device=self.dev)
-        self.rp[(r, s)] = buf
-        self.rp_work[(r, s)] = self.d.irecv(buf, r)
-
-    def _advance(self, upto):
-        """rank 0: every peer's sub-blocks < upto: row pointers waited for,
-        column / value receives posted, the next row-pointer receive posted."""
-        for r in range(1, self.world):
-            while self.next_s[r] < min(upto, len(self.sub_rows[r])):
-                s = self.next_s[r]
-                self.rp_work.pop((r, s)).wait()
-                nnz = int(self.rp[(r, s)][-1].item())
-                col = self.t.empty(nnz, dtype=self.t.int32, device=self.dev)
-                val = self.t.empty(nnz, dtype=self.t.float64, device=self.dev)
-                if nnz:
-                    self.arr_work.append(self.d.irecv(col, r))
-                    self.arr_work.append(self.d.irecv(val, r))
-                self.arr[(r, s)] = (col, val)
-                self.next_s[r] = s + 1
-                self._post_rp(r, s + 1)
+            m = pieces[-1][-1][1] if pieces else 0
+            self.out_rp = torch.empty(m + 1, dtype=torch.int32, device=device)
+            self.out_ci = torch.empty(max(1, int(products)), dtype=torch.int32, device=device)
+            self.out_v = torch.empty(max(1, int(products)), dtype=torch.float64, device=device)
+            self.m = m
 
     def push(self, s, rowptr, col, val):
-        """this rank's sub-block s (its rows' CSR; row pointers from 0)"""
+        """this rank's piece of round s (its rows' CSR, row pointers from 0)"""
+        t, d = self.t, self.d
+        n = t.tensor([col.numel()], dtype=t.int64, device=self.dev)
+        alln = [t.zeros(1, dtype=t.int64, device=self.dev) for _ in range(self.world)]
+        d.all_gather(alln, n)
+        nn = [int(x) for x in t.cat(alln).tolist()]  # (the round's one host synchronisation)
         if self.rank != 0:
             rp = rowptr.contiguous()
-            self.sends.append((self.d.isend(rp, 0), rp))
-            if col.numel():
+            ops = [d.P2POp(d.isend, rp, 0)]
+            keep = [rp]
+            if nn[self.rank]:
                 c, v = col.contiguous(), val.contiguous()
-                self.sends.append((self.d.isend(c, 0), c))
-                self.sends.append((self.d.isend(v, 0), v))
+                ops += [d.P2POp(d.isend, c, 0), d.P2POp(d.isend, v, 0)]
+                keep += [c, v]
+            self.work.append((d.batch_isend_irecv(ops), keep))
             return
-        self.mine.append((rowptr, col, val))
-        self._advance(s + 1)  # (peers finish sub-block s about when rank 0 does)
+        o = self.off
+        ops, keep = [], []
+        for r in range(self.world):
+            r0, r1 = self.pieces[s][r]
+            k = nn[r]
+            if r == 0:
+                self.out_rp[r0:r1 + 1] = rowptr.to(t.int32) + o
+                if k:
+                    self.out_ci[o:o + k] = col
+                    self.out_v[o:o + k] = val
+            else:
+                rp = t.empty(r1 - r0 + 1, dtype=t.int32, device=self.dev)
+                ops.append(d.P2POp(d.irecv, rp, r))
+                keep.append(rp)
+                self.fix.append((rp, r0, o))
+                if k:
+                    ops.append(d.P2POp(d.irecv, self.out_ci[o:o + k], r))
+                    ops.append(d.P2POp(d.irecv, self.out_v[o:o + k], r))
+            o += k
+        self.off = o
+        if ops:
+            self.work.append((d.batch_isend_irecv(ops), keep))
 
     def finish(self):
-        if self.rank != 0:
-            for w, _ in self.sends:
+        for ws, _ in self.work:
+            for w in ws:
                 w.wait()
-            self.sends = []
+        self.work = []
+        if self.rank != 0:
             return None
-        self._advance(max(len(x) for x in self.sub_rows))
-        for w in self.arr_work:
-            w.wait()
-        t = self.t
-        parts = [(rp, c, v) for rp, c, v in self.mine]
-        for r in range(1, self.world):
-            parts += [(self.rp[(r, s)],) + self.arr[(r, s)] for s in range(len(self.sub_rows[r]))]
-        M = sum(p[0].numel() - 1 for p in parts)
-        NNZ = sum(p[1].numel() for p in parts)
-        out_rp = t.empty(M + 1, dtype=t.int32, device=self.dev)
-        ro, no = 0, 0
-        for rp, c, v in parts:
-            k = rp.numel() - 1
-            out_rp[ro:ro + k + 1] = rp.to(t.int32) + no
-            ro += k
-            no += c.numel()
-        out_rp[M] = no
-        out_ci = t.cat([p[1] for p in parts]) if parts else t.empty(0, dtype=t.int32, device=self.dev)
-        out_v = t.cat([p[2] for p in parts]) if parts else t.empty(0, dtype=t.float64, device=self.dev)
-        return out_rp, out_ci, out_v
+        for rp, r0, o in self.fix:  # the peers' row pointers, rebased
+            self.out_rp[r0:r0 + rp.numel()] = rp + o
+        self.out_rp[self.m] = self.off
+        return self.out_rp, self.out_ci[:self.off], self.out_v[:self.off]

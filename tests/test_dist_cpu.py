@@ -126,7 +126,7 @@ def test_product_blocks_cover_rows_within_cap(cap):
             assert work <= cap or b1 - b0 <= 16
 
 
-def _worker_stream(rank, world, port, kind, nsub, q):
+def _worker_rounds(rank, world, port, kind, nsub, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -135,17 +135,17 @@ def _worker_stream(rank, world, port, kind, nsub, q):
         mb, nb, rpb, cib, vvb = oB.csr()
         blen = np.diff(rpb.astype(np.int64))
         cum = np.concatenate([[0], np.cumsum(blen[ci])])[rp]
-        parts = tdist.partition_tile_rows(tdist.tile_row_work(rp, ci, rpb, m, 16), world)
-        subs = [tdist.sub_blocks(cum, min(m, a * 16), min(m, b * 16), nsub, 16) for a, b in parts]
-        g = tdist.StreamingGather(rank, world, [[b1 - b0 for b0, b1 in sb] for sb in subs])
-        for s, (b0, b1) in enumerate(subs[rank]):  # each sub-block "computed" (oracle) then pushed
+        pieces = tdist.row_pieces(cum, m, world, nsub)
+        g = tdist.RoundGather(rank, world, pieces, int(cum[-1]))
+        for s in range(nsub):  # each round's piece "computed" (oracle) then pushed
+            b0, b1 = pieces[s][rank]
             mk, rpk, cik, vvk = tdist.slice_rows(m, rp, ci, vv, b0, b1)
             _, _, crp, cci, cvv = O.gustavson(O.OMat.from_csr(mk, n, rpk, cik, vvk), oB).csr()
             g.push(s, torch.from_numpy(crp.astype(np.int32)), torch.from_numpy(cci.astype(np.int32)),
                    torch.from_numpy(cvv.copy()))
         out = g.finish()
         if rank == 0:
-            q.put(("ok", subs, [x.numpy() for x in out]))
+            q.put(("ok", pieces, [x.numpy().copy() for x in out]))
         else:
             assert out is None
     except Exception as e:  # surface worker failures to the parent
@@ -155,31 +155,54 @@ def _worker_stream(rank, world, port, kind, nsub, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,nsub", [(2, 3), (3, 4), (2, 1)])
-@pytest.mark.parametrize("kind", ["powerlaw", "aat", "empty"])
-def test_streaming_gather_of_sub_blocks_matches_full_product(world, nsub, kind):
-    """The overlapped gather (dist.StreamingGather): every rank's rows as
-    sub-blocks pushed as they are computed, rank 0 receiving them in order;
-    the gathered row pointers, columns and values equal the full product
-    array by array, and the sub-blocks tile each rank's rows."""
+def _run(world, target, args):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker_stream, args=(r, world, port, kind, nsub, q)) for r in range(world)]
+    procs = [ctx.Process(target=target, args=(r, world, port) + args + (q,)) for r in range(world)]
     for p in procs:
         p.start()
-    status, subs, got = q.get(timeout=120)
+    res = q.get(timeout=180)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert status == "ok", subs
+    return res
+
+
+@pytest.mark.parametrize("world,nsub", [(2, 3), (3, 4), (2, 1), (8, 2)])
+@pytest.mark.parametrize("kind", ["powerlaw", "aat", "empty"])
+def test_round_gather_of_row_pieces_matches_full_product(world, nsub, kind):
+    """The overlapped gather (dist.RoundGather): rows cut into world x nsub
+    pieces of equal products at row granularity, rank r computing piece (s, r)
+    in round s; rank 0 receives every round straight into the final C at its
+    exact offsets (no concatenation).  The gathered row pointers, columns and
+    values equal the full product array by array, and the pieces tile the rows
+    in round-major order."""
+    status, pieces, got = _run(world, _worker_rounds, (kind, nsub))
+    assert status == "ok", pieces
     m, n, rp, ci, vv = _matrix(kind)
     oA = O.OMat.from_csr(m, n, rp, ci, vv)
     oB = O.transpose(oA) if kind == "aat" else O.OMat.alias(oA)
     _, _, erp, eci, evv = O.gustavson(oA, oB).csr()
-    flat = [b for sb in subs for b in sb]
+    flat = [b for rnd in pieces for b in rnd]
     assert flat[0][0] == 0 and flat[-1][1] == m and all(flat[i][1] == flat[i + 1][0] for i in range(len(flat) - 1))
-    assert all(len(sb) == nsub for sb in subs)
+    assert len(pieces) == nsub and all(len(rnd) == world for rnd in pieces)
     np.testing.assert_array_equal(got[0], erp)
     np.testing.assert_array_equal(got[1], eci)
     np.testing.assert_array_equal(got[2], evv)
+
+
+def test_row_pieces_balance_and_split_hub_tile_rows():
+    """Pieces of ~equal products; a heavy tile row's rows go to different ranks
+    (row granularity), so no rank carries a hub tile row whole."""
+    rng = np.random.default_rng(4)
+    m = 4000
+    per_row = rng.integers(0, 20, size=m).astype(np.int64)
+    per_row[1600:1616] = 20000  # one hub tile row: 16 rows of 20 K products
+    cum = np.concatenate([[0], np.cumsum(per_row)])
+    for world, nsub in [(2, 1), (8, 1), (8, 4)]:
+        pieces = tdist.row_pieces(cum, m, world, nsub)
+        loads = [sum(cum[b] - cum[a] for a, b in [pieces[s][r] for s in range(nsub)]) for r in range(world)]
+        assert max(loads) <= 1.15 * cum[-1] / world + 20000, (world, nsub, loads)
+        owners = {r for s in range(nsub) for r in range(world) if pieces[s][r][0] < 1616 and pieces[s][r][1] > 1600}
+        assert len(owners) > 1 or world == 1

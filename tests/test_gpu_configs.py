@@ -6,6 +6,12 @@ the product runs as sequential tile-row blocks (spgemm_amd.dist.product_blocks,
 what `bench.py --matrix lj` times).  Here: the block with the most work (the
 hub rows, the load-imbalanced case) and two strided blocks, each C against the
 numeric Gustavson oracle at 1e8-product blocks (host-checkable sizes).
+
+mawi_201512020330 (config 5) at FULL scale (226 M rows, hub degree 10^7): the
+row prefix of ~2e8 products that `bench.py --matrix mawi` times a larger
+version of, through the default route (its hub-neighbour rows take the
+dominant-run kernels), against scipy's SpGEMM of the same rows (the oracle's
+dense row accumulator would need 226 M doubles per thread).
 """
 import numpy as np
 import pytest
@@ -33,7 +39,8 @@ def test_lj_heaviest_and_strided_row_blocks_vs_oracle(lj):
     work = np.array([cum[b1] - cum[b0] for b0, b1 in blocks], dtype=np.float64)
     rows = np.array([b1 - b0 for b0, b1 in blocks])
     dens = work / rows
-    pick = [int(np.argmax(dens)), len(blocks) // 3, 2 * len(blocks) // 3]
+    # the heaviest block and ten strided ones
+    pick = [int(np.argmax(dens))] + [k * len(blocks) // 11 for k in range(1, 11)]
     B = T.Matrix.from_csr(m, n, rp, ci, vv)
     oB = O.OMat.from_csr(m, n, rp, ci, vv)
     for k in pick:
@@ -48,3 +55,32 @@ def test_lj_heaviest_and_strided_row_blocks_vs_oracle(lj):
         np.testing.assert_allclose(got[4], ref[4], rtol=1e-10, atol=0)
         assert st["nnzCub"] == 0 or st["nnzCub"] == cum[b1] - cum[b0]
         del Cm, A
+
+
+def test_mawi_full_scale_prefix_vs_scipy():
+    """Full-scale mawi stand-in: the longest row prefix within 2e8 products
+    (19 hub-neighbour rows of 10^7 products each, the dominant-run kernels'
+    rows at their benched size) times the whole matrix, default route.  Values
+    pos % 10 + 1 (no zero values: every structural entry is a nonzero sum, so
+    scipy -- which drops zero sums -- keeps it; small integers: every sum exact
+    whatever its order).  Row pointers, columns and values array for array."""
+    import scipy.sparse as sp
+    m, n, rp, ci, _ = synth.mawi()
+    vv = (np.arange(len(ci)) % 10 + 1).astype(np.float64)
+    blen = np.diff(rp.astype(np.int64))
+    cum = np.concatenate([[0], np.cumsum(blen[ci])])[rp]
+    r = int(np.searchsorted(cum, 2e8, side="right") - 1)
+    P = np.diff(cum[:r + 1])
+    assert P.max() >= 10 ** 7 and (P > 65536).sum() >= 10, (r, P.max())
+    A = T.Matrix.from_csr(r, n, rp[:r + 1].copy(), ci[:rp[r]].copy(), vv[:rp[r]].copy())
+    B = T.Matrix.from_csr(m, n, rp, ci, vv)
+    Cm, st = T.spgemm(A, B)
+    assert st["path"] == T.PATH_ROWS
+    got = Cm.csr()
+    del Cm, A, B
+    ref = (sp.csr_matrix((vv[:rp[r]], ci[:rp[r]], rp[:r + 1]), shape=(r, n)) @
+           sp.csr_matrix((vv, ci, rp), shape=(m, n))).tocsr()
+    ref.sort_indices()
+    np.testing.assert_array_equal(got[2], ref.indptr)
+    np.testing.assert_array_equal(got[3], ref.indices)
+    np.testing.assert_array_equal(got[4], ref.data)

@@ -25,7 +25,7 @@ def _bench(nproc, mtx, aat, scaling=None, extra=()):
             "--gpus", str(nproc)]
     if mtx:
         args += ["--mtx", mtx, "--aat", str(aat)]
-    if scaling:  # default invocation (no flag) = strong, the north-star measurement
+    if scaling:  # default invocation (no flag) = weak: fixed work per GPU, C stays distributed
         args += ["--scaling", scaling]
     args += list(extra)
     if nproc > 1:
@@ -43,13 +43,13 @@ def _bench(nproc, mtx, aat, scaling=None, extra=()):
 
 @pytest.mark.parametrize("name,aat", [("x_powerlaw_400", 0), ("x_rect_50x130", 1)])
 def test_two_ranks_gather_equals_single_rank(name, aat):
-    """The DEFAULT multi-rank invocation is the north-star strong scaling:
-    fixed product, work-balanced tile-row blocks, gather of C to rank 0."""
+    """Strong scaling (--scaling strong, north_star's exchange step): fixed
+    product, work-balanced row pieces, gather of C to rank 0."""
     mtx = os.path.join(REPO, "tests", "golden", "fixtures", name + ".mtx")
     one = _bench(1, mtx, aat)
     assert one["scaling"] == "single" and one["config"]["parallelism"] == "single"
-    two = _bench(2, mtx, aat)
-    assert two["n_gpus"] == 2 and two["config"]["parallelism"].startswith("row-block2")
+    two = _bench(2, mtx, aat, "strong")
+    assert two["n_gpus"] == 2 and two["config"]["parallelism"].startswith("row-pieces2")
     assert two["scaling"] == "strong"
     assert two["check"] == one["check"]
     assert two["config"]["nnzC"] == one["config"]["nnzC"]
@@ -58,12 +58,13 @@ def test_two_ranks_gather_equals_single_rank(name, aat):
 
 @pytest.mark.parametrize("name,aat", [("x_powerlaw_400", 1)])
 def test_two_ranks_weak_stacked_product(name, aat):
-    """Weak scaling (--scaling weak): each rank owns one A-sized row block of
-    [A; A] * B, no collective on the data path; every block equals the 1-rank C
-    (bench asserts this across ranks) and the job counts twice the work."""
+    """Weak scaling (the DEFAULT multi-rank invocation, no --scaling flag): each
+    rank owns one A-sized row block of [A; A] * B, no collective on the data
+    path; every block equals the 1-rank C (bench asserts this across ranks) and
+    the job counts twice the work."""
     mtx = os.path.join(REPO, "tests", "golden", "fixtures", name + ".mtx")
-    one = _bench(1, mtx, aat, "weak")
-    two = _bench(2, mtx, aat, "weak")
+    one = _bench(1, mtx, aat)
+    two = _bench(2, mtx, aat)
     assert two["scaling"] == "weak" and two["config"]["parallelism"].startswith("stacked-row-block2")
     assert two["check"] == one["check"]
     assert two["config"]["nnzC"] == 2 * one["config"]["nnzC"]
@@ -94,11 +95,11 @@ def test_mawi_eight_ranks_gather_vs_oracle(tmp_path):
     import _oracle as O
     (m, n, rp, ci, vv), rows = _mawi_rows(0.01, 2e8)
     dump = str(tmp_path / "c8.npz")
-    eight = _bench(8, None, 0, extra=("--matrix", "mawi", "--scale", "0.01", "--rows", str(rows), "--dump", dump,
+    eight = _bench(8, None, 0, "strong", extra=("--matrix", "mawi", "--scale", "0.01", "--rows", str(rows), "--dump", dump,
                                       "--gather-sub", "3"))
     assert eight["n_gpus"] == 8 and eight["scaling"] == "strong"
-    assert eight["config"]["gather_sub"] == 3  # the overlapped gather: sub-blocks streamed to rank 0
-    assert eight["config"]["parallelism"] == "row-block8 + RCCL gather"
+    assert eight["config"]["gather_rounds"] == 3  # the overlapped gather: rounds received in place on rank 0
+    assert eight["config"]["parallelism"] == "row-pieces8x3 + RCCL gather"
     ws = eight["work_share"]
     assert len(ws["products"]) == 8 and sum(ws["products"]) == eight["config"]["nnzCub"]
     assert ws["max_over_mean"] >= 1.0
@@ -125,22 +126,23 @@ def test_blocked_rows_equal_single_block():
     assert blk["config"]["row_blocks"] > 3
     assert blk["check"] == one["check"]
     assert blk["config"]["nnzCub"] == one["config"]["nnzCub"]
-    two = _bench(2, mtx, 0, extra=("--block-products", "300"))
+    two = _bench(2, mtx, 0, "strong", extra=("--block-products", "300"))
     assert "sequential blocks" in two["config"]["parallelism"]
     assert two["check"] == one["check"]
 
 
 @pytest.mark.parametrize("nsub", [1, 3])
 def test_two_ranks_streaming_gather_arrays(tmp_path, nsub):
-    """The overlapped gather (--gather-sub): each rank's rows as sub-blocks,
-    each sent to rank 0 as soon as its C is complete; the gathered C equals
-    the single-rank C array by array (--dump)."""
+    """The overlapped gather (--gather-sub, dist.RoundGather): rows in 2 x nsub
+    pieces, each round received straight into rank 0's final C while the next
+    one computes; the gathered C equals the single-rank C array by array
+    (--dump)."""
     import numpy as np
     mtx = os.path.join(REPO, "tests", "golden", "fixtures", "x_powerlaw_400.mtx")
     d1, d2 = str(tmp_path / "one.npz"), str(tmp_path / "two.npz")
     one = _bench(1, mtx, 0, extra=("--dump", d1))
-    two = _bench(2, mtx, 0, extra=("--dump", d2, "--gather-sub", str(nsub)))
-    assert two["config"]["gather_sub"] == nsub and two["gather_ms"] is not None
+    two = _bench(2, mtx, 0, "strong", extra=("--dump", d2, "--gather-sub", str(nsub)))
+    assert two["config"]["gather_rounds"] == nsub and two["gather_ms"] is not None
     a, b = np.load(d1), np.load(d2)
     for k in ("rowptr", "col", "val"):
         np.testing.assert_array_equal(a[k], b[k])

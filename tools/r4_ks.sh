@@ -16,4 +16,4 @@ rows.sort(key=lambda r: -float(r["TotalDurationNs"]))
 for r in rows[:22]:
     print(f'{r["Name"][:60]:60s} calls {r["Calls"]:>5s} avg_us {float(r["AverageNs"])/1e3:9.1f}')
 PY
-grep '^{"metric"' "$OUT/stats.log" | python3 -c "import json,sys;d=json.loads(sys.stdin.read());print(d['ms_per_step'],d['stage_ms'])"
+grep '^{"metric"' "$OUT/stats.log" | python3 -c "import json,sys;d=json.loads(sys.stdin.read());print(d['ms_per_step'],d.get('stage_ms') or {k: v for k, v in (d.get('tiled') or {}).items() if k.startswith('t_')})"
