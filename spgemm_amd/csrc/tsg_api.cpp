@@ -90,10 +90,8 @@ int Context::init(int dev) {
     TSG_HIP(hipSetDevice(dev));
     TSG_HIP(hipHostMalloc((void **)&pinned, 64, hipHostMallocDefault));
     TSG_HIP(hipHostMalloc((void **)&pinned64, 256, hipHostMallocDefault));
-    TSG_HIP(hipMalloc((void **)&dscratch, 256));
-    TSG_HIP(hipMemset(dscratch, 0, 256));
-    pinned[15] = 0;
-    TSG_HIP(hipHostGetDevicePointer((void **)&dfail, pinned + 15, 0));
+    TSG_HIP(hipHostGetDevicePointer((void **)&dpinned, pinned, 0));
+    TSG_HIP(hipHostGetDevicePointer((void **)&dpinned64, pinned64, 0));
     for (auto &e : ev) TSG_HIP(hipEventCreate(&e));
     ev_ready = true;
     return TSG_OK;
@@ -122,22 +120,11 @@ void Context::destroy() {
     pool.trim();
     if (pinned) (void)hipHostFree(pinned);
     if (pinned64) (void)hipHostFree(pinned64);
-    if (dscratch) (void)hipFree(dscratch);
-    dscratch = nullptr;
     pinned = nullptr;
     pinned64 = nullptr;
     if (ev_ready)
         for (auto &e : ev) (void)hipEventDestroy(e);
     ev_ready = false;
-}
-
-// a single-pass scan whose look-back never resolved (k_scan_lb: a fault, never
-// expected) flags pinned[15] from the device; checked after the call's sync
-static int lookback_check(Context &cx) {
-    if (cx.pinned[15] == 0) return TSG_OK;
-    cx.pinned[15] = 0;
-    fprintf(stderr, "tsg: a device-wide scan's look-back timed out\n");
-    return TSG_ERR_HIP;
 }
 
 static double ev_ms(hipEvent_t a, hipEvent_t b) {
@@ -231,7 +218,6 @@ class HostLease {
     }
     tsg_context *ctx() { return c_; }
     Context &cx() { return c_->cx; }
-    Context &cx_or(Context &other) { return c_ ? c_->cx : other; }
     hipStream_t stream() { return c_->stream; }
 
   private:
@@ -736,8 +722,6 @@ int tsg_tilespgemm(tsg_smatrix *A, tsg_smatrix *B, tsg_smatrix *C, unsigned int 
         if (rc == TSG_OK) rc = dev_tile_steps23(cx, dA, dB, dC, s, cx.ev);
     }
     if (rc == TSG_OK) TSG_HIP(hipStreamSynchronize(s));
-    if (rc == TSG_OK) rc = lookback_check(cx);
-    if (rc == TSG_OK) rc = lookback_check(aux.cx_or(cx));
     auto h1 = std::chrono::steady_clock::now();
     // (the CSR route's layout kernel already wrote the empty tiles' Ptr and mask)
     if (rc == TSG_OK) rc = dev_tiles_finalize_c(cx, dC, s, !(sq16 && use_csr));
@@ -910,7 +894,10 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
     // The sortedness check is queued ahead of A's tile counts; both results come
     // back with the counts' host round trip.  (With unsorted B rows the counts are
     // discarded: the full csr2tile below rebuilds A's tiles.)
-    TSG_TRY(dev_rows_sorted_async(cx, *B, cx.pinned + 1, s));
+    // (its last step -- the shares' sum into the flag -- rides on the row-merge
+    // setup's binning kernel, or runs before the first read-back of another route)
+    SortedShares shares;
+    TSG_TRY(dev_rows_sorted_shares(cx, *B, cx.pinned + 1, &shares, s));
     // Routing, B's rows column-sorted:
     //  * banded path (tsg_band.hip) when A averages >= 8 entries per row and every
     //    C row's reachable columns fit one window of <= 2,048 columns holding at
@@ -932,8 +919,10 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
         BandWin bw;
         // band candidates first (A rows of >= 8 entries on average): the window
         // check's read-back also brings the sortedness flag
-        if (!force_rows && (force_band || (A->m > 0 && A->nnz >= 8LL * A->m)))
+        if (!force_rows && (force_band || (A->m > 0 && A->nnz >= 8LL * A->m))) {
+            TSG_TRY(dev_rows_sorted_finish(cx, shares, s));
             TSG_TRY(dev_band_check(cx, *A, *B, force_band, &band, &bw, s));
+        }
         if (band && cx.pinned[1] != 0) {  // unsorted B rows: the windows mean nothing
             cx.put(bw.win);
             cx.put(bw.width);
@@ -952,7 +941,7 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
             // decides rows / tiles
             TSG_HIP(hipEventRecord(cx.ev[0], s));
             RowsPlan plan;
-            TSG_TRY(dev_rows_setup_async(cx, *A, *B, plan, s));
+            TSG_TRY(dev_rows_setup_async(cx, *A, *B, plan, s, shares.part ? &shares : nullptr));
             TSG_TRY(stream_wait(s));
             dev_rows_setup_read(cx, plan);
             const bool bsorted0 = cx.pinned[1] == 0;
@@ -966,7 +955,6 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
         if (path_id >= 0) {
             TSG_HIP(hipEventRecord(cx.ev[10], s));
             TSG_HIP(hipEventSynchronize(cx.ev[10]));
-            TSG_TRY(lookback_check(cx));
             auto h1 = std::chrono::steady_clock::now();
             st.numtileA = -1;
             st.numtileB = -1;
@@ -985,6 +973,7 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
             return TSG_OK;
         }
     }
+    TSG_TRY(dev_rows_sorted_finish(cx, shares, s));  // (forced tiles: the flag is still owed)
     const char *md = getenv("TSG_STEP2_MODE");
     const int forced = !md ? -1 : !strcmp(md, "elem") ? 1 : !strcmp(md, "tile") ? 0 : -1;
     const double skip = forced == 1 ? 1e300 : forced == 0 ? 0.0 : kStep2ElemMaxTileDensity;
@@ -1034,7 +1023,6 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
                            s2elem));
     TSG_HIP(hipEventRecord(cx.ev[10], s));
     TSG_HIP(hipEventSynchronize(cx.ev[10]));
-    TSG_TRY(lookback_check(cx));
     auto h1 = std::chrono::steady_clock::now();
     st.numtileA = tA.numtile;
     st.numtileB = tB.numtile;

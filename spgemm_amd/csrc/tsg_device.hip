@@ -87,125 +87,18 @@ __global__ __launch_bounds__(WG) void k_scan_apply(T *a, long n, const P *part) 
     }
 }
 
-// Single pass (decoupled look-back) for n past one tile: each workgroup takes
-// a ticket (tiles in ticket order: every predecessor is already running),
-// scans its tile in LDS, publishes the tile's sum, then its first wave sums the
-// predecessors' published values 64 at a time until it meets an inclusive
-// prefix, and publishes its own.  One launch + the status memset instead of
-// reduce / scan of the partials / apply (three launches, the values read
-// twice).  Status words: flag in bits 62-63 (1: the tile's sum, 2: its
-// inclusive prefix), the value below -- every scan here is of non-negative
-// counts.  A predecessor that never publishes within 2 s of wall clock (a
-// fault, not a slow tile) sets the caller's host-mapped failure flag
-// (Context::dfail, checked at the end of the API call) instead of hanging.
-constexpr unsigned long long LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_VAL = (1ull << 62) - 1;
-__device__ __forceinline__ unsigned long long lb_ld(unsigned long long *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void lb_st(unsigned long long *p, unsigned long long v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ long long lb_lookback(unsigned long long *status, int b, long long n, int *fail) {
-    const int lane = lane_id();
-    if (b == 0) {
-        if (lane == 0) lb_st(&status[0], LB_INC | (unsigned long long)n);
-        return 0;
-    }
-    if (lane == 0) lb_st(&status[b], LB_AGG | (unsigned long long)n);
-    long long excl = 0;
-    int j0 = b - 1;
-    for (;;) {
-        const int j = j0 - lane;
-        unsigned long long st = j >= 0 ? lb_ld(&status[j]) : LB_INC;
-        const unsigned long long w0 = wall_clock64();
-        while ((st >> 62) == 0) {
-            __builtin_amdgcn_s_sleep(1);
-            st = lb_ld(&status[j]);
-            if ((st >> 62) == 0 && wall_clock64() - w0 > 200000000ull) {  // (100 MHz wall clock: 2 s)
-                __hip_atomic_store(fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                st = LB_INC;
-            }
-        }
-        const u64 inc = __ballot((st >> 62) == 2);
-        const long long val = (long long)(st & LB_VAL);
-        if (inc) {
-            const int nearest = __ffsll((long long)inc) - 1;  // the nearest predecessor with its inclusive prefix
-            excl += wave_sum(lane <= nearest ? val : 0ll);
-            break;
-        }
-        excl += wave_sum(val);
-        j0 -= 64;
-    }
-    if (lane == 0) lb_st(&status[b], LB_INC | (unsigned long long)(excl + n));
-    return excl;
-}
-
-template <class T>
-__global__ __launch_bounds__(WG) void k_scan_lb(T *a, long n, unsigned long long *status, int *ticket, int nb,
-                                                int *fail) {
-    __shared__ T tile[SCAN_TILE + SCAN_TILE / 16];
-    __shared__ T red[WAVES];
-    __shared__ int sb;
-    __shared__ long long sx;
-    if (threadIdx.x == 0) {
-        const int b = atomicAdd(ticket, 1);
-        if (b == nb - 1) atomicExch(ticket, 0);  // (the last ticket: reset for the next scan)
-        sb = b;
-    }
-    __syncthreads();
-    const int b = sb;
-    const long base = (long)b * SCAN_TILE;
-#pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; ++k) {
-        const int li = k * WG + threadIdx.x;
-        const long i = base + li;
-        tile[scan_pad(li)] = (i < n) ? a[i] : T(0);
-    }
-    __syncthreads();
-    T sum = 0;
-#pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; ++k) sum += tile[scan_pad(threadIdx.x * SCAN_ITEMS + k)];
-    T tot;
-    T off = block_excl_scan(sum, &tot, red);
-    if (threadIdx.x < 64) {
-        const long long x = lb_lookback(status, b, (long long)tot, fail);
-        if (threadIdx.x == 0) sx = x;
-    }
-    __syncthreads();
-    off += (T)sx;
-#pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; ++k) {
-        const int li = scan_pad(threadIdx.x * SCAN_ITEMS + k);
-        const T v = tile[li];
-        tile[li] = off;
-        off += v;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; ++k) {
-        const int li = k * WG + threadIdx.x;
-        const long i = base + li;
-        if (i < n) a[i] = tile[scan_pad(li)];
-    }
-}
-
 template <class T> static int scan_exclusive(Context &cx, T *a, long n, hipStream_t s) {
     if (n <= 0) return TSG_OK;
-    const long nb = (n + SCAN_TILE - 1) / SCAN_TILE;
+    long nb = (n + SCAN_TILE - 1) / SCAN_TILE;
     if (nb == 1) {
         k_scan_apply<T><<<1, WG, 0, s>>>(a, n, (const T *)nullptr);
         TSG_HIP(hipGetLastError());
         return TSG_OK;
     }
-    if (nb < (1L << 31)) {
-        unsigned long long *status = nullptr;
-        TSG_TRY(cx.get(&status, (size_t)nb));
-        TSG_HIP(hipMemsetAsync(status, 0, (size_t)nb * sizeof(unsigned long long), s));
-        k_scan_lb<T><<<(unsigned)nb, WG, 0, s>>>(a, n, status, cx.dscratch + 2, (int)nb, cx.dfail);
-        TSG_HIP(hipGetLastError());
-        cx.put(status);
-        return TSG_OK;
-    }
+    // (a single-pass decoupled look-back scan measured slower here: 17 vs 15 us
+    // for mc2depi's 1.7 M entries, 25 vs 17 us for webbase's 3.1 M -- the
+    // inclusive prefix crosses HBM once per 64 tiles of look-back, and the
+    // status array needs its own memset)
     T *part = nullptr;
     TSG_TRY(cx.get(&part, nb));
     k_scan_reduce<T><<<(unsigned)nb, WG, 0, s>>>(a, n, part);
@@ -1179,6 +1072,31 @@ __global__ __launch_bounds__(WG) void k_step1_cap(const int *Aptr, int mA, int2 
     }
 }
 
+// the same capacities at tile level (the tile-pattern step 1 of the host tile
+// API): wave per A tile row, its tile products P = the B tile rows' lengths
+// over its tiles; every window gets min(P, window width) slots
+__global__ __launch_bounds__(WG) void k_step1_cap_tiles(const int *Atp, const int *Atc, const int *Btp, int tilemA,
+                                                        int nwin, int win, int tilenB, long long *cap, u64 *prod,
+                                                        int *ucnt) {
+    const int lane = threadIdx.x & 63;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // step 1's counters and the scans' n+1 slots
+        const long nu = (long)tilemA * nwin;
+        *prod = 0;
+        ucnt[nu] = 0;
+        cap[nu] = 0;
+    }
+    for (long i = ((long)blockIdx.x * WG + threadIdx.x) >> 6; i < tilemA; i += ((long)gridDim.x * WG) >> 6) {
+        long long p = 0;
+        for (int a = Atp[i] + lane; a < Atp[i + 1]; a += 64) {
+            const int k = Atc[a];
+            p += Btp[k + 1] - Btp[k];
+        }
+        p = wave_sum(p);
+        for (int w = lane; w < nwin; w += 64)
+            cap[i * nwin + w] = min(p, (long long)min(win, tilenB - w * win));
+    }
+}
+
 // compact the EL step-1 unit buffers into tile_columnidx (workgroup per unit)
 __global__ __launch_bounds__(WG) void k_step1_gather(const int *ubuf, const long long *ubuf_off, const int *unit_off,
                                                      long nunits, int *Ccol) {
@@ -1414,18 +1332,18 @@ __global__ __launch_bounds__(WG) void k_entry_bounds(const int *ciA, long nnzA, 
     }
 }
 
-// Row sortedness in one pass with no search: D = the non-ascents ci[p] <=
-// ci[p-1] over all entries (a descent, or a column repeated), R = those at the
-// first entry of a non-empty row (a thread per row).  The first entries of
-// non-empty rows are distinct positions, so D - R counts the non-ascents
-// inside rows: every row is strictly column-sorted iff D == R.  Each workgroup
-// adds its share of D - R to a device counter; the last workgroup to finish
-// (a done counter) reads it, reports a nonzero total by a system-scope store
-// into the caller's host-mapped flag, and resets both counters for the next
-// call (Context::dscratch, zeroed once at init).
+// Row sortedness with no search: D = the non-ascents ci[p] <= ci[p-1] over
+// all entries (a descent, or a column repeated), R = those at the first entry
+// of a non-empty row (a thread per row).  The first entries of non-empty rows
+// are distinct positions, so D - R counts the non-ascents inside rows: every
+// row is strictly column-sorted iff D == R.  Each workgroup writes its share
+// of D - R; one workgroup sums the shares and reports a nonzero total by a
+// system-scope store into the caller's host-mapped flag.  (The shares of one
+// workgroup do not cancel locally -- a row's first entry and the row itself
+// sit in different workgroups -- and one atomic per workgroup on a common
+// counter serialised: 47 us on mc2depi, 88 on webbase.)
 constexpr int SRT_PT = 4;  // entries (and rows) per thread, their loads issued together
-__global__ __launch_bounds__(WG) void k_rows_sorted_count(const int *rp, const int *ci, int m, int nnz, int *cnt,
-                                                          int *hflag) {
+__global__ __launch_bounds__(WG) void k_rows_sorted_count(const int *rp, const int *ci, int m, int nnz, int *part) {
     __shared__ int red[WAVES];
     const int tid = threadIdx.x;
     const long b0 = (long)blockIdx.x * WG * SRT_PT;
@@ -1450,33 +1368,54 @@ __global__ __launch_bounds__(WG) void k_rows_sorted_count(const int *rp, const i
 #pragma unroll
     for (int u = 0; u < SRT_PT; ++u) v -= f1[u] <= f0[u];
     v = block_sum(v, red);
-    if (tid == 0) {
-        if (v) atomicAdd(&cnt[0], v);
-        __threadfence();
-        if (atomicAdd(&cnt[1], 1) == (int)gridDim.x - 1) {  // the last workgroup
-            __threadfence();
-            const int tot = atomicAdd(&cnt[0], 0);
-            if (tot != 0) __hip_atomic_store(hflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            atomicExch(&cnt[0], 0);
-            atomicExch(&cnt[1], 0);
-        }
+    if (tid == 0) part[blockIdx.x] = v;
+}
+constexpr int SRT_FIN = 1024;  // the summing workgroup (mawi's 226 M rows: 2.2 * 10^5 shares)
+__global__ __launch_bounds__(SRT_FIN) void k_rows_sorted_final(const int *part, int nb, int *hflag) {
+    __shared__ long long red[SRT_FIN / 64];
+    long long v = 0;
+#pragma unroll 8
+    for (int i = threadIdx.x; i < nb; i += SRT_FIN) v += part[i];
+    v = wave_sum(v);
+    if (lane_id() == 0) red[wave_id()] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        long long t = 0;
+        for (int w = 0; w < SRT_FIN / 64; ++w) t += red[w];
+        if (t != 0) __hip_atomic_store(hflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
 // Queued only: the flag (1: some row is not column-sorted) lands in *host_flag
 // (pinned, host-mapped: written by the kernel itself) by the caller's next
 // stream synchronisation.
-int dev_rows_sorted_async(Context &cx, const tsg_dev_csr &M, int *host_flag, hipStream_t s) {
+int dev_rows_sorted_shares(Context &cx, const tsg_dev_csr &M, int *host_flag, SortedShares *sh, hipStream_t s) {
     *host_flag = 0;
+    *sh = SortedShares{};
     if (M.m > 0 && M.nnz > 1) {
-        int *dflag = nullptr;
-        TSG_HIP(hipHostGetDevicePointer((void **)&dflag, host_flag, 0));
+        TSG_HIP(hipHostGetDevicePointer((void **)&sh->dflag, host_flag, 0));
         const long n = std::max<long>(M.nnz, M.m);
-        k_rows_sorted_count<<<(unsigned)((n + WG * SRT_PT - 1) / (WG * SRT_PT)), WG, 0, s>>>(
-            M.rowpointer, M.columnindex, M.m, M.nnz, cx.dscratch, dflag);
+        const long nb = (n + WG * SRT_PT - 1) / (WG * SRT_PT);
+        TSG_TRY(cx.get(&sh->part, (size_t)nb));
+        sh->nb = (int)nb;
+        k_rows_sorted_count<<<(unsigned)nb, WG, 0, s>>>(M.rowpointer, M.columnindex, M.m, M.nnz, sh->part);
     }
     TSG_HIP(hipGetLastError());
     return TSG_OK;
+}
+int dev_rows_sorted_finish(Context &cx, SortedShares &sh, hipStream_t s) {
+    if (sh.part) {
+        k_rows_sorted_final<<<1, SRT_FIN, 0, s>>>(sh.part, sh.nb, sh.dflag);
+        cx.put(sh.part);  // (stream-ordered reuse)
+    }
+    sh = SortedShares{};
+    TSG_HIP(hipGetLastError());
+    return TSG_OK;
+}
+int dev_rows_sorted_async(Context &cx, const tsg_dev_csr &M, int *host_flag, hipStream_t s) {
+    SortedShares sh;
+    TSG_TRY(dev_rows_sorted_shares(cx, M, host_flag, &sh, s));
+    return dev_rows_sorted_finish(cx, sh, s);
 }
 int dev_rows_sorted(Context &cx, const tsg_dev_csr &M, bool *sorted, hipStream_t s) {
     TSG_TRY(dev_rows_sorted_async(cx, M, cx.pinned + 1, s));
@@ -2438,7 +2377,8 @@ int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_d
     TSG_TRY(cx.get(&prod, 1));
     TSG_TRY(cx.get(&C.tile_ptr, (size_t)tilemA + 1));
     const int g1 = grid_for(nunits1, 1, 16384);
-    const bool capk = el && ebnd && tilemA > 0 && !(ablate_bits() & 512);  // k_step1_cap runs (and zeroes these)
+    // k_step1_cap (element level) or k_step1_cap_tiles (tile level) runs, and zeroes these
+    const bool capk = ((el && ebnd) || !el) && tilemA > 0 && !(ablate_bits() & 512);
     if (!capk) {
         TSG_HIP(hipMemsetAsync(prod, 0, sizeof(u64), s));
         TSG_HIP(hipMemsetAsync(ucnt + nunits1, 0, sizeof(int), s));
@@ -2460,14 +2400,19 @@ int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_d
     }
     if (capk) {
         TSG_TRY(cx.get(&ubuf_off, (size_t)nunits1 + 1));
-        k_step1_cap<<<grid_for((long)tilemA * 64, WG, 8192), WG, 0, s>>>(
-            Ael->rowpointer, Ael->m, ebnd, tilemA, nwin, win, tilenB, ubuf_off,
-            fill_ebnd ? Ael->columnindex : nullptr, fill_ebnd ? Bel->rowpointer : nullptr, prod, ucnt);
+        if (el)
+            k_step1_cap<<<grid_for((long)tilemA * 64, WG, 8192), WG, 0, s>>>(
+                Ael->rowpointer, Ael->m, ebnd, tilemA, nwin, win, tilenB, ubuf_off,
+                fill_ebnd ? Ael->columnindex : nullptr, fill_ebnd ? Bel->rowpointer : nullptr, prod, ucnt);
+        else  // (the tile path's one walk: webbase's 62.5 K tile rows stored 512 MB of window bitmaps and read them back)
+            k_step1_cap_tiles<<<grid_for((long)tilemA * 64, WG, 8192), WG, 0, s>>>(
+                A.tile_ptr, A.tile_columnidx, B.tile_ptr, tilemA, nwin, win, tilenB, ubuf_off, prod, ucnt);
         fill_ebnd = false;
         TSG_HIP(hipGetLastError());
         TSG_TRY(scan_exclusive_i64(cx, ubuf_off, nunits1 + 1, s));
         TSG_TRY(read_i64(cx, ubuf_off + nunits1, &slots, s));
-        const double est = (double)Ael->nnz * ((double)Bel->nnz / (double)(Bel->m > 0 ? Bel->m : 1));
+        const double est = el ? (double)Ael->nnz * ((double)Bel->nnz / (double)(Bel->m > 0 ? Bel->m : 1))
+                              : (double)A.numtile * ((double)B.numtile / (double)(B.tilem > 0 ? B.tilem : 1));
         if ((double)slots <= 2.0 * est + (double)(1 << 26) && slots < (1LL << 31) &&
             cx.get(&ubuf, (size_t)slots + 1) == TSG_OK) {
         } else {
@@ -2494,7 +2439,7 @@ int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_d
                                                ebnd, ubuf, ubuf_off);
         else
             k_step1<0><<<g1, WG, 0, s>>>(A.tile_ptr, A.tile_columnidx, B.tile_ptr, B.tile_columnidx, tilemA, tilenB,
-                                         nwin, win, ucnt, nullptr, nullptr, prod, bmst);
+                                         nwin, win, ucnt, nullptr, nullptr, prod, bmst, 0, nullptr, ubuf, ubuf_off);
     }
     TSG_HIP(hipGetLastError());
     long long numblk64 = 0, tile_products = 0;

@@ -58,8 +58,8 @@ struct Context {
     DevicePool pool;
     int *pinned = nullptr;        // host pinned scratch for size read-backs
     long long *pinned64 = nullptr;
-    int *dscratch = nullptr;      // device counters that kernels leave zeroed (k_rows_sorted_count, k_scan_lb)
-    int *dfail = nullptr;         // device view of pinned[15]: a look-back that never resolved (k_scan_lb)
+    int *dpinned = nullptr;        // device views of the pinned scratch (kernels report
+    long long *dpinned64 = nullptr; //   small results there by system-scope stores)
     hipEvent_t ev[16];
     bool ev_ready = false;
     std::vector<void *> owned;    // outputs handed to the caller (released on reset)
@@ -120,6 +120,16 @@ int dev_tile_masks(Context &cx, const tsg_dev_csr &M, tsg_dev_tiles &t, uint16_t
 // whether every CSR row is column-sorted (synchronous)
 int dev_rows_sorted(Context &cx, const tsg_dev_csr &M, bool *sorted, hipStream_t s);
 int dev_rows_sorted_async(Context &cx, const tsg_dev_csr &M, int *host_flag, hipStream_t s);
+// the same check with its last step left to the caller: the per-workgroup shares
+// (pool-owned part, nb of them) are summed either by dev_rows_sorted_finish or
+// inside the row-merge setup's binning kernel (one launch fewer)
+struct SortedShares {
+    int *part = nullptr;
+    int nb = 0;
+    int *dflag = nullptr;  // device view of the host flag
+};
+int dev_rows_sorted_shares(Context &cx, const tsg_dev_csr &M, int *host_flag, SortedShares *sh, hipStream_t s);
+int dev_rows_sorted_finish(Context &cx, SortedShares &sh, hipStream_t s);
 int dev_tile2csr(Context &cx, const tsg_dev_tiles &C, tsg_dev_csr &out, hipStream_t s);
 // banded path (tsg_band.hip): every C row's reachable columns within one
 // window of <= 2,048 columns, the windows holding at least as many products as
@@ -164,7 +174,9 @@ constexpr long long kRowsHubProducts = 65536;
 // (peak device memory of the path: 12 B per product of staging + C + the A
 // entry table)
 constexpr long long kRowsProductSizedC = 8LL << 30;
-int dev_rows_setup_async(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPlan &p, hipStream_t s);
+// sh (optional): B's sortedness shares, summed by the binning kernel (and released)
+int dev_rows_setup_async(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPlan &p, hipStream_t s,
+                         SortedShares *sh = nullptr);
 void dev_rows_setup_read(Context &cx, RowsPlan &p);  // after the stream synchronised
 bool dev_rows_accept(const RowsPlan &p);
 void dev_rows_release(Context &cx, RowsPlan &p);

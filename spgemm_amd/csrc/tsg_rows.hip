@@ -38,7 +38,9 @@ namespace {
 
 constexpr int S16_MAX = 16;           // class S16: products (and runs) per row, 4 rows per wave
 constexpr int RS_MAX = 64;            // class S64: products (and runs) per row, a wave
-constexpr int S16_U = 4, S64_U = 2;   // rows per lane group of the S16 / S64 kernels (k_rows_small)
+constexpr int CP_CH = 2048;           // positions per chunk of the compaction (k_rows_compact)
+constexpr int S16_U = 2, S64_U = 2;   // rows per lane group of the S16 / S64 kernels (k_rows_small; S16 at
+                                      // U = 4: 95 vs 86 us on mc2depi; U = 2: 4 us under U = 1)
 // merge classes M1..M4: products and runs per row, threads per row -- each
 // sized so its LDS (16 B per product + 16 B per run) keeps several rows per CU
 // (M0..M3: run tables a few runs short of a power of two, so that 32, 16, 8
@@ -128,6 +130,115 @@ __global__ __launch_bounds__(WG) void k_rows_entries(const int *ciA, long nnzA, 
     }
 }
 
+// ---- the setup's and the row pointers' scans fused with their neighbours: at
+// mc2depi's size every launch costs 4-5 us however little it does, and the
+// generic scan is three (block sums, their scan, apply).  Up to RS_INLINE_MAX
+// tiles, each apply workgroup adds up the earlier tiles' sums itself.
+constexpr int RS_ITEMS = 16, RS_TILE = WG * RS_ITEMS;
+constexpr int RS_INLINE_MAX = 2048;
+__device__ __forceinline__ int rs_pad(int i) { return i + (i >> 4); }
+
+// the entry table with the first half of its scan: per A entry its B row's
+// range and products, per tile of RS_TILE entries their sum (E[nnzA] = 0: the
+// n+1 slot); also zeroes the binning kernel's counters
+__global__ __launch_bounds__(WG) void k_rows_entries_sum(const int *ciA, long nnzA, const int *rpB, int2 *ebnd,
+                                                         long long *E, int *cls, long long *part) {
+    __shared__ long long red[WAVES];
+    const int tid = threadIdx.x;
+    if (blockIdx.x == 0 && tid < 32) cls[tid] = 0;  // (class counts, statistics, cursors)
+    const long base = (long)blockIdx.x * RS_TILE;
+    int kk[RS_ITEMS];
+#pragma unroll
+    for (int u = 0; u < RS_ITEMS; ++u) {
+        const long a = base + u * WG + tid;
+        kk[u] = a < nnzA ? ciA[a] : 0;
+    }
+    int b0[RS_ITEMS], b1[RS_ITEMS];
+#pragma unroll
+    for (int u = 0; u < RS_ITEMS; ++u) {
+        const long a = base + u * WG + tid;
+        b0[u] = a < nnzA ? rpB[kk[u]] : 0;
+        b1[u] = a < nnzA ? rpB[kk[u] + 1] : 0;
+    }
+    long long sum = 0;
+#pragma unroll
+    for (int u = 0; u < RS_ITEMS; ++u) {
+        const long a = base + u * WG + tid;
+        if (a < nnzA) {
+            ebnd[a] = make_int2(b0[u], b1[u]);
+            E[a] = b1[u] - b0[u];
+            sum += b1[u] - b0[u];
+        } else if (a == nnzA) {
+            E[a] = 0;
+        }
+    }
+    sum = block_sum(sum, red);
+    if (tid == 0) part[blockIdx.x] = sum;
+}
+
+// per tile of RS_TILE row counts their sum
+__global__ __launch_bounds__(WG) void k_rows_count_sum(const int *a, long n, int *part) {
+    __shared__ int red[WAVES];
+    const long base = (long)blockIdx.x * RS_TILE;
+    int sum = 0;
+#pragma unroll
+    for (int u = 0; u < RS_ITEMS; ++u) {
+        const long i = base + u * WG + threadIdx.x;
+        sum += i < n ? a[i] : 0;
+    }
+    sum = block_sum(sum, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = sum;
+}
+
+// the exclusive scan's apply, the tile's prefix summed from the earlier tiles'
+// sums.  CFIRST (the row pointers, n = m + 1): also the compaction's chunk
+// table (k_rows_cfirst's job: the row holding each chunk's first position) and
+// nnz(C) (the scan's last value) into the caller's host-mapped *hnnz.
+template <class T, bool CFIRST>
+__global__ __launch_bounds__(WG) void k_rows_scan_apply(T *a, long n, const T *part, int *cfirst, int m, int *hnnz) {
+    __shared__ T tile[RS_TILE + RS_TILE / 16];
+    __shared__ T red[WAVES];
+    const int tid = threadIdx.x;
+    const long base = (long)blockIdx.x * RS_TILE;
+    T pre = 0;
+    for (int i = tid; i < (int)blockIdx.x; i += WG) pre += part[i];
+#pragma unroll
+    for (int u = 0; u < RS_ITEMS; ++u) {
+        const int li = u * WG + tid;
+        const long i = base + li;
+        tile[rs_pad(li)] = i < n ? a[i] : T(0);
+    }
+    pre = block_sum(pre, red);  // (its barriers also publish the tile)
+    T sum = 0;
+#pragma unroll
+    for (int u = 0; u < RS_ITEMS; ++u) sum += tile[rs_pad(tid * RS_ITEMS + u)];
+    T tot;
+    T off = block_excl_scan(sum, &tot, red) + pre;
+#pragma unroll
+    for (int u = 0; u < RS_ITEMS; ++u) {
+        const int li = rs_pad(tid * RS_ITEMS + u);
+        const T v = tile[li];
+        tile[li] = off;
+        if constexpr (CFIRST) {
+            const long r = base + tid * RS_ITEMS + u;
+            if (r < m) {
+                for (long long b = ((long long)off + CP_CH - 1) / CP_CH; b * CP_CH < (long long)off + v; ++b)
+                    cfirst[b] = (int)r;
+            } else if (r == m) {
+                __hip_atomic_store(hnnz, (int)off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+        off += v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < RS_ITEMS; ++u) {
+        const int li = u * WG + tid;
+        const long i = base + li;
+        if (i < n) a[i] = tile[rs_pad(li)];
+    }
+}
+
 __device__ __forceinline__ int row_class(long long P, int k) {
     if (P == 0) return -1;
     if (P <= S16_MAX && k <= S16_MAX) return 0;
@@ -152,7 +263,7 @@ __device__ __forceinline__ int row_class(long long P, int k) {
 // order into the reserved slots.
 __global__ __launch_bounds__(WG) void k_rows_bin(const int *rpA, int m, const long long *E, const long long *Etot,
                                                  int *rnnz, int4 *lists, int *cls, long long *soff,
-                                                 unsigned long long *hst) {
+                                                 unsigned long long *hst, const int *spart, int snb, int *sflag) {
     __shared__ int wc[NCLS][WAVES];
     __shared__ int gb[NCLS];
     __shared__ long long red64[WAVES];
@@ -162,6 +273,12 @@ __global__ __launch_bounds__(WG) void k_rows_bin(const int *rpA, int m, const lo
     if (blockIdx.x == 0 && tid == 0) {
         hst[2] = (unsigned long long)*Etot;
         rnnz[m] = 0;
+    }
+    if (blockIdx.x == 0 && spart) {  // B's sortedness: the shares' sum (dev_rows_sorted_shares)
+        long long v = 0;
+        for (int i = tid; i < snb; i += WG) v += spart[i];
+        v = block_sum(v, red64);
+        if (tid == 0 && v != 0) __hip_atomic_store(sflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     int n[NCLS] = {};
     long long hp = 0, pmax = 0, drp = 0, hubr = 0, hbig = 0;
@@ -295,6 +412,20 @@ __global__ __launch_bounds__(OH_NT) void k_rows_order_h(const long long *E, cons
         if (r[u].x >= 0) list[atomicAdd(&cnt[b[u]], 1)] = r[u];
 }
 
+// lane J of each row of 16 lanes, to every lane of that row: DPP row_newbcast
+// (a VALU move; __shfl inside 16 lanes is a ds_bpermute on the LDS pipe, and
+// the S16 kernel's rank loop issued 48 of them per row)
+template <int J> __device__ __forceinline__ int row_bcast16(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, 0x150 | J, 0xf, 0xf, false);
+}
+template <int V> struct IntC { static constexpr int value = V; };
+template <int J, int N, class F> __device__ __forceinline__ void static_for(F &&f) {
+    if constexpr (J < N) {
+        f(IntC<J>{});
+        static_for<J + 1, N>(f);
+    }
+}
+
 // ---- classes S16 / S64: G lanes per row (64/G rows per wave), the products
 // one per lane, ranks by counting the group's smaller (column, lane) keys.
 // Each lane group takes U rows: the rows' loads (list, entries, B) are issued
@@ -355,13 +486,17 @@ __global__ __launch_bounds__(WG) void k_rows_small(RowsArgs g) {
             inc += dpp_mov<0x143, 0xc>(0, inc);  // row_bcast:31
         }
         const int roff = sl < k[u] ? inc - len : INT_MAX;
-        P[u] = __shfl(inc, G - 1, G);
         int run = 0;
         if constexpr (G == 64) {
+            P[u] = __shfl(inc, G - 1, G);
             for (int j = 1; j < k[u]; ++j) run = (__builtin_amdgcn_readlane(roff, j) <= sl) ? j : run;
         } else {
-#pragma unroll
-            for (int j = 1; j < G; ++j) run = __shfl(roff, j, G) <= sl ? j : run;
+            static_assert(G == 16, "row broadcasts: 16-lane groups");
+            P[u] = row_bcast16<15>(inc);
+            static_for<1, 16>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                run = row_bcast16<j>(roff) <= sl ? j : run;
+            });
         }
         const int rs = __shfl(roff, run, G), rb = __shfl(bs, run, G);
         ra[u] = __shfl(av[u], run, G);
@@ -389,11 +524,12 @@ __global__ __launch_bounds__(WG) void k_rows_small(RowsArgs g) {
                 rank += kf < key[u];
             }
         } else {
-#pragma unroll
-            for (int f = 0; f < G; ++f) {
-                const u64 kf = ((u64)(u32)__shfl((int)khi, f, G) << 32) | (u32)__shfl((int)klo, f, G);
-                rank += kf < key[u];  // (lanes past P hold ~0: never below a product)
-            }
+            const u64 ku = key[u];
+            static_for<0, 16>([&](auto fc) {
+                constexpr int f = decltype(fc)::value;
+                const u64 kf = ((u64)(u32)row_bcast16<f>((int)khi) << 32) | (u32)row_bcast16<f>((int)klo);
+                rank += kf < ku;  // (lanes past P hold ~0: never below a product)
+            });
         }
         if (sl < P[u]) {
             sk[wv][u][gb + rank] = key[u];
@@ -1881,7 +2017,6 @@ __global__ __launch_bounds__(DR_NT) void k_rows_dr_fill(RowsArgs g, const int *C
 // consecutive positions): the chunk's rows from cfirst (the row holding each
 // chunk's first position), each nonempty row marks its first position in LDS, a
 // running max gives every position its row.
-constexpr int CP_CH = 2048;
 
 __global__ __launch_bounds__(WG) void k_rows_cfirst(int m, const int *Crp, int *cfirst) {
     for (int r = blockIdx.x * WG + threadIdx.x; r < m; r += gridDim.x * WG) {
@@ -1960,7 +2095,8 @@ __global__ __launch_bounds__(WG) void k_rows_compact(int m, const int *cfirst, c
 
 // Setup (stream-ordered, no host round trip): the entry table, its scan and the
 // classes; counts and statistics land in cx.pinned64[0..7) once the stream is synced.
-int dev_rows_setup_async(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPlan &p, hipStream_t s) {
+int dev_rows_setup_async(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPlan &p, hipStream_t s,
+                         SortedShares *sh) {
     static_assert(NCLS <= 8, "class counts in cls[0..8)");
     const int m = A.m;
     p = RowsPlan{};
@@ -1973,14 +2109,31 @@ int dev_rows_setup_async(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B
     TSG_TRY(cx.get(&p.cls, 32));
     TSG_TRY(cx.get(&p.rowpointer, (size_t)m + 1));
     unsigned long long *hst = reinterpret_cast<unsigned long long *>(p.cls + 8);
-    k_rows_entries<<<grid_for((long)A.nnz + 1, WG, 16384), WG, 0, s>>>(A.columnindex, A.nnz, B.rowpointer, p.ebnd,
-                                                                      p.E, p.cls);
-    TSG_HIP(hipGetLastError());
-    TSG_TRY(scan_exclusive_i64(cx, p.E, (long)A.nnz + 1, s));
+    const long ntile = ((long)A.nnz + 1 + RS_TILE - 1) / RS_TILE;
+    if (ntile <= RS_INLINE_MAX) {  // entry table + tile sums, then the apply: two launches
+        long long *part = nullptr;
+        TSG_TRY(cx.get(&part, (size_t)ntile));
+        k_rows_entries_sum<<<(unsigned)ntile, WG, 0, s>>>(A.columnindex, A.nnz, B.rowpointer, p.ebnd, p.E, p.cls,
+                                                          part);
+        k_rows_scan_apply<long long, false><<<(unsigned)ntile, WG, 0, s>>>(p.E, (long)A.nnz + 1, part, nullptr, 0,
+                                                                           nullptr);
+        TSG_HIP(hipGetLastError());
+        cx.put(part);  // (stream-ordered reuse)
+    } else {
+        k_rows_entries<<<grid_for((long)A.nnz + 1, WG, 16384), WG, 0, s>>>(A.columnindex, A.nnz, B.rowpointer,
+                                                                          p.ebnd, p.E, p.cls);
+        TSG_HIP(hipGetLastError());
+        TSG_TRY(scan_exclusive_i64(cx, p.E, (long)A.nnz + 1, s));
+    }
     // (one workgroup at least: it writes the statistics and rowpointer[m])
-    k_rows_bin<<<max(1, (m + BIN_ROWS - 1) / BIN_ROWS), WG, 0, s>>>(A.rowpointer, m, p.E, p.E + A.nnz, p.rowpointer,
-                                                                    p.lists, p.cls, p.soff, hst);
+    k_rows_bin<<<max(1, (m + BIN_ROWS - 1) / BIN_ROWS), WG, 0, s>>>(
+        A.rowpointer, m, p.E, p.E + A.nnz, p.rowpointer, p.lists, p.cls, p.soff, hst, sh ? sh->part : nullptr,
+        sh ? sh->nb : 0, sh ? sh->dflag : nullptr);
     TSG_HIP(hipGetLastError());
+    if (sh) {
+        cx.put(sh->part);  // (stream-ordered reuse)
+        *sh = SortedShares{};
+    }
     TSG_HIP(hipMemcpyAsync(cx.pinned64, p.cls, 26 * sizeof(int), hipMemcpyDeviceToHost, s));
     return TSG_OK;
 }
@@ -2200,15 +2353,38 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
     long long nnz = 0;  // (C.rowpointer[m] = 0 from the binning kernel)
     bool small = products <= 0x7fffffffLL && products * 12 <= kRowsProductSizedC;
     long long cap = 0;
+    // small with at most RS_INLINE_MAX tiles of row counts: one launch of tile
+    // sums, then one apply that also fills the compaction's chunk table and
+    // reports nnz(C) through the host-mapped pinned64[15] (no copy back)
+    const long rtile = ((long)m + 1 + RS_TILE - 1) / RS_TILE;
+    const bool fused_scan = small && rtile <= RS_INLINE_MAX;
+    int *const hnnz = reinterpret_cast<int *>(cx.pinned64 + 15);
+    int *cfirst = nullptr;
     auto scan_alloc = [&]() -> int {
         if (small) {
-            TSG_TRY(scan_exclusive_i32(cx, C.rowpointer, (long)m + 1, s));
+            if (fused_scan) {
+                int *part = nullptr;
+                TSG_TRY(cx.get(&part, (size_t)rtile));
+                TSG_TRY(cx.get(&cfirst, (size_t)((products + CP_CH - 1) / CP_CH) + 1));
+                k_rows_count_sum<<<(unsigned)rtile, WG, 0, s>>>(C.rowpointer, (long)m + 1, part);
+                k_rows_scan_apply<int, true><<<(unsigned)rtile, WG, 0, s>>>(
+                    C.rowpointer, (long)m + 1, part, cfirst, m, reinterpret_cast<int *>(cx.dpinned64 + 15));
+                TSG_HIP(hipGetLastError());
+                cx.put(part);  // (stream-ordered reuse)
+            } else {
+                TSG_TRY(scan_exclusive_i32(cx, C.rowpointer, (long)m + 1, s));
+            }
             if (cx.get(&C.columnindex, (size_t)products + 1) != TSG_OK ||
                 cx.get(&C.value, (size_t)products + 1) != TSG_OK) {
                 cx.put(C.columnindex);
                 C.columnindex = nullptr;
                 small = false;  // (the scan's total is read back below)
-                TSG_TRY(read_i32(cx, C.rowpointer + m, &C.nnz, s));
+                if (fused_scan) {
+                    TSG_TRY(stream_wait(s));
+                    C.nnz = *hnnz;
+                } else {
+                    TSG_TRY(read_i32(cx, C.rowpointer + m, &C.nnz, s));
+                }
                 nnz = C.nnz;
             }
         } else {  // the checked scan (nnz(C) past int32 fails)
@@ -2237,7 +2413,6 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
         }
         return TSG_OK;
     };
-    int *cfirst = nullptr;
     {
         TSG_TRY(classes());
         // (the numeric phase: to the class kernels' end, or -- with windowed or
@@ -2268,17 +2443,20 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
         if (ev && fills) TSG_HIP(hipEventRecord(ev[5], s));
         if (cap > 0) {
             const int nch = (int)((cap + CP_CH - 1) / CP_CH);
-            TSG_TRY(cx.get(&cfirst, (size_t)nch + 1));
-            k_rows_cfirst<<<grid_for(m, WG, 8192), WG, 0, s>>>(m, C.rowpointer, cfirst);
-            TSG_HIP(hipGetLastError());
+            if (!cfirst) {  // (the fused scan filled it)
+                TSG_TRY(cx.get(&cfirst, (size_t)nch + 1));
+                k_rows_cfirst<<<grid_for(m, WG, 8192), WG, 0, s>>>(m, C.rowpointer, cfirst);
+                TSG_HIP(hipGetLastError());
+            }
             k_rows_compact<<<nch, WG, 0, s>>>(m, cfirst, soff, C.rowpointer, Scol, Sval, C.columnindex, C.value);
         }
         TSG_HIP(hipGetLastError());
     }
-    if (small) TSG_HIP(hipMemcpyAsync(cx.pinned64 + 15, C.rowpointer + m, sizeof(int), hipMemcpyDeviceToHost, s));
+    if (small && !fused_scan)
+        TSG_HIP(hipMemcpyAsync(cx.pinned64 + 15, C.rowpointer + m, sizeof(int), hipMemcpyDeviceToHost, s));
     if (ev) TSG_HIP(hipEventRecord(ev[3], s));
     TSG_TRY(stream_wait(s));
-    if (small) nnz = *reinterpret_cast<const int *>(cx.pinned64 + 15);
+    if (small) nnz = *hnnz;
     C.nnz = (int)nnz;
     cx.put(cfirst);
     dev_rows_release(cx, p);

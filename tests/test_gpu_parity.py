@@ -390,3 +390,50 @@ def test_tiled_api_csr_streaming_real_values():
     np.testing.assert_array_equal(got[2], ref[2])
     np.testing.assert_array_equal(got[3], ref[3])
     assert np.all(np.abs(got[4] - ref[4]) <= RTOL * mag)
+
+
+def test_tiled_csr_route_wide_tile_rows_and_empty_tiles():
+    """The 16x16 tiled route through the CSR C (tsg_ctiles.hip): one tile row
+    spanning ~20 units of <= 992 tiles (B's row 0 reaches 20,000 tile columns),
+    several rows of the tile row in the same tiles (multi-row masks and Ptr),
+    and step-1 tiles whose element product is empty (A's column 1 selects an
+    empty B row inside a tile pair that the tile pattern matches).  Every C
+    tile array against the oracle's tiled product, CSR C against Gustavson."""
+    nt = 20000
+    n = 16 * nt
+    rows = {0: [0, 1], 3: [0], 7: [0, 2], 15: [2], 16: [0], 40: [1, 2]}
+    m = 48
+    rp = np.zeros(m + 1, np.int64)
+    for r, cs in rows.items():
+        rp[r + 1] = len(cs)
+    rp = np.cumsum(rp).astype(np.int32)
+    ci = np.concatenate([np.array(rows[r], np.int32) for r in sorted(rows)])
+    va = np.arange(1, len(ci) + 1, dtype=np.float64)
+    # B (n x n, only rows 0 and 2 non-empty): row 0 hits column 16j + (j % 16) for
+    # every tile column j, row 2 every 7th tile column; row 1 is empty
+    b0 = 16 * np.arange(nt) + np.arange(nt) % 16
+    b2 = 16 * np.arange(0, nt, 7) + 3
+    brp = np.zeros(n + 1, np.int64)
+    brp[1] = len(b0)
+    brp[3] = len(b2)
+    brp = np.cumsum(brp).astype(np.int32)
+    bci = np.concatenate([b0, b2]).astype(np.int32)
+    bvv = (np.arange(len(bci)) % 10 + 1).astype(np.float64)
+    A = T.Matrix.from_csr(m, n, rp, ci, va)
+    B = T.Matrix.from_csr(n, n, brp, bci, bvv)
+    oA = O.OMat.from_csr(m, n, rp, ci, va)
+    oB = O.OMat.from_csr(n, n, brp, bci, bvv)
+    T.csr2tile_row_major(A, 16, 16)
+    T.csr2tile_col_major(B, 16, 16)
+    O.csr2tile_row_major(oA, 16, 16)
+    O.csr2tile_col_major(oB, 16, 16)
+    Cm, info = T.tilespgemm(A, B, 16, 16)
+    oC = O.tilespgemm(oA, oB, 16, 16)
+    ct, oct_ = Cm.tiles(16, 1), O.c_tiles(oC, 16)
+    for k in C_KEYS:
+        np.testing.assert_array_equal(ct[k], oct_[k], err_msg="C " + k)
+    assert int(ct["tile_ptr"][1]) > 5 * 992  # the first tile row spans several units
+    tn = np.diff(ct["tile_nnz"][: len(ct["tile_columnidx"]) + 1])
+    assert (tn == 0).any()  # structurally present, numerically empty tiles
+    T.tile2csr(Cm, 16, 16)
+    assert_csr_equal(Cm.csr(), O.gustavson(oA, oB).csr())

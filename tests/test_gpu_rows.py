@@ -411,3 +411,23 @@ def test_repeated_column_in_b_row_routes_to_tiles(monkeypatch):
     arows = [np.sort(np.concatenate([[0], rng.choice(np.arange(1, n), size=3, replace=False)])) for _ in range(40)]
     A = _csr(40, n, arows)
     _check(A, B, real=True, seed=62, path=T.PATH_TILES)
+
+
+def test_rows_scans_past_the_fused_tiles():
+    """More than RS_INLINE_MAX = 2,048 tiles of 4,096 A entries and of row
+    counts (9 * 10^6 rows, one entry each: A a permutation with two shuffled
+    blocks, C = A*A): the setup's entry scan and the row-pointer scan take the
+    generic three-launch scans and k_rows_cfirst instead of the fused kernels.
+    C is A's permutation applied twice -- checked exactly with numpy."""
+    m = 9_000_000
+    rng = np.random.default_rng(5)
+    ci = rng.permutation(m).astype(np.int32)
+    rp = np.arange(m + 1, dtype=np.int32)
+    vv = rng.uniform(0.5, 2.0, m)
+    A = T.Matrix.from_csr(m, m, rp, ci, vv)
+    Cm, st = T.spgemm(A, T.Matrix.alias(A))
+    got = Cm.csr()
+    np.testing.assert_array_equal(got[2], rp)
+    np.testing.assert_array_equal(got[3], ci[ci])
+    np.testing.assert_array_equal(got[4], vv * vv[ci])  # one product per entry: exact
+    assert st["path"] == T.PATH_ROWS and st["nnzC"] == m
