@@ -46,51 +46,26 @@ __global__ __launch_bounds__(WG) void k_ct_fill(const int *tptr, int tilem, cons
         if (i == tilem - 1) *nu = ubase[tilem];
     }
 }
-// Each unit's record (CT_REC ints), a wave per unit, lane r < 16 = row r of the
-// unit's tile row: rec[0..16) the row segments' starts in the unit's columns
-// (a binary search of the row for the unit's first tile column, the row start
-// for a tile row's first unit), rec[16..33) the segments' lengths scanned,
-// rec[33] the unit's first offset in the tiled arrays (rowpointer[16i] + the
-// row nonzeros before the segments), rec[34..37) (i, c0, c1).  The searches run
-// here, all independent, and k_ctiles reads its unit's whole description in one
-// round trip instead of three dependent ones.
-constexpr int CT_REC = 40;
+// ulo[16u + r]: where row r of unit u's tile row reaches the unit's first tile
+// column (the row start for a tile row's first unit).  A thread per (unit,
+// row): the binary searches run here, all independent, rather than on each
+// unit workgroup's critical path.
 __global__ __launch_bounds__(WG) void k_ct_bounds(int m, const int *Crp, const int *Ccol, const int *tptr,
-                                                  const int *tcol, const int4 *units, const int *nu, int *urec) {
-    const int lane = lane_id();
-    const long nx = *nu;
-    for (long u = ((long)blockIdx.x * WG + threadIdx.x) >> 6; u < nx; u += ((long)gridDim.x * WG) >> 6) {
-        const int4 un = units[u];
-        const bool last = un.z == tptr[un.x + 1];  // (the tile row's last unit)
-        const int r = min(lane, 15);
-        const int row = min(16 * un.x + r, m);
-        const int rs = Crp[row], re = Crp[min(row + 1, m)];
-        int lo = rs, hi = re;
-        if (lane < 16 && un.y != tptr[un.x] && row < m) lo = lower_bound_dev(Ccol, rs, re, 16 * tcol[un.y]);
-        if (lane < 16 && !last && row < m) hi = lower_bound_dev(Ccol, lo, re, 16 * tcol[un.z]);
-        const int len = lane < 16 ? hi - lo : 0, skip = lane < 16 ? lo - rs : 0;
-        const int inc = wave_incl_scan_dpp(len);
-        const int sk = wave_last(wave_incl_scan_dpp(skip));
-        int *rec = urec + u * CT_REC;
-        if (lane < 16) {
-            rec[lane] = lo;
-            rec[17 + lane] = inc;
-        }
-        if (lane == 0) {
-            rec[16] = 0;
-            rec[33] = __shfl(rs, 0, 64) + sk;
-            rec[34] = un.x;
-            rec[35] = un.y;
-            rec[36] = un.z;
-        }
+                                                  const int *tcol, const int4 *units, const int *nu, int *ulo) {
+    const long nx = 16L * *nu;
+    for (long x = (long)blockIdx.x * WG + threadIdx.x; x < nx; x += (long)gridDim.x * WG) {
+        const int4 un = units[x >> 4];
+        const int row = min(16 * un.x + (int)(x & 15), m);
+        const int b0 = Crp[row];
+        ulo[x] = (un.y == tptr[un.x] || row == m) ? b0 : lower_bound_dev(Ccol, b0, Crp[row + 1], 16 * tcol[un.y]);
     }
 }
 
 // A workgroup per unit (tile row i = rows 16i..16i+15, tiles [c0, c1) with
 // columns tcl[0..n)):
-//   * the unit's record (k_ct_bounds: its 16 row segments, their lengths
-//     scanned, its first tile offset = rowptr[16i] + the row nonzeros before
-//     the segments; units are independent, no carry) in one load;
+//   * row r's nonzeros in the unit's columns: [ulo[16u+r], the next unit's
+//     ulo or the row end); the unit's first tile offset = rowptr[16i] + the
+//     row nonzeros before the range (units are independent: no carry);
 //   * the unit's nonzeros, flat over its 16 row segments, CT_EPT per thread in
 //     registers (columns, values, rows; every load independent), in batches
 //     past CT_EB;
@@ -102,24 +77,43 @@ __global__ __launch_bounds__(WG) void k_ct_bounds(int m, const int *Crp, const i
 //   * pass B: each nonzero to offset + Ptr[row] + its rank in the row's mask
 //     word (the popcount of the mask bits of smaller columns: the CSR row is
 //     column-sorted, a column appears once), local column and value.
-__global__ __launch_bounds__(CT_NT) void k_ctiles(const int *Ccol, const double *Cval, const int *tcol,
-                                                  const int *nu, const int *urec, int *tnnz, u16 *Ptr, u16 *mask,
-                                                  u16 *Col, double *Val, int *fail) {
+__global__ __launch_bounds__(CT_NT) void k_ctiles(int m, const int *Crp, const int *Ccol, const double *Cval,
+                                                  const int *tptr, const int *tcol, const int4 *units, const int *nu,
+                                                  const int *ulo, int *tnnz, u16 *Ptr, u16 *mask, u16 *Col,
+                                                  double *Val, int *fail) {
     __shared__ __align__(16) u32 mk[CT_TC * 8];  // per unit tile: 16 mask words, two per u32 (row 2j low)
     __shared__ int toff[CT_TC];
     __shared__ int tcl[CT_TC];
-    __shared__ int rec[CT_REC];  // the unit's record (k_ct_bounds): lo[16], fpre[17], base, i, c0, c1
-    __shared__ int red[CT_NW];
+    __shared__ int rs[16], lo[16], fpre[17];
+    __shared__ int red[CT_NW + 1];
     const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
     const int u = blockIdx.x;
     if (u >= *nu) return;  // (the grid is an upper bound of the units)
-    if (tid < CT_REC) rec[tid] = urec[(long)u * CT_REC + tid];
-    __syncthreads();
-    const int *const lo = rec, *const fpre = rec + 16;
-    const int c0 = rec[35], n = rec[36] - c0;
-    const int nflat = fpre[16], base = rec[33];
+    const int4 un = units[u];
+    const int i = un.x, c0 = un.y, c1 = un.z, n = c1 - c0;
+    const int r0 = 16 * i;
+    if (tid < 16) {
+        const int row = min(r0 + tid, m);
+        rs[tid] = Crp[row];
+        lo[tid] = ulo[16 * u + tid];
+        fpre[tid + 1] = c1 == tptr[i + 1] ? Crp[min(row + 1, m)] : ulo[16 * (u + 1) + tid];  // (the end, for now)
+    }
     for (int t = tid; t < n; t += CT_NT) tcl[t] = tcol[c0 + t];
     for (int w = tid; w < 8 * n; w += CT_NT) mk[w] = 0u;
+    __syncthreads();
+    if (wv == 0) {  // segment lengths scanned; the unit's first offset
+        const int v = lane < 16 ? fpre[lane + 1] - lo[lane] : 0;
+        const int skip = lane < 16 ? lo[lane] - rs[lane] : 0;
+        const int inc = wave_incl_scan_dpp(v);
+        const int sk = wave_last(wave_incl_scan_dpp(skip));
+        if (lane < 16) fpre[lane + 1] = inc;  // (lane l: the inclusive prefix of segments 0..l)
+        if (lane == 0) {
+            fpre[0] = 0;
+            red[CT_NW] = rs[0] + sk;
+        }
+    }
+    __syncthreads();
+    const int nflat = fpre[16], base = red[CT_NW];
     const int nbat = (nflat + CT_EB - 1) / CT_EB;  // (workgroup-uniform)
     int cc[CT_EPT], rr[CT_EPT];                    // a batch: columns (-1: none), rows, values
     double xv[CT_EPT];
@@ -151,8 +145,7 @@ __global__ __launch_bounds__(CT_NT) void k_ctiles(const int *Ccol, const double 
         }
         return tcl[a] == tc ? a : -1;
     };
-    if (nbat == 1) load_batch(0);  // (in flight with tcl's loads)
-    __syncthreads();                // (tcl and the zeroed masks)
+    if (nbat == 1) load_batch(0);
     // pass A: the masks
     for (int bb = 0; bb < nbat; ++bb) {  // (workgroup-uniform)
         if (nbat > 1) load_batch(bb);
@@ -258,13 +251,13 @@ int dev_ctiles_from_csr(Context &cx, const tsg_dev_csr &Cc, tsg_dev_tiles &C, hi
     TSG_TRY(cx.get(&C.tile_csr_Col, (size_t)Cc.nnz + 1));
     TSG_TRY(cx.get(&C.tile_csr_Value, (size_t)Cc.nnz + 1));
     C.nnz = Cc.nnz;
-    int *fail = nullptr, *ubase = nullptr, *urec = nullptr;
+    int *fail = nullptr, *ubase = nullptr, *ulo = nullptr;
     int4 *units = nullptr;
     const long umax = (long)C.numtile / CT_TC + C.tilem + 1;  // (units: an upper bound)
     TSG_TRY(cx.get(&fail, 2));
     TSG_TRY(cx.get(&ubase, (size_t)C.tilem + 1));
     TSG_TRY(cx.get(&units, (size_t)umax));
-    TSG_TRY(cx.get(&urec, CT_REC * (size_t)umax));
+    TSG_TRY(cx.get(&ulo, 16 * (size_t)umax + 16));
     TSG_HIP(hipMemsetAsync(fail, 0, 2 * sizeof(int), s));
     cx.pinned[9] = Cc.nnz;  // tile_nnz[numtile] = nnz(C)
     TSG_HIP(hipMemcpyAsync(C.tile_nnz + C.numtile, cx.pinned + 9, sizeof(int), hipMemcpyHostToDevice, s));
@@ -273,11 +266,11 @@ int dev_ctiles_from_csr(Context &cx, const tsg_dev_csr &Cc, tsg_dev_tiles &C, hi
         TSG_HIP(hipMemsetAsync(ubase + C.tilem, 0, sizeof(int), s));
         TSG_TRY(scan_exclusive_i32(cx, ubase, (long)C.tilem + 1, s));
         k_ct_fill<<<grid_for(C.tilem, WG, 4096), WG, 0, s>>>(C.tile_ptr, C.tilem, ubase, units, fail + 1);
-        k_ct_bounds<<<grid_for(64 * umax, WG, 16384), WG, 0, s>>>(C.m, Cc.rowpointer, Cc.columnindex, C.tile_ptr,
-                                                                  C.tile_columnidx, units, fail + 1, urec);
-        k_ctiles<<<(unsigned)umax, CT_NT, 0, s>>>(Cc.columnindex, Cc.value, C.tile_columnidx, fail + 1, urec,
-                                                  C.tile_nnz, C.tile_csr_Ptr, C.mask, C.tile_csr_Col,
-                                                  C.tile_csr_Value, fail);
+        k_ct_bounds<<<grid_for(16 * umax, WG, 16384), WG, 0, s>>>(C.m, Cc.rowpointer, Cc.columnindex, C.tile_ptr,
+                                                                  C.tile_columnidx, units, fail + 1, ulo);
+        k_ctiles<<<(unsigned)umax, CT_NT, 0, s>>>(C.m, Cc.rowpointer, Cc.columnindex, Cc.value, C.tile_ptr,
+                                                  C.tile_columnidx, units, fail + 1, ulo, C.tile_nnz, C.tile_csr_Ptr,
+                                                  C.mask, C.tile_csr_Col, C.tile_csr_Value, fail);
     }
     TSG_HIP(hipGetLastError());
     cx.pinned[8] = 0;
@@ -285,7 +278,7 @@ int dev_ctiles_from_csr(Context &cx, const tsg_dev_csr &Cc, tsg_dev_tiles &C, hi
     cx.put(fail);  // (stream-ordered reuse: the copies above precede any later use)
     cx.put(ubase);
     cx.put(units);
-    cx.put(urec);
+    cx.put(ulo);
     return TSG_OK;
 }
 

@@ -1089,38 +1089,51 @@ __global__ __launch_bounds__(RH_NT) void k_rows_bitmap(RowsArgs g, int *Tc, doub
     __shared__ u16 g4[RH_NGRP];       // each 4-word group's bits before it in its block
     __shared__ int blk[RH_NBLK];      // each block's bits before it in the window
     __shared__ WalkTab wt;
-    __shared__ int red[2 * (RH_NT / 64)];
+    __shared__ int red[3 * (RH_NT / 64)];
     constexpr int NW = RH_NT / 64;
     RP_INIT
     const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
     const int4 le = g.list[blockIdx.x];
     const int r = le.x, a0 = le.y, k = le.z;
     const long long base = g.E[a0];
-    // the row's columns [lo, hi]
-    int lo = INT_MAX, hi = -1;
-    for (int j = tid; j < k; j += RH_NT) {
-        const int2 be = g.ebnd[a0 + j];
-        if (be.y > be.x) {
-            lo = min(lo, g.Bcol[be.x]);
-            hi = max(hi, g.Bcol[be.y - 1]);
-        }
-    }
-    lo = wave_last(wave_incl_dpp(lo, INT_MAX, OpMin{}));
-    hi = wave_last(wave_incl_dpp(hi, INT_MIN, OpMax{}));
-    if (lane == 0) {
-        red[wv] = lo;
-        red[NW + wv] = hi;
-    }
-    __syncthreads();
-    lo = red[0];
-    hi = red[NW];
-    for (int w = 1; w < NW; ++w) {
-        lo = min(lo, red[w]);
-        hi = max(hi, red[NW + w]);
-    }
-    const int P = (int)(g.E[a0 + k] - base);  // (<= kRowsHubProducts: hub rows left above)
     // (rows of more runs or a wider span: the windowed kernels, k_rows_w*)
-    if (k > OW_RUNS || (long long)hi - lo >= RH_SPAN) return;  // (workgroup-uniform)
+    if (k > OW_RUNS) return;  // (workgroup-uniform)
+    const int P = (int)(g.E[a0 + k] - base);  // (<= kRowsHubProducts: hub rows left above)
+    // run table (2 runs per thread; the walk table's LDS): product prefix, B
+    // start -- and from the same loads the row's columns [lo, hi]
+    int *const opre = reinterpret_cast<int *>(&wt);
+    int *const obs = opre + OW_RUNS;
+    int lo = INT_MAX, hi = -1;
+    {
+        int2 be0 = make_int2(0, 0), be1 = make_int2(0, 0);
+        if (2 * tid < k) be0 = g.ebnd[a0 + 2 * tid];
+        if (2 * tid + 1 < k) be1 = g.ebnd[a0 + 2 * tid + 1];
+        const int l0 = be0.y - be0.x, l1 = be1.y - be1.x;
+        const int f0 = l0 > 0 ? g.Bcol[be0.x] : INT_MAX, e0 = l0 > 0 ? g.Bcol[be0.y - 1] : -1;
+        const int f1 = l1 > 0 ? g.Bcol[be1.x] : INT_MAX, e1 = l1 > 0 ? g.Bcol[be1.y - 1] : -1;
+        const int inc = wave_incl_scan_dpp(l0 + l1);
+        lo = wave_last(wave_incl_dpp(min(f0, f1), INT_MAX, OpMin{}));
+        hi = wave_last(wave_incl_dpp(max(e0, e1), INT_MIN, OpMax{}));
+        if (lane == 63) red[wv] = inc;
+        if (lane == 0) {
+            red[NW + wv] = lo;
+            red[2 * NW + wv] = hi;
+        }
+        __syncthreads();
+        int woff = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            woff += w < wv ? red[w] : 0;
+            lo = min(lo, red[NW + w]);
+            hi = max(hi, red[2 * NW + w]);
+        }
+        const int ex = woff + inc - l0 - l1;
+        opre[2 * tid] = ex;
+        opre[2 * tid + 1] = ex + l0;
+        obs[2 * tid] = be0.x;
+        obs[2 * tid + 1] = be1.x;
+    }
+    if ((long long)hi - lo >= RH_SPAN) return;  // (workgroup-uniform)
     {
         // one window, ONE walk: each product's column and value gathered together
         // once -- the first OW_CH products held in registers, the rest (rows past
@@ -1128,27 +1141,6 @@ __global__ __launch_bounds__(RH_NT) void k_rows_bitmap(RowsArgs g, int *Tc, doub
         // LDS then holds the columns at their ranks (copied out coalesced) and
         // the values (ds_add_f64 at the ranks, copied out), OW_CV / OW_CH ranks
         // per pass.  No global atomic, no second walk over B.
-        // run table (2 runs per thread; the walk table's LDS): product prefix, B start
-        int *const opre = reinterpret_cast<int *>(&wt);
-        int *const obs = opre + OW_RUNS;
-        __syncthreads();  // (red: the span's reduction read above)
-        {
-            int2 be0 = make_int2(0, 0), be1 = make_int2(0, 0);
-            if (2 * tid < k) be0 = g.ebnd[a0 + 2 * tid];
-            if (2 * tid + 1 < k) be1 = g.ebnd[a0 + 2 * tid + 1];
-            const int l0 = be0.y - be0.x, l1 = be1.y - be1.x;
-            const int inc = wave_incl_scan_dpp(l0 + l1);
-            if (lane == 63) red[wv] = inc;
-            __syncthreads();
-            int woff = 0;
-#pragma unroll
-            for (int w = 0; w < NW; ++w) woff += w < wv ? red[w] : 0;
-            const int ex = woff + inc - l0 - l1;
-            opre[2 * tid] = ex;
-            opre[2 * tid + 1] = ex + l0;
-            obs[2 * tid] = be0.x;
-            obs[2 * tid + 1] = be1.x;
-        }
         __shared__ long long s_toff;
         if (tid == 0 && P > OW_CH) s_toff = (long long)atomicAdd(tcur, (unsigned long long)(P - OW_CH));
         const int nwd = (int)(((long long)hi - lo + 64) >> 6);
@@ -1177,26 +1169,40 @@ __global__ __launch_bounds__(RH_NT) void k_rows_bitmap(RowsArgs g, int *Tc, doub
                     x4[u] = g.vA[a0 + jr] * g.Bval[pp];
                 }
         };
+        // the first RH_PPT products per thread: every run search first (LDS
+        // only), then all their loads in flight together -- one memory round
+        // trip for the register share instead of one per group of four (the
+        // walk was 20 of a class-H row's 27 us on webbase)
         int cc[RH_PPT];
         double xx[RH_PPT];
+        {
+            int pa[RH_PPT], jr[RH_PPT];
 #pragma unroll
-        for (int j0 = 0; j0 < RH_PPT; j0 += 4) {
-            int c4[4];
-            double x4[4];
-            if (j0 * RH_NT < P) {  // (workgroup-uniform)
-                gather4(j0, c4, x4);
-            } else {
+            for (int j0 = 0; j0 < RH_PPT; j0 += 4) {
+                int b[4], len2[4], q[4];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
-                    c4[u] = -1;
-                    x4[u] = 0.0;
+                    q[u] = (j0 + u) * RH_NT + tid;
+                    b[u] = 0;
+                    len2[u] = q[u] < P ? k : 0;
+                }
+                const bool ub[4] = {true, true, true, true};
+                if (j0 * RH_NT < P) search_ilp(opre, b, len2, q, ub);  // (workgroup-uniform)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    jr[j0 + u] = q[u] < P ? b[u] - 1 : -1;
+                    pa[j0 + u] = q[u] < P ? obs[b[u] - 1] + q[u] - opre[b[u] - 1] : 0;
                 }
             }
+            double bv[RH_PPT], av[RH_PPT];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                cc[j0 + u] = c4[u];
-                xx[j0 + u] = x4[u];
+            for (int j = 0; j < RH_PPT; ++j) {
+                cc[j] = jr[j] >= 0 ? g.Bcol[pa[j]] - lo : -1;
+                bv[j] = jr[j] >= 0 ? g.Bval[pa[j]] : 0.0;
+                av[j] = jr[j] >= 0 ? g.vA[a0 + jr[j]] : 0.0;
             }
+#pragma unroll
+            for (int j = 0; j < RH_PPT; ++j) xx[j] = av[j] * bv[j];
         }
 #pragma unroll
         for (int j = 0; j < RH_PPT; ++j)
