@@ -371,10 +371,21 @@ def main():
         # --leg tiled): every kernel's bytes over the calls, which also spreads the
         # one-time csr2tile of A and B (outside the timed region) over the calls
         pfile = pmc_file(out["config"]["workload"], args.pmc_from)
-        _, allk = pmc_traffic([], pfile)
         rl = out["roofline"]
-        rl["traffic_all_kernels"] = allk
+        rl["traffic_all_kernels"] = None
+        if pfile:
+            # the compute kernels' bytes per call; the runtime's copy kernels
+            # (__amd_rocclr_*: the tiles' uploads and the tiled C's downloads,
+            # outside the timed region as in the reference) left out
+            d = json.load(open(pfile))
+            calls = (d.get("_per_call") or {}).get("calls")
+            tot = sum(v["hbm_bytes_per_dispatch"] * v["dispatches"] for k, v in d.items()
+                      if isinstance(v, dict) and v.get("hbm_bytes_per_dispatch") and v.get("dispatches")
+                      and not k.startswith("__amd_rocclr"))
+            rl["traffic_all_kernels"] = round(tot / calls) if calls else None
+        allk = rl["traffic_all_kernels"]
         rl["traffic_over_b_alg"] = round(allk / rl["algorithmic_bytes"], 3) if allk else None
+        rl["layout_traffic_ratio"] = round(allk / rl["layout_bytes"], 3) if allk else None
         rl["traffic_source"] = os.path.relpath(pfile, REPO) if pfile else None
         print(json.dumps(out), flush=True)
         return

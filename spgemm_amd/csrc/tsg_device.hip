@@ -1342,31 +1342,35 @@ __global__ __launch_bounds__(WG) void k_entry_bounds(const int *ciA, long nnzA, 
 // workgroup do not cancel locally -- a row's first entry and the row itself
 // sit in different workgroups -- and one atomic per workgroup on a common
 // counter serialised: 47 us on mc2depi, 88 on webbase.)
-constexpr int SRT_PT = 4;  // entries (and rows) per thread, their loads issued together
+constexpr int SRT_PT = 4;        // entries (and rows) per thread, their loads issued together
+constexpr int SRT_MAXB = 4096;   // workgroups at most (grid-stride past it): few shares to sum
 __global__ __launch_bounds__(WG) void k_rows_sorted_count(const int *rp, const int *ci, int m, int nnz, int *part) {
     __shared__ int red[WAVES];
     const int tid = threadIdx.x;
-    const long b0 = (long)blockIdx.x * WG * SRT_PT;
-    int c0[SRT_PT], c1[SRT_PT], r0[SRT_PT], r1[SRT_PT];
+    const long n = max((long)nnz, (long)m);
+    int v = 0;
+    for (long b0 = (long)blockIdx.x * WG * SRT_PT; b0 < n; b0 += (long)gridDim.x * WG * SRT_PT) {
+        int c0[SRT_PT], c1[SRT_PT], r0[SRT_PT], r1[SRT_PT];
 #pragma unroll
-    for (int u = 0; u < SRT_PT; ++u) {
-        const long p = b0 + u * WG + tid;
-        const bool okp = p >= 1 && p < nnz, okr = p < m;
-        c0[u] = okp ? ci[p - 1] : 0;
-        c1[u] = okp ? ci[p] : 1;
-        r0[u] = okr ? rp[p] : 0;
-        r1[u] = okr ? rp[p + 1] : 0;
+        for (int u = 0; u < SRT_PT; ++u) {
+            const long p = b0 + u * WG + tid;
+            const bool okp = p >= 1 && p < nnz, okr = p < m;
+            c0[u] = okp ? ci[p - 1] : 0;
+            c1[u] = okp ? ci[p] : 1;
+            r0[u] = okr ? rp[p] : 0;
+            r1[u] = okr ? rp[p + 1] : 0;
+        }
+        int f0[SRT_PT], f1[SRT_PT];
+#pragma unroll
+        for (int u = 0; u < SRT_PT; ++u) {
+            v += c1[u] <= c0[u];
+            const bool st = r0[u] >= 1 && r0[u] < r1[u];  // a non-empty row past the first entry
+            f0[u] = st ? ci[r0[u] - 1] : 0;
+            f1[u] = st ? ci[r0[u]] : 1;
+        }
+#pragma unroll
+        for (int u = 0; u < SRT_PT; ++u) v -= f1[u] <= f0[u];
     }
-    int v = 0, f0[SRT_PT], f1[SRT_PT];
-#pragma unroll
-    for (int u = 0; u < SRT_PT; ++u) {
-        v += c1[u] <= c0[u];
-        const bool st = r0[u] >= 1 && r0[u] < r1[u];  // a non-empty row past the first entry
-        f0[u] = st ? ci[r0[u] - 1] : 0;
-        f1[u] = st ? ci[r0[u]] : 1;
-    }
-#pragma unroll
-    for (int u = 0; u < SRT_PT; ++u) v -= f1[u] <= f0[u];
     v = block_sum(v, red);
     if (tid == 0) part[blockIdx.x] = v;
 }
@@ -1395,7 +1399,7 @@ int dev_rows_sorted_shares(Context &cx, const tsg_dev_csr &M, int *host_flag, So
     if (M.m > 0 && M.nnz > 1) {
         TSG_HIP(hipHostGetDevicePointer((void **)&sh->dflag, host_flag, 0));
         const long n = std::max<long>(M.nnz, M.m);
-        const long nb = (n + WG * SRT_PT - 1) / (WG * SRT_PT);
+        const long nb = std::min<long>((n + WG * SRT_PT - 1) / (WG * SRT_PT), SRT_MAXB);
         TSG_TRY(cx.get(&sh->part, (size_t)nb));
         sh->nb = (int)nb;
         k_rows_sorted_count<<<(unsigned)nb, WG, 0, s>>>(M.rowpointer, M.columnindex, M.m, M.nnz, sh->part);

@@ -275,7 +275,8 @@ __global__ __launch_bounds__(WG) void k_rows_bin(const int *rpA, int m, const lo
         rnnz[m] = 0;
     }
     if (blockIdx.x == 0 && spart) {  // B's sortedness: the shares' sum (dev_rows_sorted_shares)
-        long long v = 0;
+        long long v = 0;  // (<= 4,096 shares: SRT_MAXB)
+#pragma unroll 8
         for (int i = tid; i < snb; i += WG) v += spart[i];
         v = block_sum(v, red64);
         if (tid == 0 && v != 0) __hip_atomic_store(sflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -2024,10 +2025,18 @@ __global__ __launch_bounds__(DR_NT) void k_rows_dr_fill(RowsArgs g, const int *C
 // chunk's first position), each nonempty row marks its first position in LDS, a
 // running max gives every position its row.
 
-__global__ __launch_bounds__(WG) void k_rows_cfirst(int m, const int *Crp, int *cfirst) {
-    for (int r = blockIdx.x * WG + threadIdx.x; r < m; r += gridDim.x * WG) {
-        const int s = Crp[r], e = Crp[r + 1];
-        for (long long b = ((long long)s + CP_CH - 1) / CP_CH; b * CP_CH < e; ++b) cfirst[b] = r;
+__global__ __launch_bounds__(WG) void k_rows_cfirst(int m, const int *Crp, long nch, int *cfirst) {
+    // a thread per chunk: the last row starting at or before its first position
+    // (a row per thread walked its chunks serially: 83 us on the mawi prefix,
+    // 3,360 rows of ~445 K nonzeros)
+    for (long b = (long)blockIdx.x * WG + threadIdx.x; b < nch; b += (long)gridDim.x * WG) {
+        const long long pos = b * CP_CH;
+        int lo = 0, hi = m;  // the answer lies in [lo, hi): Crp[lo] <= pos
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if ((long long)Crp[mid] <= pos) lo = mid; else hi = mid;
+        }
+        cfirst[b] = lo;
     }
 }
 
@@ -2451,7 +2460,7 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
             const int nch = (int)((cap + CP_CH - 1) / CP_CH);
             if (!cfirst) {  // (the fused scan filled it)
                 TSG_TRY(cx.get(&cfirst, (size_t)nch + 1));
-                k_rows_cfirst<<<grid_for(m, WG, 8192), WG, 0, s>>>(m, C.rowpointer, cfirst);
+                k_rows_cfirst<<<grid_for(nch, WG, 16384), WG, 0, s>>>(m, C.rowpointer, (long)nch, cfirst);
                 TSG_HIP(hipGetLastError());
             }
             k_rows_compact<<<nch, WG, 0, s>>>(m, cfirst, soff, C.rowpointer, Scol, Sval, C.columnindex, C.value);

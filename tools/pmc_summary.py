@@ -43,6 +43,7 @@ def bench_line(log):
 
 def main():
     src, tag = sys.argv[1], sys.argv[2]
+    calls = int(sys.argv[3]) if len(sys.argv) > 3 else 0  # (read before kstats rewrites sys.argv)
     prof = os.path.join(REPO, "profiles")
     os.makedirs(prof, exist_ok=True)
     stats = glob.glob(os.path.join(src, "stats", "**", "*kernel_stats.csv"), recursive=True)
@@ -101,7 +102,6 @@ def main():
         tot_w += sum(w)
         if f and w:
             out[k]["hbm_bytes_per_dispatch"] = out[k]["fetch_bytes_per_dispatch"] + out[k]["write_bytes_per_dispatch"]
-    calls = int(sys.argv[3]) if len(sys.argv) > 3 else 0
     if calls and (tot_f or tot_w):
         # every kernel of the pass (the whole device pass), per call: the dispatches of
         # the PMC runs summed, over the calls each run makes (warmup + steps)
