@@ -270,7 +270,11 @@ int dev_spgemm_band(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, Ban
     TSG_TRY(cx.get(&C.rowpointer, (size_t)m + 1));
     if (A.nnz > 0) k_band_ebnd<<<grid_for(A.nnz, WG, 16384), WG, 0, s>>>(A.columnindex, A.nnz, B.rowpointer, ebnd);
     TSG_HIP(hipGetLastError());
-    TSG_TRY(scan_exclusive_i64(cx, bw.width, (long)m + 1, s));  // window widths -> staging offsets
+    {  // window widths -> staging offsets
+        const int rc = dev_scan_i64_fused(cx, bw.width, (long)m + 1, s);
+        if (rc == TSG_ERR_UNSUPPORTED) TSG_TRY(scan_exclusive_i64(cx, bw.width, (long)m + 1, s));
+        else TSG_TRY(rc);
+    }
     if (ev) TSG_HIP(hipEventRecord(ev[1], s));
     if (ev) TSG_HIP(hipEventRecord(ev[4], s));
     if (m > 0) {
@@ -279,20 +283,44 @@ int dev_spgemm_band(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, Ban
         TSG_HIP(hipGetLastError());
     }
     if (ev) TSG_HIP(hipEventRecord(ev[5], s));
-    // row counts -> CSR row pointers (nnz(C) <= the window columns; past int32 fails)
+    // row counts -> CSR row pointers (nnz(C) <= the window columns; past int32 fails).
+    // While the window columns fit int32 and their 12 B each stay within
+    // kRowsProductSizedC, C is sized by them: no read-back of nnz(C) before the
+    // compaction (the fused scan stores it through host-mapped memory); else the
+    // checked scan reads it back first and C is sized exactly.
     long long nnz = 0;
     TSG_HIP(hipMemsetAsync(C.rowpointer + m, 0, sizeof(int), s));
-    TSG_TRY(scan_exclusive_i32_total(cx, C.rowpointer, (long)m + 1, s, &nnz));
-    if (nnz > 0x7fffffffLL) return TSG_ERR_OVERFLOW;
-    C.nnz = (int)nnz;
-    TSG_TRY(cx.get(&C.columnindex, (size_t)nnz + 1));
-    TSG_TRY(cx.get(&C.value, (size_t)nnz + 1));
+    bool fused = bw.wcols <= 0x7fffffffLL && bw.wcols * 12 <= kRowsProductSizedC;
+    int *const hnnz = reinterpret_cast<int *>(cx.pinned64 + 15);
+    if (fused) {
+        const int rc = dev_scan_rows_fused(cx, C.rowpointer, m, reinterpret_cast<int *>(cx.dpinned64 + 15), s);
+        if (rc == TSG_ERR_UNSUPPORTED) fused = false;
+        else TSG_TRY(rc);
+    }
+    if (fused && (cx.get(&C.columnindex, (size_t)bw.wcols + 1) != TSG_OK ||
+                  cx.get(&C.value, (size_t)bw.wcols + 1) != TSG_OK)) {
+        (void)hipGetLastError();
+        cx.put(C.columnindex);
+        C.columnindex = nullptr;
+        TSG_TRY(stream_wait(s));  // (the fused scan's nnz(C), then C sized exactly)
+        nnz = *hnnz;
+        TSG_TRY(cx.get(&C.columnindex, (size_t)nnz + 1));
+        TSG_TRY(cx.get(&C.value, (size_t)nnz + 1));
+    } else if (!fused) {
+        TSG_TRY(scan_exclusive_i32_total(cx, C.rowpointer, (long)m + 1, s, &nnz));
+        if (nnz > 0x7fffffffLL) return TSG_ERR_OVERFLOW;
+        TSG_TRY(cx.get(&C.columnindex, (size_t)nnz + 1));
+        TSG_TRY(cx.get(&C.value, (size_t)nnz + 1));
+    }
     if (m > 0)
         k_band_compact<<<grid_for(m, WAVES, 16384), WG, 0, s>>>(m, bw.width, C.rowpointer, Scol, Sval, C.columnindex,
                                                                C.value);
     TSG_HIP(hipGetLastError());
     if (ev) TSG_HIP(hipEventRecord(ev[3], s));
     TSG_TRY(stream_wait(s));
+    if (fused) nnz = *hnnz;
+    if (nnz > 0x7fffffffLL) return TSG_ERR_OVERFLOW;
+    C.nnz = (int)nnz;
     cx.put(ebnd);
     cx.put(Scol);
     cx.put(Sval);

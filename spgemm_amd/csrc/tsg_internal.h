@@ -183,6 +183,11 @@ void dev_rows_release(Context &cx, RowsPlan &p);
 // ev (optional): 1 set up | 4..5 the row kernels | 3 end
 int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPlan &p, tsg_dev_csr &C,
                  tsg_stats *st, hipStream_t s, hipEvent_t *ev);
+// two-launch exclusive scans (tsg_rows.hip) for up to 2,048 tiles of 4,096
+// values (TSG_ERR_UNSUPPORTED past it): i64 in place; row pointers (n = m + 1)
+// with nnz(C) stored into the host-mapped *hnnz_dev by the kernel
+int dev_scan_i64_fused(Context &cx, long long *a, long n, hipStream_t s);
+int dev_scan_rows_fused(Context &cx, int *rp, int m, int *hnnz_dev, hipStream_t s);
 // exclusive scan (n+1 idiom) whose total is read back
 int scan_exclusive_i32_total(Context &cx, int *a, long n, hipStream_t s, long long *total);
 

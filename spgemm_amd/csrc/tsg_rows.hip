@@ -176,11 +176,12 @@ __global__ __launch_bounds__(WG) void k_rows_entries_sum(const int *ciA, long nn
     if (tid == 0) part[blockIdx.x] = sum;
 }
 
-// per tile of RS_TILE row counts their sum
-__global__ __launch_bounds__(WG) void k_rows_count_sum(const int *a, long n, int *part) {
-    __shared__ int red[WAVES];
+// per tile of RS_TILE values their sum
+template <class T>
+__global__ __launch_bounds__(WG) void k_rows_count_sum(const T *a, long n, T *part) {
+    __shared__ T red[WAVES];
     const long base = (long)blockIdx.x * RS_TILE;
-    int sum = 0;
+    T sum = 0;
 #pragma unroll
     for (int u = 0; u < RS_ITEMS; ++u) {
         const long i = base + u * WG + threadIdx.x;
@@ -222,9 +223,10 @@ __global__ __launch_bounds__(WG) void k_rows_scan_apply(T *a, long n, const T *p
         if constexpr (CFIRST) {
             const long r = base + tid * RS_ITEMS + u;
             if (r < m) {
-                for (long long b = ((long long)off + CP_CH - 1) / CP_CH; b * CP_CH < (long long)off + v; ++b)
-                    cfirst[b] = (int)r;
-            } else if (r == m) {
+                if (cfirst)
+                    for (long long b = ((long long)off + CP_CH - 1) / CP_CH; b * CP_CH < (long long)off + v; ++b)
+                        cfirst[b] = (int)r;
+            } else if (r == m && hnnz) {
                 __hip_atomic_store(hnnz, (int)off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
@@ -2108,6 +2110,34 @@ __global__ __launch_bounds__(WG) void k_rows_compact(int m, const int *cfirst, c
         }
 }
 
+// Two-launch exclusive scans (tile sums, then an apply that adds up the earlier
+// tiles' sums) for the other CSR paths; TSG_ERR_UNSUPPORTED past RS_INLINE_MAX
+// tiles (the caller then takes the generic scan).  Row pointers: n = m + 1,
+// nnz(C) (the last value) into the host-mapped *hnnz_dev.
+int dev_scan_i64_fused(Context &cx, long long *a, long n, hipStream_t s) {
+    const long nt = (n + RS_TILE - 1) / RS_TILE;
+    if (n <= 0) return TSG_OK;
+    if (nt > RS_INLINE_MAX) return TSG_ERR_UNSUPPORTED;
+    long long *part = nullptr;
+    TSG_TRY(cx.get(&part, (size_t)nt));
+    k_rows_count_sum<long long><<<(unsigned)nt, WG, 0, s>>>(a, n, part);
+    k_rows_scan_apply<long long, false><<<(unsigned)nt, WG, 0, s>>>(a, n, part, nullptr, 0, nullptr);
+    TSG_HIP(hipGetLastError());
+    cx.put(part);  // (stream-ordered reuse)
+    return TSG_OK;
+}
+int dev_scan_rows_fused(Context &cx, int *rp, int m, int *hnnz_dev, hipStream_t s) {
+    const long n = (long)m + 1, nt = (n + RS_TILE - 1) / RS_TILE;
+    if (nt > RS_INLINE_MAX) return TSG_ERR_UNSUPPORTED;
+    int *part = nullptr;
+    TSG_TRY(cx.get(&part, (size_t)nt));
+    k_rows_count_sum<int><<<(unsigned)nt, WG, 0, s>>>(rp, n, part);
+    k_rows_scan_apply<int, true><<<(unsigned)nt, WG, 0, s>>>(rp, n, part, nullptr, m, hnnz_dev);
+    TSG_HIP(hipGetLastError());
+    cx.put(part);  // (stream-ordered reuse)
+    return TSG_OK;
+}
+
 // Setup (stream-ordered, no host round trip): the entry table, its scan and the
 // classes; counts and statistics land in cx.pinned64[0..7) once the stream is synced.
 int dev_rows_setup_async(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPlan &p, hipStream_t s,
@@ -2381,7 +2411,7 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
                 int *part = nullptr;
                 TSG_TRY(cx.get(&part, (size_t)rtile));
                 TSG_TRY(cx.get(&cfirst, (size_t)((products + CP_CH - 1) / CP_CH) + 1));
-                k_rows_count_sum<<<(unsigned)rtile, WG, 0, s>>>(C.rowpointer, (long)m + 1, part);
+                k_rows_count_sum<int><<<(unsigned)rtile, WG, 0, s>>>(C.rowpointer, (long)m + 1, part);
                 k_rows_scan_apply<int, true><<<(unsigned)rtile, WG, 0, s>>>(
                     C.rowpointer, (long)m + 1, part, cfirst, m, reinterpret_cast<int *>(cx.dpinned64 + 15));
                 TSG_HIP(hipGetLastError());
