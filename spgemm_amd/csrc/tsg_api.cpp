@@ -283,6 +283,18 @@ static int download_tiles(const tsg_dev_tiles &t, tsg_smatrix *M, bool csc, hipS
     return TSG_OK;
 }
 
+// the tile structure alone (tile_ptr, tile_columnidx): what step 1 reads
+static int upload_tile_structure(Context &cx, const tsg_smatrix *M, int tile_m, int tile_n, tsg_dev_tiles &t,
+                                 hipStream_t s) {
+    t = tsg_dev_tiles{};
+    t.m = M->m; t.n = M->n; t.nnz = M->nnz;
+    t.tile_m = tile_m; t.tile_n = tile_n;
+    t.tilem = M->tilem; t.tilen = M->tilen; t.numtile = M->numtile;
+    TSG_TRY(upload(cx, &t.tile_ptr, M->tile_ptr, (size_t)M->tilem + 1, s));
+    TSG_TRY(upload(cx, &t.tile_columnidx, M->tile_columnidx, (size_t)M->numtile, s));
+    return TSG_OK;
+}
+
 static int upload_tiles(Context &cx, const tsg_smatrix *M, int tile_m, int tile_n, bool csc, tsg_dev_tiles &t,
                         hipStream_t s) {
     t = tsg_dev_tiles{};
@@ -641,28 +653,32 @@ int tsg_tilespgemm(tsg_smatrix *A, tsg_smatrix *B, tsg_smatrix *C, unsigned int 
     Context &cx = lease.cx();
     hipStream_t s = lease.stream();
     tsg_dev_tiles dA, dB, dC;
-    TSG_TRY(upload_tiles(cx, A, tm, tn, false, dA, s));
-    TSG_TRY(upload_tiles(cx, B, tn, tm, true, dB, s));
     // The reference's SMatrix carries the CSR beside the tiles (src/main.cu builds
-    // both).  When both operands have it and B's rows are column-sorted, steps 2
-    // and 3 stream the element products from it (the CSR path's kernels, writing
-    // the tiled C); copied in with the tiles, outside the timed region.
-    // TSG_TILED_CSR=0 keeps the tile-payload kernels.
+    // both).  When both operands have it and B's rows are column-sorted, C comes
+    // from the device CSR route and the tiled layout kernel (below): then only
+    // the tile STRUCTURES of A and B are read (step 1), and only they are copied
+    // in -- no tile payloads, no B row-major views.  Copies are outside the timed
+    // region, as in the reference.  TSG_TILED_CSR=0 keeps the tile-payload kernels.
     tsg_dev_csr cA{}, cB{};
     bool use_csr = false, s2e = false;
     {
         const char *e = getenv("TSG_TILED_CSR");
         const bool allow = !(e && !strcmp(e, "0"));
         if (sq16 && allow && A->rowpointer && A->columnindex && A->value && B->rowpointer && B->columnindex &&
-            B->value && A->nnz == dA.nnz && B->nnz == dB.nnz) {
+            B->value) {
             TSG_TRY(upload_csr(cx, A, cA, s));
             TSG_TRY(upload_csr(cx, B, cB, s));
             bool sorted = false;
             TSG_TRY(dev_rows_sorted(cx, cB, &sorted, s));
             use_csr = sorted;
-            // element masks for sparse tiles, tile-row mask ORs for denser ones (as dev_spgemm16)
-            s2e = use_csr && (double)dA.nnz < kStep2ElemMaxTileDensity * (double)dA.numtile;
         }
+    }
+    if (use_csr) {
+        TSG_TRY(upload_tile_structure(cx, A, tm, tn, dA, s));
+        TSG_TRY(upload_tile_structure(cx, B, tn, tm, dB, s));
+    } else {
+        TSG_TRY(upload_tiles(cx, A, tm, tn, false, dA, s));
+        TSG_TRY(upload_tiles(cx, B, tn, tm, true, dB, s));
     }
     TSG_HIP(hipStreamSynchronize(s));
     tsg_stats st{};
