@@ -7,15 +7,17 @@ step 3 + GPU tile2csr (SURVEY.md §8d t_e2e).  Inputs are resident in HBM
 (src/tilespgemm-cuda.h:2808).
 
   python bench.py                       # N=1, webbase-1M synthetic stand-in
-  python bench.py --gpus N ...          # under torch.distributed.run (default: weak
-                                        # scaling): rank r computes row block r of
-                                        # [A; A; ...; A]*B (one full A per rank, B
-                                        # replicated, C stays distributed, no collective)
-  python bench.py --gpus N --scaling strong
-                                        # north_star's exchange: the fixed product A*B,
-                                        # A's rows split into pieces of equal work, B
-                                        # replicated, C gathered to rank 0 over RCCL
-                                        # inside the timed region (gather-bound: DESIGN 5)
+  python bench.py --gpus N ...          # under torch.distributed.run (default: strong
+                                        # scaling, north_star's exchange): the fixed
+                                        # product A*B, A's rows split into pieces of
+                                        # equal work, B replicated, C gathered to rank 0
+                                        # over RCCL inside the timed region (gather_ms
+                                        # reported; gather-bound: DESIGN 5)
+  python bench.py --gpus N --scaling weak
+                                        # NOT the north-star metric: rank r computes row
+                                        # block r of [A; A; ...; A]*B (one full A per
+                                        # rank, B replicated, C stays distributed, no
+                                        # collective)
   python bench.py --matrix lj           # products past int32 nnz(C) (the reference's
                                         # `int nnzC`, src/tilespgemm-cuda.h:2327) run as
                                         # sequential tile-row blocks of <= 1.5e9 products
@@ -298,11 +300,12 @@ def main():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N>1 (nccl = RCCL over xGMI; gloo = host-staged "
                          "rehearsal of the multi-rank path, e.g. several ranks on one GPU)")
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="N>1: weak (default) = every rank owns one A-sized row block of the stacked "
-                         "product (fixed work per GPU, C stays distributed, no data-path collective); "
-                         "strong = the fixed product, A's rows partitioned by work + the RCCL gather of C "
-                         "to rank 0 (north_star's exchange step; gather-bound, DESIGN section 5)")
+    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
+                    help="N>1: strong (default, north_star's exchange step) = the fixed product, A's rows "
+                         "partitioned by work, B replicated, the RCCL gather of C to rank 0 inside the timed "
+                         "region (gather-bound, DESIGN section 5); weak = NOT the north-star metric: every "
+                         "rank owns one A-sized row block of the stacked product [A; ...; A]*B (fixed work "
+                         "per GPU, C stays distributed, no data-path collective)")
     ap.add_argument("--gather-sub", type=int, default=0,
                     help="N>1 strong: the rows are cut into N x this many pieces of equal products, rank r "
                          "computing piece (s, r) in round s; each round goes to rank 0 straight into the final "
@@ -442,6 +445,12 @@ def main():
 
     gathered = [None]
     gather_ms = []
+    sg = None
+    if gather:
+        # one gatherer for every step: rank 0's C arrays are sized from the gathered
+        # nnz counts in the warmup and reused; the counts travel on a host (gloo) group
+        meta = dist.new_group(backend="gloo")
+        sg = tdist.RoundGather(rank, world, pieces, 0, device="cpu" if host_coll else "cuda", meta_group=meta)
 
     def one_step():
         sts, nnz = [], 0
@@ -450,16 +459,17 @@ def main():
             # the rounds in turn, each piece handed to the gather as soon as its C is
             # complete (the context keeps every piece's C until the step ends)
             ctx.reset()
-            sg = tdist.RoundGather(rank, world, pieces, nnzcub_full, device="cpu" if host_coll else "cuda")
+            gathered[0] = None
+            sg.reset()
             for s, (_, _, dAb) in enumerate(dA_blocks):
                 c, st = ctx.spgemm(dAb, dB, tm, tm)
                 sts.append(st)
                 nnz += c.nnz
                 cv = ctx.view_torch(c)  # zero-copy views of the context-owned C
                 if host_coll:
-                    sg.push(s, cv.rowptr.cpu(), cv.col.cpu(), cv.val.cpu())
+                    sg.push(s, cv.rowptr.cpu(), cv.col.cpu(), cv.val.cpu(), nnz=c.nnz)
                 else:
-                    sg.push(s, cv.rowptr, cv.col, cv.val)
+                    sg.push(s, cv.rowptr, cv.col, cv.val, nnz=c.nnz)
             g0 = time.perf_counter()
             gathered[0] = sg.finish()
             if not host_coll:

@@ -323,8 +323,32 @@ static int upload_tiles(Context &cx, const tsg_smatrix *M, int tile_m, int tile_
 static constexpr double kStep2ElemMaxTileDensity = 16.0;
 
 static bool quiet() { return getenv("TSG_QUIET") != nullptr; }
+// b_sorted: 1 = the caller already checked B's rows column-sorted (the check
+// is skipped), -1 = unknown (checked here)
 static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B, hipStream_t s, tsg_dev_csr *C,
-                        tsg_stats *stats);
+                        tsg_stats *stats, int b_sorted = -1);
+
+// tsg_tilespgemm's CSR route computes C from the CSR that the reference's
+// SMatrix carries beside the tiles (src/main.cu:261-276 builds both from one
+// CSR).  It is taken only when that CSR is present and agrees with the tiles:
+// A's and B's nnz equal their tiles' totals (tile_nnz[numtile], an exclusive
+// scan) and every A tile row holds as many nonzeros as the CSR rows it covers.
+// Otherwise the tile payloads are used (the payload route), so a caller whose
+// CSR and tiles disagree gets C of the tiles, as from the reference.
+static bool csr_matches_tiles(const tsg_smatrix *A, const tsg_smatrix *B, int tm) {
+    for (const tsg_smatrix *M : {A, B}) {
+        if (!M->rowpointer || !M->columnindex || !M->value || !M->tile_nnz || !M->tile_ptr) return false;
+        if (M->numtile < 0 || M->tile_nnz[M->numtile] != M->nnz || M->rowpointer[M->m] != M->nnz) return false;
+    }
+    if (A->tilem != (A->m + tm - 1) / tm) return false;
+    for (int i = 0; i < A->tilem; ++i) {
+        const int r0 = std::min(A->m, i * tm), r1 = std::min(A->m, (i + 1) * tm);
+        const int t0 = A->tile_ptr[i], t1 = A->tile_ptr[i + 1];
+        if (t0 < 0 || t1 < t0 || t1 > A->numtile) return false;
+        if (A->tile_nnz[t1] - A->tile_nnz[t0] != A->rowpointer[r1] - A->rowpointer[r0]) return false;
+    }
+    return true;
+}
 
 // ------------------------------------------------------------------ C ABI
 extern "C" {
@@ -660,17 +684,15 @@ int tsg_tilespgemm(tsg_smatrix *A, tsg_smatrix *B, tsg_smatrix *C, unsigned int 
     // in -- no tile payloads, no B row-major views.  Copies are outside the timed
     // region, as in the reference.  TSG_TILED_CSR=0 keeps the tile-payload kernels.
     tsg_dev_csr cA{}, cB{};
-    bool use_csr = false, s2e = false;
+    bool use_csr = false, bsorted = false;
     {
         const char *e = getenv("TSG_TILED_CSR");
         const bool allow = !(e && !strcmp(e, "0"));
-        if (sq16 && allow && A->rowpointer && A->columnindex && A->value && B->rowpointer && B->columnindex &&
-            B->value) {
+        if (sq16 && allow && csr_matches_tiles(A, B, tm)) {
             TSG_TRY(upload_csr(cx, A, cA, s));
             TSG_TRY(upload_csr(cx, B, cB, s));
-            bool sorted = false;
-            TSG_TRY(dev_rows_sorted(cx, cB, &sorted, s));
-            use_csr = sorted;
+            TSG_TRY(dev_rows_sorted(cx, cB, &bsorted, s));
+            use_csr = bsorted;
         }
     }
     if (use_csr) {
@@ -696,7 +718,6 @@ int tsg_tilespgemm(tsg_smatrix *A, tsg_smatrix *B, tsg_smatrix *C, unsigned int 
         // Step 1 and the CSR product read only A and B: step 1 runs on a second
         // stream from a host thread (each has host round trips of its own), the
         // layout kernel joins them.
-        (void)s2e;
         evi[0] = 12, evi[1] = 12, evi[2] = 13, evi[3] = 14;
         dC = tsg_dev_tiles{};
         dC.m = A->m; dC.n = B->n; dC.tile_m = 16; dC.tile_n = 16;
@@ -705,29 +726,41 @@ int tsg_tilespgemm(tsg_smatrix *A, tsg_smatrix *B, tsg_smatrix *C, unsigned int 
         Context &cx1 = aux.cx();
         hipStream_t s1 = aux.stream();
         int rc1 = TSG_OK;
-        std::thread th([&] {
+        auto step1 = [&] {
             long long tp = 0;
             rc1 = hipSetDevice(cx.device) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
             if (rc1 == TSG_OK) rc1 = hipEventRecord(cx1.ev[11], s1) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
             if (rc1 == TSG_OK) rc1 = dev_step1(cx1, dA, dB, dC, &tp, s1);
             if (rc1 == TSG_OK) rc1 = hipEventRecord(cx1.ev[12], s1) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
             if (rc1 == TSG_OK) rc1 = hipStreamSynchronize(s1) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
-        });
+        };
+        // step 1 from a host thread of its own; when the thread cannot be made
+        // (std::system_error: no exception may leave this C ABI) it runs here,
+        // before the product, on its own stream
+        std::thread th;
+        bool threaded = true;
+        try {
+            th = std::thread(step1);
+        } catch (...) {
+            threaded = false;
+            step1();
+        }
         tsg_dev_csr Cc{};
         tsg_stats st2{};
         rc = hipEventRecord(cx.ev[12], s) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
-        if (rc == TSG_OK) rc = dev_spgemm16(cx, &cA, &cB, s, &Cc, &st2);
+        if (rc == TSG_OK) rc = dev_spgemm16(cx, &cA, &cB, s, &Cc, &st2, bsorted ? 1 : -1);
         if (rc == TSG_OK) rc = hipEventRecord(cx.ev[13], s) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
-        th.join();
+        if (threaded) th.join();
         if (rc == TSG_OK) rc = rc1;
         if (rc == TSG_OK) t_s1 = ev_ms(cx1.ev[11], cx1.ev[12]);
         if (rc == TSG_OK) rc = dev_ctiles_from_csr(cx, Cc, dC, s);
         if (rc == TSG_OK) rc = hipEventRecord(cx.ev[14], s) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
         if (rc == TSG_OK) TSG_HIP(hipStreamSynchronize(s));
-        if (rc == TSG_OK && cx.pinned[8] != 0) rc = TSG_ERR_HIP;  // (a nonzero outside step 1's tiles)
+        // a nonzero of the CSR product outside step 1's tiles, or tile totals that
+        // miss nnz(C): the CSR disagrees with the tiles it was passed with
+        if (rc == TSG_OK && cx.pinned[8] != 0) rc = TSG_ERR_INVALID;
     } else if (sq16) {
-        rc = dev_tilespgemm(cx, dA, dB, dC, &st, s, cx.ev, nullptr, use_csr ? &cA : nullptr, use_csr ? &cB : nullptr,
-                            s2e);
+        rc = dev_tilespgemm(cx, dA, dB, dC, &st, s, cx.ev, nullptr, nullptr, nullptr, false);
     } else {
         dC = tsg_dev_tiles{};
         dC.m = A->m; dC.n = B->n; dC.tile_m = tm; dC.tile_n = tm;
@@ -897,7 +930,7 @@ static void release_tiles(Context &cx, tsg_dev_tiles &t) {
 // CSR in -> CSR out through the 16x16 tiled pipeline (C does not depend on the
 // tile size; other sizes are a layout choice of the host tile API).
 static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B, hipStream_t s, tsg_dev_csr *C,
-                        tsg_stats *stats) {
+                        tsg_stats *stats, int b_sorted) {
     const int tm = 16, tn = 16;
     tsg_stats st{};
     tsg_dev_tiles tA, tB, tC;
@@ -913,7 +946,10 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
     // (its last step -- the shares' sum into the flag -- rides on the row-merge
     // setup's binning kernel, or runs before the first read-back of another route)
     SortedShares shares;
-    TSG_TRY(dev_rows_sorted_shares(cx, *B, cx.pinned + 1, &shares, s));
+    if (b_sorted == 1)
+        cx.pinned[1] = 0;  // (known: no check, no shares for the binning kernel to sum)
+    else
+        TSG_TRY(dev_rows_sorted_shares(cx, *B, cx.pinned + 1, &shares, s));
     // Routing, B's rows column-sorted:
     //  * banded path (tsg_band.hip) when A averages >= 8 entries per row and every
     //    C row's reachable columns fit one window of <= 2,048 columns holding at

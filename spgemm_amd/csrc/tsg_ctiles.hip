@@ -272,6 +272,8 @@ int dev_ctiles_from_csr(Context &cx, const tsg_dev_csr &Cc, tsg_dev_tiles &C, hi
                                                   C.tile_columnidx, units, fail + 1, ulo, C.tile_nnz, C.tile_csr_Ptr,
                                                   C.mask, C.tile_csr_Col, C.tile_csr_Value, fail);
     }
+    else if (Cc.nnz > 0)
+        TSG_HIP(hipMemsetAsync(fail, 1, 1, s));  // (nonzeros but no tiles to hold them)
     TSG_HIP(hipGetLastError());
     cx.pinned[8] = 0;
     TSG_HIP(hipMemcpyAsync(cx.pinned + 8, fail, sizeof(int), hipMemcpyDeviceToHost, s));

@@ -136,51 +136,90 @@ def row_pieces(cum, m, world, nsub):
 class RoundGather:
     """Gather of C to rank 0 in rounds, each overlapped with the next round's
     computation.  The rows are cut into world x nsub pieces (row_pieces): rank
-    r computes piece (s, r) in round s and hands it to push(s, ...).  After each
-    round one all_gather brings every piece's nnz to every rank (one host
-    synchronisation per round); rank 0 then posts the receives of the peers'
-    pieces straight into the final C at their exact offsets (the earlier
-    rounds' nonzeros + the round's earlier pieces) and copies its own piece
-    there, while the peers post non-blocking sends and go on computing the next
-    round.  No concatenation: C's columns and values are written once on rank
-    0, into arrays sized by the product bound (`products`, fixed before the
-    first round; the returned arrays are views of their first nnz(C) entries).
+    r computes piece (s, r) in round s and hands it to push(s, ..., nnz).
+
+    Counts travel on the host, never through a device read-back: every rank
+    already holds its piece's nnz(C) as a host integer (the SpGEMM call returns
+    it), and one non-blocking all_gather of those integers per round runs on a
+    separate host (gloo) group, `meta_group`.  The peers post their sends at
+    once and go on computing; rank 0 waits only for the round's host counts
+    (no device synchronisation), then posts the receives of the peers' pieces
+    straight into the final C at their exact offsets (the earlier rounds'
+    nonzeros + the round's earlier pieces) and copies its own piece there.
+
+    No concatenation: C's columns and values are written once on rank 0.  The
+    output arrays are sized from the gathered nnz counts -- grown (after the
+    receives into the old arrays complete) only when a round's counts exceed
+    the capacity -- and kept across reset() calls, so a repeated product
+    (the bench's steps) allocates them once at exactly nnz(C).  The returned
+    arrays are views of the first nnz(C) entries, valid until the next step.
     Point-to-point messages between a pair match in posting order (RCCL/NCCL
     P2P have no tags): every pair posts rounds in order."""
 
-    def __init__(self, rank, world, pieces, products, device=None):
+    def __init__(self, rank, world, pieces, capacity=0, device=None, meta_group=None):
         import torch
         import torch.distributed as dist
         self.t, self.d = torch, dist
         self.rank, self.world, self.pieces = rank, world, pieces
         self.dev = device
-        self.off = 0            # rank 0: nonzeros of the rounds gathered so far
-        self.work = []          # (work handle(s), tensors kept alive)
-        self.fix = []           # rank 0: (received row pointers, first row, offset)
+        self.meta = meta_group  # host group of the counts (None: the default group, which must be gloo)
+        self.cap = 0
+        self.out_ci = self.out_v = None
+        self.reset()
         if rank == 0:
             m = pieces[-1][-1][1] if pieces else 0
             self.out_rp = torch.empty(m + 1, dtype=torch.int32, device=device)
-            self.out_ci = torch.empty(max(1, int(products)), dtype=torch.int32, device=device)
-            self.out_v = torch.empty(max(1, int(products)), dtype=torch.float64, device=device)
             self.m = m
+            self._grow(max(1, int(capacity)))
 
-    def push(self, s, rowptr, col, val):
-        """this rank's piece of round s (its rows' CSR, row pointers from 0)"""
+    def reset(self):
+        """start a new gather (one step) on the same pieces; rank 0 keeps its arrays"""
+        self.off = 0            # rank 0: nonzeros of the rounds gathered so far
+        self.work = []          # (work handle(s), tensors kept alive)
+        self.fix = []           # rank 0: (received row pointers, first row, offset)
+        self.meta_work = []     # peers: the count all_gathers still in flight
+
+    def _wait(self):
+        for ws, _ in self.work:
+            for w in ws:
+                w.wait()
+        self.work = []
+
+    def _grow(self, need):
+        """rank 0: output arrays of at least `need` nonzeros, the first `off` kept"""
+        t = self.t
+        if need <= self.cap:
+            return
+        self._wait()  # (receives still landing in the old arrays)
+        ci = t.empty(need, dtype=t.int32, device=self.dev)
+        v = t.empty(need, dtype=t.float64, device=self.dev)
+        if self.cap and self.off:
+            ci[:self.off] = self.out_ci[:self.off]
+            v[:self.off] = self.out_v[:self.off]
+        self.out_ci, self.out_v, self.cap = ci, v, need
+
+    def push(self, s, rowptr, col, val, nnz=None):
+        """this rank's piece of round s (its rows' CSR, row pointers from 0;
+        `nnz` its host-side nonzero count, default col.numel())"""
         t, d = self.t, self.d
-        n = t.tensor([col.numel()], dtype=t.int64, device=self.dev)
-        alln = [t.zeros(1, dtype=t.int64, device=self.dev) for _ in range(self.world)]
-        d.all_gather(alln, n)
-        nn = [int(x) for x in t.cat(alln).tolist()]  # (the round's one host synchronisation)
+        k_own = int(col.numel() if nnz is None else nnz)
+        n = t.tensor([k_own], dtype=t.int64)
+        alln = [t.zeros(1, dtype=t.int64) for _ in range(self.world)]
+        h = d.all_gather(alln, n, group=self.meta, async_op=True)
         if self.rank != 0:
             rp = rowptr.contiguous()
             ops = [d.P2POp(d.isend, rp, 0)]
             keep = [rp]
-            if nn[self.rank]:
-                c, v = col.contiguous(), val.contiguous()
+            if k_own:
+                c, v = col[:k_own].contiguous(), val[:k_own].contiguous()
                 ops += [d.P2POp(d.isend, c, 0), d.P2POp(d.isend, v, 0)]
                 keep += [c, v]
             self.work.append((d.batch_isend_irecv(ops), keep))
+            self.meta_work.append((h, alln))
             return
+        h.wait()  # the round's host counts (waits for the peers' progress, not for a device)
+        nn = [int(x[0]) for x in alln]
+        self._grow(self.off + sum(nn))
         o = self.off
         ops, keep = [], []
         for r in range(self.world):
@@ -189,8 +228,8 @@ class RoundGather:
             if r == 0:
                 self.out_rp[r0:r1 + 1] = rowptr.to(t.int32) + o
                 if k:
-                    self.out_ci[o:o + k] = col
-                    self.out_v[o:o + k] = val
+                    self.out_ci[o:o + k] = col[:k]
+                    self.out_v[o:o + k] = val[:k]
             else:
                 rp = t.empty(r1 - r0 + 1, dtype=t.int32, device=self.dev)
                 ops.append(d.P2POp(d.irecv, rp, r))
@@ -205,13 +244,14 @@ class RoundGather:
             self.work.append((d.batch_isend_irecv(ops), keep))
 
     def finish(self):
-        for ws, _ in self.work:
-            for w in ws:
-                w.wait()
-        self.work = []
+        self._wait()
+        for h, _ in self.meta_work:
+            h.wait()
+        self.meta_work = []
         if self.rank != 0:
             return None
         for rp, r0, o in self.fix:  # the peers' row pointers, rebased
             self.out_rp[r0:r0 + rp.numel()] = rp + o
+        self.fix = []
         self.out_rp[self.m] = self.off
         return self.out_rp, self.out_ci[:self.off], self.out_v[:self.off]

@@ -136,15 +136,26 @@ def _worker_rounds(rank, world, port, kind, nsub, q):
         blen = np.diff(rpb.astype(np.int64))
         cum = np.concatenate([[0], np.cumsum(blen[ci])])[rp]
         pieces = tdist.row_pieces(cum, m, world, nsub)
-        g = tdist.RoundGather(rank, world, pieces, int(cum[-1]))
-        for s in range(nsub):  # each round's piece "computed" (oracle) then pushed
-            b0, b1 = pieces[s][rank]
-            mk, rpk, cik, vvk = tdist.slice_rows(m, rp, ci, vv, b0, b1)
-            _, _, crp, cci, cvv = O.gustavson(O.OMat.from_csr(mk, n, rpk, cik, vvk), oB).csr()
-            g.push(s, torch.from_numpy(crp.astype(np.int32)), torch.from_numpy(cci.astype(np.int32)),
-                   torch.from_numpy(cvv.copy()))
-        out = g.finish()
+        meta = dist.new_group(backend="gloo")  # the counts' host group (bench.py: beside RCCL)
+        # capacity 1: rank 0's arrays grow from the gathered counts (round by round)
+        g = tdist.RoundGather(rank, world, pieces, 1, meta_group=meta)
+        caps = []
+        for step in range(2):  # the second step reuses the arrays sized by the first
+            g.reset()
+            for s in range(nsub):  # each round's piece "computed" (oracle) then pushed
+                b0, b1 = pieces[s][rank]
+                mk, rpk, cik, vvk = tdist.slice_rows(m, rp, ci, vv, b0, b1)
+                _, _, crp, cci, cvv = O.gustavson(O.OMat.from_csr(mk, n, rpk, cik, vvk), oB).csr()
+                # padded arrays + the host count: only the first nnz entries travel
+                pc = np.concatenate([cci.astype(np.int32), np.full(3, -7, np.int32)])
+                pv = np.concatenate([cvv, np.full(3, np.nan)])
+                g.push(s, torch.from_numpy(crp.astype(np.int32)), torch.from_numpy(pc), torch.from_numpy(pv),
+                       nnz=len(cci))
+            out = g.finish()
+            caps.append(g.cap)
         if rank == 0:
+            # sized by the gathered nnz (not the products bound), allocated once
+            assert caps[0] == caps[1] == max(1, len(out[1])), (caps, len(out[1]))
             q.put(("ok", pieces, [x.numpy().copy() for x in out]))
         else:
             assert out is None
@@ -175,9 +186,10 @@ def test_round_gather_of_row_pieces_matches_full_product(world, nsub, kind):
     """The overlapped gather (dist.RoundGather): rows cut into world x nsub
     pieces of equal products at row granularity, rank r computing piece (s, r)
     in round s; rank 0 receives every round straight into the final C at its
-    exact offsets (no concatenation).  The gathered row pointers, columns and
-    values equal the full product array by array, and the pieces tile the rows
-    in round-major order."""
+    exact offsets (no concatenation), the counts exchanged on a host group with
+    no device read-back, its arrays sized by the gathered nnz and reused by the
+    next step.  The gathered row pointers, columns and values equal the full
+    product array by array, and the pieces tile the rows in round-major order."""
     status, pieces, got = _run(world, _worker_rounds, (kind, nsub))
     assert status == "ok", pieces
     m, n, rp, ci, vv = _matrix(kind)

@@ -6,6 +6,7 @@ reference's value[k] = k % 10 every product and sum is a small integer).
 The structural oracle is pinned to the reference's own host code by
 tests/test_oracle.py; goldens in tests/golden/ref come from that code.
 """
+import ctypes
 import os
 
 import numpy as np
@@ -435,5 +436,42 @@ def test_tiled_csr_route_wide_tile_rows_and_empty_tiles():
     assert int(ct["tile_ptr"][1]) > 5 * 992  # the first tile row spans several units
     tn = np.diff(ct["tile_nnz"][: len(ct["tile_columnidx"]) + 1])
     assert (tn == 0).any()  # structurally present, numerically empty tiles
+    T.tile2csr(Cm, 16, 16)
+    assert_csr_equal(Cm.csr(), O.gustavson(oA, oB).csr())
+
+
+@pytest.mark.parametrize("which", ["A", "B"])
+def test_tiled_csr_disagreeing_with_tiles_takes_the_payload_route(which):
+    """tsg_tilespgemm's CSR route reads the CSR that the SMatrix carries beside
+    its tiles (src/main.cu:261-276 builds both from one CSR).  When that CSR
+    disagrees with the tiles -- here A's (or B's) CSR lost its last nonzero
+    after csr2tile, so its nnz no longer equals the tiles' tile_nnz[numtile] --
+    the call must fall back to the tile payloads: C is the product of the
+    TILES, every C tile field equal to the oracle's tiled product of the
+    original operands."""
+    m, n, rp, ci, vv = synth.random_csr(700, 700, density=0.006, seed=17)
+    A = T.Matrix.from_csr(m, n, rp, ci, vv)
+    B = T.Matrix.from_csr(m, n, rp.copy(), ci.copy(), vv.copy())
+    T.csr2tile_row_major(A, 16, 16)
+    T.csr2tile_col_major(B, 16, 16)
+    oA = O.OMat.from_csr(m, n, rp, ci, vv)
+    oB = O.OMat.from_csr(m, n, rp, ci, vv)
+    O.csr2tile_row_major(oA, 16, 16)
+    O.csr2tile_col_major(oB, 16, 16)
+    want = O.c_tiles(O.tilespgemm(oA, oB, 16, 16), 16)
+    # the operand's CSR without its last nonzero (row pointers only: the arrays keep
+    # their length), swapped in beside the unchanged tiles (whose nnz stays)
+    M = A if which == "A" else B
+    rp2 = rp.astype(np.int32).copy()
+    rp2[-1] -= 1
+    ci2, vv2 = ci.astype(np.int32).copy(), vv.copy()
+    M._keep += [rp2, ci2, vv2]
+    M.s.rowpointer = rp2.ctypes.data_as(ctypes.POINTER(ctypes.c_int))
+    M.s.columnindex = ci2.ctypes.data_as(ctypes.POINTER(ctypes.c_int))
+    M.s.value = vv2.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+    Cm, _ = T.tilespgemm(A, B, 16, 16)
+    ct = Cm.tiles(16, 1)
+    for k in C_KEYS:
+        np.testing.assert_array_equal(ct[k], want[k], err_msg=f"C {k} ({which}'s CSR disagrees)")
     T.tile2csr(Cm, 16, 16)
     assert_csr_equal(Cm.csr(), O.gustavson(oA, oB).csr())
