@@ -39,7 +39,8 @@ namespace {
 constexpr int BD_WG = 256;
 constexpr int BD_SPAN = 2048;            // window columns per row: 16 KB fp64 + 256 B bitmap of LDS
 constexpr int BD_WORDS = BD_SPAN / 32;   // bitmap words (= 64: one wave scans them)
-constexpr int BD_U = 4;                  // entries per wave in flight
+constexpr int BD_SLOTS = 64;             // copies of the window statistics (k_band_stats)
+constexpr int BD_U = 2;                  // entries per register set (two sets: 4 in flight)
 static_assert(BD_WORDS == 64, "one bitmap word per lane");
 
 }  // namespace
@@ -51,29 +52,56 @@ static_assert(BD_WORDS == 64, "one bitmap word per lane");
 // = the windows' columns in all.
 __global__ __launch_bounds__(WG) void k_band_stats(const int *rpA, const int *ciA, int m, const int *rpB,
                                                    const int *ciB, int2 *win, long long *width, int *bad) {
+    // 16 lanes per row, lane sl taking the row's entries sl, sl + 16, ... (four
+    // entries' loads in flight): a row's ~64 entries (cant) are four dependent
+    // load chains deep, not 64 (a thread per row walked them serially: 65 us)
+    constexpr int G = 16, U = 4;
     __shared__ int red[2 * WAVES];
     __shared__ long long red64[WAVES];
+    const int sl = threadIdx.x % G;
     int nbad = 0, wmax = 0;
     long long prod = 0, wsum = 0;
-    for (int r = blockIdx.x * WG + threadIdx.x; r < m; r += gridDim.x * WG) {
+    const int rows_per_pass = gridDim.x * (WG / G);
+    for (int r0 = blockIdx.x * (WG / G); r0 < m; r0 += rows_per_pass) {  // (workgroup-uniform)
+        const int r = r0 + threadIdx.x / G;
         int lo = INT_MAX, hi = -1;
         long long q = 0;
-        for (int a = rpA[r]; a < rpA[r + 1]; ++a) {
-            const int k = ciA[a], b0 = rpB[k], b1 = rpB[k + 1];
-            if (b1 > b0) {
-                lo = min(lo, ciB[b0]);
-                hi = max(hi, ciB[b1 - 1]);
-                q += b1 - b0;
+        if (r < m) {
+            const int a1 = rpA[r + 1];
+            for (int a = rpA[r] + sl; a < a1; a += U * G) {
+                int k[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) k[u] = a + u * G < a1 ? ciA[a + u * G] : -1;
+                int b0[U], b1[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    b0[u] = k[u] >= 0 ? rpB[k[u]] : 0;
+                    b1[u] = k[u] >= 0 ? rpB[k[u] + 1] : 0;
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (b1[u] > b0[u]) {
+                        lo = min(lo, ciB[b0[u]]);
+                        hi = max(hi, ciB[b1[u] - 1]);
+                        q += b1[u] - b0[u];
+                    }
             }
-            if (hi >= lo && hi - lo >= BD_SPAN) break;  // already too wide
         }
-        const int w = hi >= lo ? hi - lo + 1 : 0;
-        if (w > BD_SPAN) ++nbad;
-        prod += q;
-        wsum += w;
-        wmax = max(wmax, w);
-        win[r] = make_int2(lo, hi);
-        width[r] = w;
+#pragma unroll
+        for (int d = G / 2; d > 0; d >>= 1) {
+            lo = min(lo, __shfl_xor(lo, d, G));
+            hi = max(hi, __shfl_xor(hi, d, G));
+            q += __shfl_xor(q, d, G);
+        }
+        if (r < m && sl == 0) {
+            const int w = hi >= lo ? hi - lo + 1 : 0;
+            if (w > BD_SPAN) ++nbad;
+            prod += q;
+            wsum += w;
+            wmax = max(wmax, w);
+            win[r] = make_int2(lo, hi);
+            width[r] = w;
+        }
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) width[m] = 0;
     int mn = 0;
@@ -81,11 +109,31 @@ __global__ __launch_bounds__(WG) void k_band_stats(const int *rpA, const int *ci
     const int tb = block_sum(nbad, red);
     const long long tp = block_sum(prod, red64);
     const long long tw = block_sum(wsum, red64);
-    if (threadIdx.x == 0) {
-        if (tb) atomicAdd(&bad[0], tb);
-        if (wmax) atomicMax(&bad[1], wmax);
-        if (tp) atomicAdd(reinterpret_cast<unsigned long long *>(bad + 2), (unsigned long long)tp);
-        if (tw) atomicAdd(reinterpret_cast<unsigned long long *>(bad + 4), (unsigned long long)tw);
+    if (threadIdx.x == 0) {  // (spread over BD_SLOTS copies: thousands of workgroups, no one hot address)
+        int *const b = bad + 6 * (blockIdx.x % BD_SLOTS);
+        if (tb) atomicAdd(&b[0], tb);
+        if (wmax) atomicMax(&b[1], wmax);
+        if (tp) atomicAdd(reinterpret_cast<unsigned long long *>(b + 2), (unsigned long long)tp);
+        if (tw) atomicAdd(reinterpret_cast<unsigned long long *>(b + 4), (unsigned long long)tw);
+    }
+}
+
+// the BD_SLOTS copies of the statistics into the first (one wave)
+__global__ __launch_bounds__(64) void k_band_stats_final(int *bad) {
+    const int l = threadIdx.x;
+    int nb = l < BD_SLOTS ? bad[6 * l] : 0, wm = l < BD_SLOTS ? bad[6 * l + 1] : 0;
+    long long tp = l < BD_SLOTS ? *reinterpret_cast<const long long *>(bad + 6 * l + 2) : 0;
+    long long tw = l < BD_SLOTS ? *reinterpret_cast<const long long *>(bad + 6 * l + 4) : 0;
+    nb = wave_sum(nb);
+    wm = wave_last(wave_incl_max(wm));
+    tp = wave_sum(tp);
+    tw = wave_sum(tw);
+    __syncthreads();
+    if (l == 0) {
+        bad[0] = nb;
+        bad[1] = wm;
+        *reinterpret_cast<long long *>(bad + 2) = tp;
+        *reinterpret_cast<long long *>(bad + 4) = tw;
     }
 }
 
@@ -116,61 +164,104 @@ __global__ __launch_bounds__(BD_WG) void k_band_rows(BandArgs g) {
     for (int i = tid; i < span; i += BD_WG) acc[i] = 0.0;
     reinterpret_cast<uint2 *>(hit)[tid] = make_uint2(0u, 0u);  // 256 x 8 B = BD_SPAN bytes
     __syncthreads();
-    // ---- the walk: a wave per A entry.  The wave's entries (a0 + wv + 4j) are
-    // loaded once, one per lane, and broadcast from there; the B loads of the
-    // next BD_U entries are issued before this group's LDS updates.
+    // ---- the walk: each wave takes a contiguous share of the row's A entries,
+    // so consecutive entries -- whose B rows in FEM operands are the dof
+    // triplets of one node, with identical column sets (cant: rows 3u, 3u+1,
+    // 3u+2) -- meet in one wave.  Lane l holds entries l and l + 64 of the
+    // current B row (rows of <= 128 entries); while the next B row has the same
+    // length and the same column on every lane (one ballot), its a*b is added in
+    // registers, and only a change of pattern flushes the sums to the LDS
+    // accumulator (ds_add_f64) and the hit bytes: one LDS atomic per column per
+    // run of equal B rows instead of one per product.  B rows past 128 entries
+    // go to the accumulator directly.  The next BD_U entries' B loads are in
+    // flight during each group's work.
     const int a0 = g.rpA[r], a1 = g.rpA[r + 1];
-    for (int base = a0 + wv; base < a1; base += 4 * 64) {  // wave-uniform
-        const int my = base + 4 * lane;
+    const int per = (a1 - a0 + 3) / 4;
+    const int e0 = min(a1, a0 + wv * per), e1 = min(a1, a0 + (wv + 1) * per);
+    int pc0 = -1, pc1 = -1, plen = -1;  // the pending pattern: columns of lanes l, l + 64; its length
+    double px0 = 0.0, px1 = 0.0;
+    auto put = [&](int c, double x) {
+        atomicAdd(&acc[c], x);
+        hit[c] = 1;  // (byte stores: an atomicOr into the bitmap put 32 lanes on one word)
+    };
+    auto flush = [&]() {
+        if (pc0 >= 0) put(pc0, px0);
+        if (pc1 >= 0) put(pc1, px1);
+    };
+    for (int base = e0; base < e1; base += 64) {  // wave-uniform
+        const int my = base + lane;
         int2 me = make_int2(0, 0);
         double mav = 0.0;
-        if (my < a1) {
+        if (my < e1) {
             me = g.ebnd[my];
             mav = g.vA[my];
         }
-        const int nj = min(64, (a1 - base + 3) / 4);
-        auto load = [&](int j, int o, int *c, double *x, int &mx) {
-            mx = 0;
+        const int nj = min(64, e1 - base);
+        // two register sets, a group of BD_U entries each: one loading while the
+        // other is worked on (compile-time indices: the sets stay in VGPRs)
+        int lnA[BD_U], cA0[BD_U], cA1[BD_U], lnB[BD_U], cB0[BD_U], cB1[BD_U];
+        double xA0[BD_U], xA1[BD_U], xB0[BD_U], xB1[BD_U];
+        auto load = [&](int j, int (&ln)[BD_U], int (&c0)[BD_U], int (&c1)[BD_U], double (&x0)[BD_U],
+                        double (&x1)[BD_U]) {
 #pragma unroll
             for (int k = 0; k < BD_U; ++k) {
                 const int jj = min(j + k, 63);
-                const int bs = __shfl(me.x, jj, 64), be = j + k < nj ? __shfl(me.y, jj, 64) : bs;
+                const int bs = __builtin_amdgcn_readlane(me.x, jj);
+                const int be = j + k < nj ? __builtin_amdgcn_readlane(me.y, jj) : bs;
                 const double av = __shfl(mav, jj, 64);
-                mx = max(mx, be - bs);
-                const int bb = bs + o + lane;
-                c[k] = -1;
-                x[k] = 0.0;
-                if (bb < be) {
-                    c[k] = g.Bcol[bb] - lo;
-                    x[k] = av * g.Bval[bb];
+                ln[k] = be - bs;
+                c0[k] = c1[k] = -1;
+                x0[k] = x1[k] = 0.0;
+                if (bs + lane < be) {
+                    c0[k] = g.Bcol[bs + lane] - lo;
+                    x0[k] = av * g.Bval[bs + lane];
+                }
+                if (bs + 64 + lane < be) {
+                    c1[k] = g.Bcol[bs + 64 + lane] - lo;
+                    x1[k] = av * g.Bval[bs + 64 + lane];
                 }
             }
         };
-        int c0[BD_U], c1[BD_U], mx0 = 0, mx1 = 0;
-        double x0[BD_U], x1[BD_U];
-        load(0, 0, c0, x0, mx0);
-        for (int j = 0; j < nj; j += BD_U) {
-            if (j + BD_U < nj) load(j + BD_U, 0, c1, x1, mx1);  // in flight during this group's updates
-            for (int o = 0;;) {
-#pragma unroll
-                for (int k = 0; k < BD_U; ++k)
-                    if (c0[k] >= 0) {
-                        atomicAdd(&acc[c0[k]], x0[k]);
-                        hit[c0[k]] = 1;  // (byte stores: an atomicOr into the bitmap put 32 lanes on one word)
-                    }
-                o += 64;
-                if (o >= mx0) break;  // B rows longer than 64: their next 64 entries
-                int t;
-                load(j, o, c0, x0, t);
-            }
+        auto work = [&](int j, const int (&ln)[BD_U], const int (&c0)[BD_U], const int (&c1)[BD_U],
+                        const double (&x0)[BD_U], const double (&x1)[BD_U]) {
 #pragma unroll
             for (int k = 0; k < BD_U; ++k) {
-                c0[k] = c1[k];
-                x0[k] = x1[k];
+                if (j + k >= nj) break;  // (wave-uniform)
+                const int len = ln[k];
+                if (len > 128) {  // a long B row: straight to the accumulator
+                    flush();
+                    pc0 = pc1 = plen = -1;
+                    if (c0[k] >= 0) put(c0[k], x0[k]);
+                    if (c1[k] >= 0) put(c1[k], x1[k]);
+                    const int bs = __builtin_amdgcn_readlane(me.x, j + k);
+                    const double av = __shfl(mav, j + k, 64);
+                    for (int o = 128 + lane; o < len; o += 64) put(g.Bcol[bs + o] - lo, av * g.Bval[bs + o]);
+                    continue;
+                }
+                const bool same = len == plen && __ballot(c0[k] != pc0 || c1[k] != pc1) == 0ull;
+                if (same) {
+                    px0 += x0[k];
+                    px1 += x1[k];
+                } else {
+                    flush();
+                    pc0 = c0[k];
+                    pc1 = c1[k];
+                    px0 = x0[k];
+                    px1 = x1[k];
+                    plen = len;
+                }
             }
-            mx0 = mx1;
+        };
+        load(0, lnA, cA0, cA1, xA0, xA1);
+        for (int j = 0; j < nj; j += 2 * BD_U) {  // (wave-uniform)
+            if (j + BD_U < nj) load(j + BD_U, lnB, cB0, cB1, xB0, xB1);
+            work(j, lnA, cA0, cA1, xA0, xA1);
+            if (j + BD_U >= nj) break;
+            if (j + 2 * BD_U < nj) load(j + 2 * BD_U, lnA, cA0, cA1, xA0, xA1);
+            work(j + BD_U, lnB, cB0, cB1, xB0, xB1);
         }
     }
+    flush();
     __syncthreads();
     {  // pack the marks: thread t's 8 columns [8t, 8t+8) -> bitmap byte t
         const uint2 v = reinterpret_cast<const uint2 *>(hit)[tid];
@@ -224,10 +315,11 @@ int dev_band_check(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, bool
     int *bad = nullptr;
     TSG_TRY(cx.get(&win, (size_t)A.m));
     TSG_TRY(cx.get(&width, (size_t)A.m + 1));
-    TSG_TRY(cx.get(&bad, 6));
-    TSG_HIP(hipMemsetAsync(bad, 0, 6 * sizeof(int), s));
-    k_band_stats<<<grid_for(A.m, WG, 4096), WG, 0, s>>>(A.rowpointer, A.columnindex, A.m, B.rowpointer,
+    TSG_TRY(cx.get(&bad, 6 * BD_SLOTS));
+    TSG_HIP(hipMemsetAsync(bad, 0, 6 * BD_SLOTS * sizeof(int), s));
+    k_band_stats<<<grid_for(A.m, WG / 16, 16384), WG, 0, s>>>(A.rowpointer, A.columnindex, A.m, B.rowpointer,
                                                         B.columnindex, win, width, bad);
+    k_band_stats_final<<<1, 64, 0, s>>>(bad);
     TSG_HIP(hipGetLastError());
     TSG_HIP(hipMemcpyAsync(cx.pinned + 8, bad, 6 * sizeof(int), hipMemcpyDeviceToHost, s));
     TSG_TRY(stream_wait(s));

@@ -540,7 +540,7 @@ __global__ __launch_bounds__(WG) void k_rows_small(RowsArgs g) {
         }
     }
     wave_lds_sync();
-    const u64 gm = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << gb;
+    const u64 gm = (G == 64 ? ~0ull : ((1ull << (G & 63)) - 1ull)) << gb;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         int col = -1;
@@ -2229,8 +2229,11 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
     int ncls[NCLS];
     for (int t = 0; t < NCLS; ++t) ncls[t] = p.ncls[t];
     // (exact row counts first, so that the classes write C in place, measured
-    // slower on webbase in round 3: the count kernels took 318 us against the
-    // 300 us compaction they save; the staging + compaction stays)
+    // slower on webbase twice: round 3's per-row count kernels took 318 us
+    // against the 300 us compaction they save; round 5's several-rows-per-
+    // workgroup LDS hash counts of the merge classes (k_rows_mcount, the staged
+    // S/H rows copied by row) took 326 us, e2e 1.56 vs 1.29 ms --
+    // tools/archive/rows_direct_hashcount.patch; the staging + compaction stays)
     int *Scol = nullptr;
     double *Sval = nullptr;
     TSG_TRY(cx.get(&Scol, (size_t)products + 1));
