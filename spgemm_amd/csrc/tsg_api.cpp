@@ -972,12 +972,12 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
         // band candidates first (A rows of >= 8 entries on average): the window
         // check's read-back also brings the sortedness flag
         if (!force_rows && (force_band || (A->m > 0 && A->nnz >= 8LL * A->m))) {
-            TSG_TRY(dev_rows_sorted_finish(cx, shares, s));
-            TSG_TRY(dev_band_check(cx, *A, *B, force_band, &band, &bw, s));
+            TSG_TRY(dev_band_check(cx, *A, *B, force_band, &band, &bw, s, &shares));  // (sums the shares too)
         }
         if (band && cx.pinned[1] != 0) {  // unsorted B rows: the windows mean nothing
             cx.put(bw.win);
             cx.put(bw.width);
+            cx.put(bw.ebnd);
             band = false;
         }
         long long path_id = -1;
@@ -986,6 +986,7 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
             const int rc = dev_spgemm_band(cx, *A, *B, bw, *C, &st, s, cx.ev);
             cx.put(bw.win);
             cx.put(bw.width);
+            cx.put(bw.ebnd);
             TSG_TRY(rc);
             path_id = TSG_PATH_BAND;
         } else {

@@ -51,7 +51,8 @@ static_assert(BD_WORDS == 64, "one bitmap word per lane");
 // bad[2..3] (u64) = the element products (they bound nnz(C)), bad[4..5] (u64)
 // = the windows' columns in all.
 __global__ __launch_bounds__(WG) void k_band_stats(const int *rpA, const int *ciA, int m, const int *rpB,
-                                                   const int *ciB, int2 *win, long long *width, int *bad) {
+                                                   const int *ciB, int2 *win, long long *width, int *bad,
+                                                   int2 *ebnd) {
     // 16 lanes per row, lane sl taking the row's entries sl, sl + 16, ... (four
     // entries' loads in flight): a row's ~64 entries (cant) are four dependent
     // load chains deep, not 64 (a thread per row walked them serially: 65 us)
@@ -78,6 +79,9 @@ __global__ __launch_bounds__(WG) void k_band_stats(const int *rpA, const int *ci
                     b0[u] = k[u] >= 0 ? rpB[k[u]] : 0;
                     b1[u] = k[u] >= 0 ? rpB[k[u] + 1] : 0;
                 }
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (k[u] >= 0) ebnd[a + u * G] = make_int2(b0[u], b1[u]);  // (the banded path's entry table)
 #pragma unroll
                 for (int u = 0; u < U; ++u)
                     if (b1[u] > b0[u]) {
@@ -118,9 +122,17 @@ __global__ __launch_bounds__(WG) void k_band_stats(const int *rpA, const int *ci
     }
 }
 
-// the BD_SLOTS copies of the statistics into the first (one wave)
-__global__ __launch_bounds__(64) void k_band_stats_final(int *bad) {
+// the BD_SLOTS copies of the statistics into the first (one wave); with
+// spart, also B's sortedness shares summed into the host-mapped flag (the
+// work of k_rows_sorted_final, in the same launch)
+__global__ __launch_bounds__(64) void k_band_stats_final(int *bad, const int *spart, int snb, int *sflag) {
     const int l = threadIdx.x;
+    if (spart) {
+        long long v = 0;
+        for (int i = l; i < snb; i += 64) v += spart[i];
+        v = wave_sum(v);
+        if (l == 0 && v != 0) __hip_atomic_store(sflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     int nb = l < BD_SLOTS ? bad[6 * l] : 0, wm = l < BD_SLOTS ? bad[6 * l + 1] : 0;
     long long tp = l < BD_SLOTS ? *reinterpret_cast<const long long *>(bad + 6 * l + 2) : 0;
     long long tw = l < BD_SLOTS ? *reinterpret_cast<const long long *>(bad + 6 * l + 4) : 0;
@@ -157,7 +169,7 @@ __global__ __launch_bounds__(BD_WG) void k_band_rows(BandArgs g) {
     __shared__ int wpre[BD_WORDS];
     const u32 *bm = reinterpret_cast<const u32 *>(bmb);
     const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
-    const int r = blockIdx.x;
+    const int r = xcd_item(blockIdx.x, gridDim.x);  // (neighbouring rows on one XCD: their B rows in its L2)
     const int2 w = g.win[r];
     const int lo = w.x, span = w.y >= w.x ? w.y - w.x + 1 : 0;
     const int nw = (span + 31) >> 5;
@@ -306,21 +318,28 @@ __global__ __launch_bounds__(WG) void k_band_compact(int m, const long long *sof
 // the density test).  Leaves the windows in *win_out (caller-owned, cx.put)
 // when the answer is yes.
 int dev_band_check(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, bool force, bool *ok, BandWin *bw,
-                   hipStream_t s) {
+                   hipStream_t s, SortedShares *sh) {
     *ok = false;
     *bw = BandWin{};
-    if (A.m <= 0 || A.n != B.m) return TSG_OK;
-    int2 *win = nullptr;
+    if (A.m <= 0 || A.n != B.m) return sh ? dev_rows_sorted_finish(cx, *sh, s) : TSG_OK;
+    int2 *win = nullptr, *ebnd = nullptr;
     long long *width = nullptr;
     int *bad = nullptr;
     TSG_TRY(cx.get(&win, (size_t)A.m));
     TSG_TRY(cx.get(&width, (size_t)A.m + 1));
+    TSG_TRY(cx.get(&ebnd, (size_t)A.nnz + 1));
     TSG_TRY(cx.get(&bad, 6 * BD_SLOTS));
     TSG_HIP(hipMemsetAsync(bad, 0, 6 * BD_SLOTS * sizeof(int), s));
     k_band_stats<<<grid_for(A.m, WG / 16, 16384), WG, 0, s>>>(A.rowpointer, A.columnindex, A.m, B.rowpointer,
-                                                        B.columnindex, win, width, bad);
-    k_band_stats_final<<<1, 64, 0, s>>>(bad);
+                                                        B.columnindex, win, width, bad, ebnd);
+    const bool shares = sh && sh->part;
+    k_band_stats_final<<<1, 64, 0, s>>>(bad, shares ? sh->part : nullptr, shares ? sh->nb : 0,
+                                         shares ? sh->dflag : nullptr);
     TSG_HIP(hipGetLastError());
+    if (sh) {
+        cx.put(sh->part);  // (stream-ordered reuse)
+        *sh = SortedShares{};
+    }
     TSG_HIP(hipMemcpyAsync(cx.pinned + 8, bad, 6 * sizeof(int), hipMemcpyDeviceToHost, s));
     TSG_TRY(stream_wait(s));
     cx.put(bad);
@@ -328,10 +347,11 @@ int dev_band_check(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, bool
     const long long wcols = *reinterpret_cast<const long long *>(cx.pinned + 12);
     if (cx.pinned[8] == 0 && (force || products >= wcols)) {
         *ok = true;
-        *bw = BandWin{win, width, products, wcols};
+        *bw = BandWin{win, width, products, wcols, ebnd};
     } else {
         cx.put(win);
         cx.put(width);
+        cx.put(ebnd);
     }
     return TSG_OK;
 }
@@ -353,15 +373,18 @@ int dev_spgemm_band(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, Ban
     C.m = m;
     C.n = B.n;
     if (ev) TSG_HIP(hipEventRecord(ev[0], s));
-    int2 *ebnd = nullptr;
+    int2 *ebnd = bw.ebnd;  // (filled by the window check's statistics kernel)
+    bw.ebnd = nullptr;
     int *Scol = nullptr;
     double *Sval = nullptr;
-    TSG_TRY(cx.get(&ebnd, (size_t)A.nnz + 1));
+    if (!ebnd) {
+        TSG_TRY(cx.get(&ebnd, (size_t)A.nnz + 1));
+        if (A.nnz > 0) k_band_ebnd<<<grid_for(A.nnz, WG, 16384), WG, 0, s>>>(A.columnindex, A.nnz, B.rowpointer, ebnd);
+        TSG_HIP(hipGetLastError());
+    }
     TSG_TRY(cx.get(&Scol, (size_t)bw.wcols + 1));
     TSG_TRY(cx.get(&Sval, (size_t)bw.wcols + 1));
     TSG_TRY(cx.get(&C.rowpointer, (size_t)m + 1));
-    if (A.nnz > 0) k_band_ebnd<<<grid_for(A.nnz, WG, 16384), WG, 0, s>>>(A.columnindex, A.nnz, B.rowpointer, ebnd);
-    TSG_HIP(hipGetLastError());
     {  // window widths -> staging offsets
         const int rc = dev_scan_i64_fused(cx, bw.width, (long)m + 1, s);
         if (rc == TSG_ERR_UNSUPPORTED) TSG_TRY(scan_exclusive_i64(cx, bw.width, (long)m + 1, s));

@@ -166,6 +166,17 @@ __device__ __forceinline__ int owner_search(const int *off, int n, int it) {
     return lo;
 }
 
+// XCD-aware work order: the dispatcher deals a grid's workgroups round-robin
+// over the 8 XCDs (workgroup b to XCD b % 8), each with its own L2.  This maps
+// workgroup b to item xcd_item(b, n) of n so that every XCD takes one
+// contiguous range of items, in order: neighbouring rows (which read
+// neighbouring B rows in banded and local web-graph operands) share an L2.
+constexpr int kXcds = 8;
+__device__ __forceinline__ int xcd_item(int b, int n) {
+    const int q = n / kXcds, r = n % kXcds, x = b % kXcds, k = b / kXcds;
+    return x * q + min(x, r) + k;
+}
+
 static inline int grid_for(long work, int per_block, int cap) {
     long g = (work + per_block - 1) / per_block;
     if (g < 1) g = 1;

@@ -1097,13 +1097,24 @@ __global__ __launch_bounds__(WG) void k_step1_cap_tiles(const int *Atp, const in
     }
 }
 
-// compact the EL step-1 unit buffers into tile_columnidx (workgroup per unit)
+// compact the step-1 unit buffers into tile_columnidx: a wave per unit (a
+// unit holds ~1 K tile columns on webbase: a workgroup per unit left most of
+// its lanes idle), four loads in flight per lane
 __global__ __launch_bounds__(WG) void k_step1_gather(const int *ubuf, const long long *ubuf_off, const int *unit_off,
                                                      long nunits, int *Ccol) {
-    for (long u = blockIdx.x; u < nunits; u += gridDim.x) {
+    const int lane = lane_id();
+    for (long u = (long)blockIdx.x * WAVES + wave_id(); u < nunits; u += (long)gridDim.x * WAVES) {
         const int o = unit_off[u], n = unit_off[u + 1] - o;
         const int *src = ubuf + ubuf_off[u];
-        for (int q = threadIdx.x; q < n; q += WG) Ccol[o + q] = src[q];
+        int q = lane;
+        for (; q + 192 < n; q += 256) {
+            const int v0 = src[q], v1 = src[q + 64], v2 = src[q + 128], v3 = src[q + 192];
+            Ccol[o + q] = v0;
+            Ccol[o + q + 64] = v1;
+            Ccol[o + q + 128] = v2;
+            Ccol[o + q + 192] = v3;
+        }
+        for (; q < n; q += 64) Ccol[o + q] = src[q];
     }
 }
 
@@ -2473,7 +2484,8 @@ int dev_step1(Context &cx, const tsg_dev_tiles &A, const tsg_dev_tiles &B, tsg_d
     TSG_TRY(cx.get(&C.tile_columnidx, nb1));
     if (tilemA > 0) {
         if (ubuf)
-            k_step1_gather<<<g1, WG, 0, s>>>(ubuf, ubuf_off, ucnt, nunits1, C.tile_columnidx);
+            k_step1_gather<<<grid_for(nunits1, WAVES, 16384), WG, 0, s>>>(ubuf, ubuf_off, ucnt, nunits1,
+                                                                           C.tile_columnidx);
         else if (bmst)
             k_step1<2><<<g1, WG, 0, s>>>(A.tile_ptr, A.tile_columnidx, B.tile_ptr, B.tile_columnidx, tilemA, tilenB,
                                          nwin, win, nullptr, ucnt, C.tile_columnidx, nullptr, bmst);

@@ -140,9 +140,11 @@ struct BandWin {
     long long *width = nullptr;  // per row: window width (+1 slot), scanned into staging offsets
     long long products = 0;      // element products (nnzCub)
     long long wcols = 0;         // window columns in all (bounds nnz(C))
+    int2 *ebnd = nullptr;        // per A entry: its B row's [start, end) (the statistics kernel's by-product)
 };
+// sh (optional): B's sortedness shares, summed by the check's last kernel (and released)
 int dev_band_check(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, bool force, bool *ok, BandWin *bw,
-                   hipStream_t s);
+                   hipStream_t s, SortedShares *sh = nullptr);
 int dev_spgemm_band(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, BandWin &bw, tsg_dev_csr &C,
                     tsg_stats *st, hipStream_t s, hipEvent_t *ev);
 // row-merge path (tsg_rows.hip): CSR in -> CSR out, B's rows column-sorted;

@@ -15,6 +15,9 @@ fi
 for ab in ${AB:-}; do  # matrix:variant (spgemm_amd/lib/variants/libtsg_<variant>.so)
   bash tools/r4_ab.sh ${TAG}_${ab%%:*} "${ab#*:}" --matrix ${ab%%:*} || exit 1
 done
+for ab in ${TAB:-}; do  # matrix:variant, the tiled drop-in leg (tsg_tilespgemm)
+  bash tools/r4_ab.sh ${TAG}_tiled_${ab%%:*} "${ab#*:}" --matrix ${ab%%:*} --leg tiled --steps 5 || exit 1
+done
 for ab in ${ENVAB:-}; do  # matrix:VAR=VALUE
   bash tools/r4_abenv.sh ${TAG}_${ab%%:*} "${ab#*:}" --matrix ${ab%%:*} || exit 1
 done
