@@ -229,6 +229,11 @@ def tiled_leg(m, n, rp, ci, vv, mb, nb, rpb, cib, vvb, aat, tm, nnzcub, reps=3, 
             "t_step1_ms": round(med("time_step1"), 4), "t_step2_ms": round(med("time_step2"), 4),
             "t_step3_ms": round(med("time_step3"), 4), "t_malloc_ms": round(med("time_malloc"), 4),
             "numblkC": numblk, "nnzC": nnzc, "reps": reps, "tile": tm,
+            "step_times_overlap": tm == 16,
+            "step_times_note": ("16x16 CSR route: step 1 runs on its own stream beside steps 2-3, so the three "
+                                "step times overlap and do not add up to t_kern_tiled_ms (t_malloc_ms, the "
+                                "remainder, clamps at 0); the reference's steps run one after another")
+                               if tm == 16 else "steps 1-3 in turn",
             "roofline": {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
                          "algorithmic_bytes": int(b_alg), "achieved": round(b_alg / (t * 1e-3) / 1e9, 2),
                          "frac": round(b_alg / (t * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),

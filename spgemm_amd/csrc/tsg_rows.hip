@@ -2413,7 +2413,12 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
             if (fused_scan) {
                 int *part = nullptr;
                 TSG_TRY(cx.get(&part, (size_t)rtile));
-                TSG_TRY(cx.get(&cfirst, (size_t)((products + CP_CH - 1) / CP_CH) + 1));
+                // the apply fills the compaction's chunk table, a row's chunks by
+                // one thread: fine for short rows, serial for hub rows (a 3.5 M-
+                // nonzero LiveJournal row: 1.7 K chunks, ~50 us) -- past 2^20
+                // products in a row, k_rows_cfirst (a thread per chunk) after it
+                if (p.pmax <= (1LL << 20))
+                    TSG_TRY(cx.get(&cfirst, (size_t)((products + CP_CH - 1) / CP_CH) + 1));
                 k_rows_count_sum<int><<<(unsigned)rtile, WG, 0, s>>>(C.rowpointer, (long)m + 1, part);
                 k_rows_scan_apply<int, true><<<(unsigned)rtile, WG, 0, s>>>(
                     C.rowpointer, (long)m + 1, part, cfirst, m, reinterpret_cast<int *>(cx.dpinned64 + 15));
