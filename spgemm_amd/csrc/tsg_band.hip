@@ -89,6 +89,10 @@ __global__ __launch_bounds__(WG) void k_band_stats(const int *rpA, const int *ci
                         hi = max(hi, ciB[b1[u] - 1]);
                         q += b1[u] - b0[u];
                     }
+                // this lane's share is already wider than a window: the row is
+                // (its products and entry table only matter when every row fits,
+                // and this one does not -- a hub row's 10^5 entries stop here)
+                if (hi >= lo && hi - lo >= BD_SPAN) break;
             }
         }
 #pragma unroll

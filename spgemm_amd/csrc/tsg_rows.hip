@@ -2000,19 +2000,34 @@ __global__ __launch_bounds__(DR_NT) void k_rows_dr_fill(RowsArgs g, const int *C
     __syncthreads();
     int *const Ocol = Ccol + Crp[d.r];
     double *const Oval = Cval + Crp[d.r];
-    for (int i = i0 + tid; i < i1; i += DR_NT) {
-        const int c = g.Bcol[d.bs + i];
-        double v = d.aL * g.Bval[d.bs + i];
-        // entries with p <= i: the count t; the inserted ones before i = nd of entry t
-        int lo = 0, hi = ne;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (sp[mid] <= i) lo = mid + 1; else hi = mid;
+    // the run streamed: DR_U elements per thread with every load issued first,
+    // C written with streaming (nontemporal) stores -- this call never reads it
+    constexpr int DR_U = 4;
+    for (int ib = i0 + tid; ib < i1; ib += DR_U * DR_NT) {
+        int c[DR_U];
+        double v[DR_U];
+#pragma unroll
+        for (int u = 0; u < DR_U; ++u) {
+            const int i = ib + u * DR_NT;
+            c[u] = i < i1 ? g.Bcol[d.bs + i] : 0;
+            v[u] = i < i1 ? g.Bval[d.bs + i] : 0.0;
         }
-        const int ins = lo < ne ? snd[lo] : (ne ? snd[ne - 1] + !sdup[ne - 1] : nd0);
-        if (lo > 0 && sp[lo - 1] == i && sdup[lo - 1]) v += sval[lo - 1];
-        Ocol[i + ins] = c;
-        Oval[i + ins] = v;
+#pragma unroll
+        for (int u = 0; u < DR_U; ++u) {
+            const int i = ib + u * DR_NT;
+            if (i >= i1) break;
+            double x = d.aL * v[u];
+            // entries with p <= i: the count t; the inserted ones before i = nd of entry t
+            int lo = 0, hi = ne;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (sp[mid] <= i) lo = mid + 1; else hi = mid;
+            }
+            const int ins = lo < ne ? snd[lo] : (ne ? snd[ne - 1] + !sdup[ne - 1] : nd0);
+            if (lo > 0 && sp[lo - 1] == i && sdup[lo - 1]) x += sval[lo - 1];
+            __builtin_nontemporal_store(c[u], Ocol + i + ins);
+            __builtin_nontemporal_store(x, Oval + i + ins);
+        }
     }
     for (int t = tid; t < ne; t += DR_NT)
         if (!sdup[t]) {
