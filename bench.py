@@ -270,13 +270,18 @@ def pmc_traffic(kernels, path):
     if not path:
         return None, None
     d = json.load(open(path))
+    calls = (d.get("_per_call") or {}).get("calls")
     tot, found = 0, False
     for kernel in kernels:  # (the kernels of the unit that ran for this workload)
         hits = [v for k, v in d.items() if kernel in k and isinstance(v, dict) and v.get("hbm_bytes_per_dispatch")]
         found |= bool(hits)
-        tot += sum(int(v["hbm_bytes_per_dispatch"]) for v in hits)
+        for v in hits:
+            # per call: a kernel dispatched several times per call (sequential row
+            # blocks: once per block) counts every dispatch
+            per_call = v["dispatches"] / calls if calls and v.get("dispatches") else 1.0
+            tot += int(v["hbm_bytes_per_dispatch"]) * max(1.0, per_call)
     allk = (d.get("_per_call") or {}).get("hbm_bytes")
-    return (tot if found else None), allk
+    return (int(tot) if found else None), allk
 
 
 def main():
