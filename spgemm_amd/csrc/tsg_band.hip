@@ -126,17 +126,20 @@ __global__ __launch_bounds__(WG) void k_band_stats(const int *rpA, const int *ci
     }
 }
 
-// the BD_SLOTS copies of the statistics into the first (one wave); with
-// spart, also B's sortedness shares summed into the host-mapped flag (the
-// work of k_rows_sorted_final, in the same launch)
-__global__ __launch_bounds__(64) void k_band_stats_final(int *bad, const int *spart, int snb, int *sflag) {
+// the BD_SLOTS copies of the statistics into the first (the first wave); with
+// spart, also B's sortedness shares (up to 4,096) summed by the workgroup into
+// the host-mapped flag (the work of k_rows_sorted_final, in the same launch)
+__global__ __launch_bounds__(WG) void k_band_stats_final(int *bad, const int *spart, int snb, int *sflag) {
+    __shared__ long long red[WAVES];
     const int l = threadIdx.x;
-    if (spart) {
+    if (spart) {  // (workgroup-uniform)
         long long v = 0;
-        for (int i = l; i < snb; i += 64) v += spart[i];
-        v = wave_sum(v);
+#pragma unroll 8
+        for (int i = l; i < snb; i += WG) v += spart[i];
+        v = block_sum(v, red);
         if (l == 0 && v != 0) __hip_atomic_store(sflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    if (l >= 64) return;
     int nb = l < BD_SLOTS ? bad[6 * l] : 0, wm = l < BD_SLOTS ? bad[6 * l + 1] : 0;
     long long tp = l < BD_SLOTS ? *reinterpret_cast<const long long *>(bad + 6 * l + 2) : 0;
     long long tw = l < BD_SLOTS ? *reinterpret_cast<const long long *>(bad + 6 * l + 4) : 0;
@@ -144,8 +147,7 @@ __global__ __launch_bounds__(64) void k_band_stats_final(int *bad, const int *sp
     wm = wave_last(wave_incl_max(wm));
     tp = wave_sum(tp);
     tw = wave_sum(tw);
-    __syncthreads();
-    if (l == 0) {
+    if (l == 0) {  // (one wave: its reads of every slot are done, the sums need them)
         bad[0] = nb;
         bad[1] = wm;
         *reinterpret_cast<long long *>(bad + 2) = tp;
@@ -337,7 +339,7 @@ int dev_band_check(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, bool
     k_band_stats<<<grid_for(A.m, WG / 16, 16384), WG, 0, s>>>(A.rowpointer, A.columnindex, A.m, B.rowpointer,
                                                         B.columnindex, win, width, bad, ebnd);
     const bool shares = sh && sh->part;
-    k_band_stats_final<<<1, 64, 0, s>>>(bad, shares ? sh->part : nullptr, shares ? sh->nb : 0,
+    k_band_stats_final<<<1, WG, 0, s>>>(bad, shares ? sh->part : nullptr, shares ? sh->nb : 0,
                                          shares ? sh->dflag : nullptr);
     TSG_HIP(hipGetLastError());
     if (sh) {

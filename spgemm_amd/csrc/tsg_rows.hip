@@ -1744,6 +1744,35 @@ __global__ __launch_bounds__(W_NT) void k_rows_wunit(RowsArgs g, const int *umap
 #pragma unroll
     for (int t = 0; t < W_RPT; ++t) rk[t] = cc[t] >= 0 ? w_rank(bm, g4, blk, cc[t]) : 0;
     const long long o0 = wpre[i] + ubo[u];
+    static_assert(2 * W_WORDS >= W_RPT * W_NT, "the bitmap's LDS holds a column per rank (wn <= n)");
+    if (n <= W_RPT * W_NT) {  // (workgroup-uniform) every product in registers
+        // the bitmap is done with once the ranks are: its LDS takes each rank's
+        // column (a column's products store the same one), the values are
+        // summed at their ranks W_VCAP at a time, and both go out coalesced
+        // (consecutive lanes, consecutive ranks) -- not a thread per bitmap
+        // word emitting its bits
+        int *const cl = reinterpret_cast<int *>(bm);
+        __syncthreads();  // (every rank read from the bitmap)
+#pragma unroll
+        for (int t = 0; t < W_RPT; ++t)
+            if (cc[t] >= 0) cl[rk[t]] = cc[t];
+        for (int r0 = 0; r0 < wn; r0 += W_VCAP) {  // (workgroup-uniform)
+            const int r1 = min(wn, r0 + W_VCAP);
+            for (int j = tid; j < r1 - r0; j += W_NT) vals[j] = 0.0;
+            __syncthreads();
+#pragma unroll
+            for (int t = 0; t < W_RPT; ++t)
+                if (cc[t] >= 0 && (unsigned)(rk[t] - r0) < (unsigned)W_VCAP) atomicAdd(&vals[rk[t] - r0], xx[t]);
+            __syncthreads();
+            for (int j = tid; j < r1 - r0; j += W_NT) {
+                Ocol[o0 + r0 + j] = (int)(wlo0 + cl[r0 + j]);
+                Oval[o0 + r0 + j] = vals[j];
+            }
+            __syncthreads();  // (the pass's values read before the next pass zeroes them)
+        }
+        if (tid == 0) ucount[u] = wn;
+        return;
+    }
     for (int r0 = 0; r0 < wn; r0 += W_VCAP) {  // (workgroup-uniform; one pass unless wn > W_VCAP)
         const int r1 = min(wn, r0 + W_VCAP);
         for (int j = tid; j < r1 - r0; j += W_NT) vals[j] = 0.0;
