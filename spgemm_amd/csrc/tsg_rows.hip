@@ -1582,10 +1582,24 @@ __global__ __launch_bounds__(W_NT) void k_rows_wcount(RowsArgs g, const int4 *ch
         if (hist[w]) cb[w] = atomicAdd(&ucnt[u0 + w], hist[w]);
 }
 
+// a unit's work record (k_rows_wscan writes it beside the bucket offsets): the
+// unit kernel's one dependent load before its bucket loads (reading umap ->
+// list -> E first cost three round trips per unit)
+struct WUnit {
+    long long s0;   // its bucket in the row's staging slots
+    long long o0;   // its output slots
+    int wlo0;       // its window's first column
+    int wb;         // window bits
+    int n;          // its bucket's products
+    int pad;
+};
+
 // per W row (a workgroup per class-H row): out[u] = exclusive scan of in[u]
-// over the row's units; rnnz (optional) gets the row's total
+// over the row's units; rnnz (optional) gets the row's total; rec (optional,
+// with wlo, wwb, wpre) the units' work records
 __global__ __launch_bounds__(W_NT) void k_rows_wscan(RowsArgs g, const int *ubase, const int *in, int *out,
-                                                    int *rnnz) {
+                                                    int *rnnz, WUnit *rec = nullptr, const int *wlo = nullptr,
+                                                    const int *wwb = nullptr, const long long *wpre = nullptr) {
     constexpr int NW = W_NT / 64, PT = W_MAXW / W_NT;
     __shared__ int red[NW];
     const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
@@ -1607,10 +1621,21 @@ __global__ __launch_bounds__(W_NT) void k_rows_wscan(RowsArgs g, const int *ubas
         off += w < wv ? red[w] : 0;
         tot += red[w];
     }
+    long long rb = 0, ob = 0;
+    int lo = 0, wb = 0;
+    if (rec) {  // (kernel-uniform)
+        rb = g.E[g.list[blockIdx.x].y];
+        ob = wpre[blockIdx.x];
+        lo = wlo[blockIdx.x];
+        wb = wwb[blockIdx.x];
+    }
 #pragma unroll
     for (int t = 0; t < PT; ++t) {
         const int w = tid * PT + t;
-        if (w < nw) out[u0 + w] = off;
+        if (w < nw) {
+            out[u0 + w] = off;
+            if (rec) rec[u0 + w] = WUnit{rb + off, ob + off, lo + (w << wb), wb, v[t], 0};
+        }
         off += v[t];
     }
     if (rnnz && tid == 0) rnnz[g.list[blockIdx.x].x] = tot;
@@ -1676,26 +1701,26 @@ __device__ __forceinline__ int w_rank(const u64 *bm, const u16 *g4, const int *b
 // a workgroup per unit u (row i = umap[u], window u - ubase[i]): its bucket
 // (ucnt[u] products at E[a0] + ubo[u]) -> its nonzeros, column-sorted, at
 // Ocol/Oval + wpre[i] + ubo[u]; ucount[u] = their number
-__global__ __launch_bounds__(W_NT) void k_rows_wunit(RowsArgs g, const int *umap, const int *ubase, const int *wlo,
-                                                    const int *wwb, const long long *wpre, const int *ucnt,
-                                                    const int *ubo, int *ucount, int *Ocol, double *Oval) {
+__global__ __launch_bounds__(W_NT) void k_rows_wunit(RowsArgs g, const WUnit *urec, int *ucount, int *Ocol,
+                                                    double *Oval) {
     constexpr int NW = W_NT / 64;
     __shared__ __align__(16) u64 bm[W_WORDS];
     __shared__ u16 g4[W_WORDS / 4];
     __shared__ int blk[W_NBLK];
     __shared__ __align__(16) double vals[W_VCAP];
     __shared__ int red[NW];
+    RP_INIT
     const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
-    const int u = blockIdx.x, i = umap[u];
-    const int n = ucnt[u];
+    const int u = blockIdx.x;
+    const WUnit R = urec[u];
+    const int n = R.n;
     if (n == 0) {  // (workgroup-uniform)
         if (tid == 0) ucount[u] = 0;
         return;
     }
-    const int4 le = g.list[i];
-    const int wb = wwb[i];
-    const long long wlo0 = (long long)wlo[i] + ((long long)(u - ubase[i]) << wb);
-    const long long s0 = g.E[le.y] + ubo[u];
+    const int wb = R.wb;
+    const long long wlo0 = R.wlo0;
+    const long long s0 = R.s0;
     const int nwd = 1 << (wb - 6);
     for (int w = tid; w < nwd; w += W_NT) bm[w] = 0ull;
     // the first W_RPT * W_NT products in registers (the rest read again below)
@@ -1708,6 +1733,7 @@ __global__ __launch_bounds__(W_NT) void k_rows_wunit(RowsArgs g, const int *umap
         xx[t] = q < n ? g.Sval[s0 + q] : 0.0;
     }
     __syncthreads();
+    RP(0);
 #pragma unroll
     for (int t = 0; t < W_RPT; ++t)
         if (cc[t] >= 0) atomicOr(&bm[cc[t] >> 6], 1ull << (cc[t] & 63));
@@ -1716,6 +1742,7 @@ __global__ __launch_bounds__(W_NT) void k_rows_wunit(RowsArgs g, const int *umap
         atomicOr(&bm[c >> 6], 1ull << (c & 63));
     }
     __syncthreads();
+    RP(1);
     // ranks: a wave per W_BLK-word block (a lane: two 4-word groups), then the blocks
     for (int bb = wv; bb * W_BLK < nwd; bb += NW) {
         const int w0 = bb * W_BLK + lane * 8;
@@ -1740,10 +1767,11 @@ __global__ __launch_bounds__(W_NT) void k_rows_wunit(RowsArgs g, const int *umap
     }
     __syncthreads();
     const int wn = red[0];
+    RP(2);
     int rk[W_RPT];
 #pragma unroll
     for (int t = 0; t < W_RPT; ++t) rk[t] = cc[t] >= 0 ? w_rank(bm, g4, blk, cc[t]) : 0;
-    const long long o0 = wpre[i] + ubo[u];
+    const long long o0 = R.o0;
     static_assert(2 * W_WORDS >= W_RPT * W_NT, "the bitmap's LDS holds a column per rank (wn <= n)");
     if (n <= W_RPT * W_NT) {  // (workgroup-uniform) every product in registers
         // the bitmap is done with once the ranks are: its LDS takes each rank's
@@ -1756,6 +1784,7 @@ __global__ __launch_bounds__(W_NT) void k_rows_wunit(RowsArgs g, const int *umap
 #pragma unroll
         for (int t = 0; t < W_RPT; ++t)
             if (cc[t] >= 0) cl[rk[t]] = cc[t];
+        RP(3);
         for (int r0 = 0; r0 < wn; r0 += W_VCAP) {  // (workgroup-uniform)
             const int r1 = min(wn, r0 + W_VCAP);
             for (int j = tid; j < r1 - r0; j += W_NT) vals[j] = 0.0;
@@ -1764,13 +1793,16 @@ __global__ __launch_bounds__(W_NT) void k_rows_wunit(RowsArgs g, const int *umap
             for (int t = 0; t < W_RPT; ++t)
                 if (cc[t] >= 0 && (unsigned)(rk[t] - r0) < (unsigned)W_VCAP) atomicAdd(&vals[rk[t] - r0], xx[t]);
             __syncthreads();
+            RP(4);
             for (int j = tid; j < r1 - r0; j += W_NT) {
                 Ocol[o0 + r0 + j] = (int)(wlo0 + cl[r0 + j]);
                 Oval[o0 + r0 + j] = vals[j];
             }
             __syncthreads();  // (the pass's values read before the next pass zeroes them)
+            RP(5);
         }
         if (tid == 0) ucount[u] = wn;
+        RP_DONE(0);
         return;
     }
     for (int r0 = 0; r0 < wn; r0 += W_VCAP) {  // (workgroup-uniform; one pass unless wn > W_VCAP)
@@ -2324,6 +2356,7 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
     // windowed (W) rows' arrays: per class-H row, per unit, per chunk
     int *wnw = nullptr, *wnch = nullptr, *wlo = nullptr, *wwb = nullptr, *umap = nullptr;
     int *ucnt = nullptr, *ubo = nullptr, *ucount = nullptr, *uoff = nullptr, *Wc = nullptr;
+    WUnit *urec = nullptr;
     long long *wpre = nullptr, *wmat = nullptr, *cmoff = nullptr;
     int *cbo = nullptr;
     unsigned long long *wst = nullptr;
@@ -2389,6 +2422,7 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
             TSG_TRY(cx.get(&ubo, (size_t)nu));
             TSG_TRY(cx.get(&ucount, (size_t)nu));
             TSG_TRY(cx.get(&uoff, (size_t)nu));
+            TSG_TRY(cx.get(&urec, (size_t)nu));
             TSG_TRY(cx.get(&Wc, (size_t)wprod + 1));
             TSG_TRY(cx.get(&Wv, (size_t)wprod + 1));
             TSG_HIP(hipMemsetAsync(ucnt, 0, (size_t)nu * sizeof(int), s));
@@ -2398,11 +2432,11 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
             TSG_HIP(hipGetLastError());
             k_rows_wcount<<<nc, W_NT, 0, s>>>(g, wchunks, cmoff, wlo, wwb, ubase, ucnt, cbo);
             TSG_HIP(hipGetLastError());
-            k_rows_wscan<<<n7, W_NT, 0, s>>>(g, ubase, ucnt, ubo, nullptr);
+            k_rows_wscan<<<n7, W_NT, 0, s>>>(g, ubase, ucnt, ubo, nullptr, urec, wlo, wwb, wpre);
             TSG_HIP(hipGetLastError());
             k_rows_wscatter<<<nc, W_NT, 0, s>>>(g, wchunks, cmoff, wlo, wwb, ubase, ubo, cbo);
             TSG_HIP(hipGetLastError());
-            k_rows_wunit<<<nu, W_NT, 0, s>>>(g, umap, ubase, wlo, wwb, wpre, ucnt, ubo, ucount, Wc, Wv);
+            k_rows_wunit<<<nu, W_NT, 0, s>>>(g, urec, ucount, Wc, Wv);
             TSG_HIP(hipGetLastError());
             k_rows_wscan<<<n7, W_NT, 0, s>>>(g, ubase, ucount, uoff, g.rnnz);
             TSG_HIP(hipGetLastError());
@@ -2560,7 +2594,8 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
     cx.put(Scol);
     cx.put(Sval);
     {
-        void *ws[] = {wnw, wnch, wlo, wwb, wpre, wmat, wst, wchunks, cmoff, cbo, umap, ucnt, ubo, ucount, uoff, Wc, Wv};
+        void *ws[] = {wnw, wnch, wlo, wwb, wpre, wmat, wst, wchunks, cmoff, cbo, umap, ucnt, ubo, ucount, uoff, Wc, Wv,
+                      urec};
         for (void *q : ws) cx.put(q);
     }
     cx.put(Oc);
