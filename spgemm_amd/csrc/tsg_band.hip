@@ -160,12 +160,13 @@ struct BandArgs {
     const double *vA;
     const int2 *ebnd;
     const int2 *win;
-    const long long *soff;  // staging offset of each row (prefix of the window widths)
+    const long long *soff;  // staging offset of each row (prefix of the window widths; null: r * BD_SPAN)
     const int *Bcol;
     const double *Bval;
     int *rnnz;              // nnz of each row (the row pointers after a scan)
     int *Scol;              // staging: each row's columns / values from soff[r]
     double *Sval;
+    int m;                  // (rnnz[m] := 0, the scan's n+1 slot)
 };
 
 __global__ __launch_bounds__(BD_WG) void k_band_rows(BandArgs g) {
@@ -295,7 +296,8 @@ __global__ __launch_bounds__(BD_WG) void k_band_rows(BandArgs g) {
     }
     __syncthreads();
     // ---- the row's columns and values, in column order, to the staging area
-    const long long E = g.soff[r];
+    if (r == 0 && tid == 0) g.rnnz[g.m] = 0;
+    const long long E = g.soff ? g.soff[r] : (long long)r * BD_SPAN;
     for (int i = tid; i < span; i += BD_WG) {
         const u32 word = bm[i >> 5], bit = 1u << (i & 31);
         if (word & bit) {
@@ -310,9 +312,25 @@ __global__ __launch_bounds__(BD_WG) void k_band_rows(BandArgs g) {
 __global__ __launch_bounds__(WG) void k_band_compact(int m, const long long *soff, const int *Crp, const int *Scol,
                                                      const double *Sval, int *Ccol, double *Cval) {
     for (int r = blockIdx.x * WAVES + wave_id(); r < m; r += gridDim.x * WAVES) {
-        const long long s0 = soff[r];
+        const long long s0 = soff ? soff[r] : (long long)r * BD_SPAN;
         const int d0 = Crp[r], n = Crp[r + 1] - d0;
-        for (int i = lane_id(); i < n; i += 64) {
+        // (a cant row: ~280 nonzeros -- every load of a lane issued before its stores)
+        int i = lane_id();
+        for (; i + 192 < n; i += 256) {
+            int c[4];
+            double v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                c[u] = Scol[s0 + i + 64 * u];
+                v[u] = Sval[s0 + i + 64 * u];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                Ccol[d0 + i + 64 * u] = c[u];
+                Cval[d0 + i + 64 * u] = v[u];
+            }
+        }
+        for (; i < n; i += 64) {
             Ccol[d0 + i] = Scol[s0 + i];
             Cval[d0 + i] = Sval[s0 + i];
         }
@@ -388,18 +406,23 @@ int dev_spgemm_band(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, Ban
         if (A.nnz > 0) k_band_ebnd<<<grid_for(A.nnz, WG, 16384), WG, 0, s>>>(A.columnindex, A.nnz, B.rowpointer, ebnd);
         TSG_HIP(hipGetLastError());
     }
-    TSG_TRY(cx.get(&Scol, (size_t)bw.wcols + 1));
-    TSG_TRY(cx.get(&Sval, (size_t)bw.wcols + 1));
+    // staging: BD_SPAN slots per row while that stays within 2 GiB (no scan of
+    // the window widths: two launches fewer), else the widths' prefix
+    const bool fixed = (long long)m * BD_SPAN * 12 <= (2LL << 30);
+    const long long slots = fixed ? (long long)m * BD_SPAN : bw.wcols;
+    TSG_TRY(cx.get(&Scol, (size_t)slots + 1));
+    TSG_TRY(cx.get(&Sval, (size_t)slots + 1));
     TSG_TRY(cx.get(&C.rowpointer, (size_t)m + 1));
-    {  // window widths -> staging offsets
+    if (!fixed) {  // window widths -> staging offsets
         const int rc = dev_scan_i64_fused(cx, bw.width, (long)m + 1, s);
         if (rc == TSG_ERR_UNSUPPORTED) TSG_TRY(scan_exclusive_i64(cx, bw.width, (long)m + 1, s));
         else TSG_TRY(rc);
     }
+    const long long *soff = fixed ? nullptr : bw.width;
     if (ev) TSG_HIP(hipEventRecord(ev[1], s));
     if (ev) TSG_HIP(hipEventRecord(ev[4], s));
     if (m > 0) {
-        BandArgs g{A.rowpointer, A.value, ebnd, bw.win, bw.width, B.columnindex, B.value, C.rowpointer, Scol, Sval};
+        BandArgs g{A.rowpointer, A.value, ebnd, bw.win, soff, B.columnindex, B.value, C.rowpointer, Scol, Sval, m};
         k_band_rows<<<m, BD_WG, 0, s>>>(g);
         TSG_HIP(hipGetLastError());
     }
@@ -410,7 +433,7 @@ int dev_spgemm_band(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, Ban
     // compaction (the fused scan stores it through host-mapped memory); else the
     // checked scan reads it back first and C is sized exactly.
     long long nnz = 0;
-    TSG_HIP(hipMemsetAsync(C.rowpointer + m, 0, sizeof(int), s));
+    if (m == 0) TSG_HIP(hipMemsetAsync(C.rowpointer + m, 0, sizeof(int), s));  // (else k_band_rows writes it)
     bool fused = bw.wcols <= 0x7fffffffLL && bw.wcols * 12 <= kRowsProductSizedC;
     int *const hnnz = reinterpret_cast<int *>(cx.pinned64 + 15);
     if (fused) {
@@ -434,7 +457,7 @@ int dev_spgemm_band(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, Ban
         TSG_TRY(cx.get(&C.value, (size_t)nnz + 1));
     }
     if (m > 0)
-        k_band_compact<<<grid_for(m, WAVES, 16384), WG, 0, s>>>(m, bw.width, C.rowpointer, Scol, Sval, C.columnindex,
+        k_band_compact<<<grid_for(m, WAVES, 16384), WG, 0, s>>>(m, soff, C.rowpointer, Scol, Sval, C.columnindex,
                                                                C.value);
     TSG_HIP(hipGetLastError());
     if (ev) TSG_HIP(hipEventRecord(ev[3], s));
