@@ -53,7 +53,9 @@ constexpr int M3_CAP = 2048, M3_RUNS = 504, M3_NT = 512;   // 40,912 B
 constexpr int M4_CAP = 4096, M4_RUNS = 512, M4_NT = 1024;  // 72 KB
 constexpr int NCLS = 8;               // S16, S64, M0..M4, H
 constexpr int DR_SMAX = 4096;         // hub rows: products outside the dominant run (the DR kernels)
-constexpr int DR_CH = 65536;          // DR fill: dominant-run elements per workgroup
+constexpr int DR_CH = 16384;          // DR fill: dominant-run elements per chunk
+constexpr int DR_GR = 16;             // DR fill: rows of one run per chunk (the run's range read once for them)
+constexpr int DR_GMAX = 8192;         // DR rows grouped by run in one workgroup's LDS (more: a chunk per row)
 constexpr int BIN_ROWS = 2048;        // rows per workgroup of the binning kernel
 constexpr int RH_NT = 1024;           // class H: workgroup
 constexpr int RH_WORDS = 16384;       // class H: bitmap words (u64) per window: 128 KB of LDS
@@ -1883,8 +1885,8 @@ struct DrEnt {     // one S column (sorted by column): insertion point, kind, co
 constexpr int DR_NT = 1024;
 
 __global__ __launch_bounds__(DR_NT) void k_rows_dr_prep(RowsArgs g, long long *soff, DrRow *rows, DrEnt *ents,
-                                                        int2 *chunks,
-                                                        int *nchunk, int *ndr) {
+                                                        int *ord, int4 *chunks, int *nchunk, int *ndr,
+                                                        int enq) {
     constexpr int NW = DR_NT / 64;
     __shared__ unsigned long long sk[DR_SMAX];  // (column << 12 | S position), sorted
     __shared__ double sv[DR_SMAX];              // S values by S position
@@ -2017,85 +2019,204 @@ __global__ __launch_bounds__(DR_NT) void k_rows_dr_prep(RowsArgs g, long long *s
         rows[h] = d;
         g.rnnz[r] = (int)L + ndt;
         soff[r] = -1;  // (the compaction skips the row: k_rows_dr_fill writes it into C)
-        const int nch = (int)((L + DR_CH - 1) / DR_CH);
-        const int c0 = atomicAdd(nchunk, nch);
-        for (int c = 0; c < nch; ++c) chunks[c0 + c] = make_int2(h, c * DR_CH);
+        if (enq) {     // (more DR rows than k_rows_dr_group sorts: a chunk per row and range)
+            ord[h] = h;
+            const int nch = (int)((L + DR_CH - 1) / DR_CH);
+            const int c0 = atomicAdd(nchunk, nch);
+            for (int c = 0; c < nch; ++c) chunks[c0 + c] = make_int4(h, 1, c * DR_CH, 0);
+        }
     }
 }
 
+// one workgroup: the DR rows sorted by their run (B position) -> ord; a run's
+// rows (mawi: every hub neighbour holds the hub's whole B row) cut into blocks
+// of DR_GR, each block's chunks one per DR_CH range of the run -- so the fill
+// reads the run once per block, not once per row (149 mawi rows re-read a
+// 120 MB run: 18.7 GB of fetch beside 19.4 GB of writes, r5p).  A run's chunks
+// are range-major (the blocks of one range adjacent).
+__global__ __launch_bounds__(DR_NT) void k_rows_dr_group(const DrRow *rows, const int *ndrp, int *ord, int4 *chunks,
+                                                         int *nchunk) {
+    constexpr int NW = DR_NT / 64, PT = DR_GMAX / DR_NT;
+    __shared__ unsigned long long sk[DR_GMAX];  // (run start << 32 | row slot), sorted
+    __shared__ int red[NW];
+    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    const int n = *ndrp;
+    int npow = 1;
+    while (npow < n) npow <<= 1;
+    for (int q = tid; q < npow; q += DR_NT)
+        sk[q] = q < n ? ((unsigned long long)(unsigned)rows[q].bs << 32) | (unsigned)q : ~0ull;
+    __syncthreads();
+    for (int K = 2; K <= npow; K <<= 1)
+        for (int J = K >> 1; J > 0; J >>= 1) {
+            for (int i = tid; i < npow; i += DR_NT) {
+                const int ij = i ^ J;
+                if (ij > i) {
+                    const unsigned long long a = sk[i], b = sk[ij];
+                    const bool asc = (i & K) == 0;
+                    if ((a > b) == asc) {
+                        sk[i] = b;
+                        sk[ij] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    // PT consecutive positions per thread: block heads, their chunk counts
+    int cnt[PT], tot = 0;
+#pragma unroll
+    for (int u = 0; u < PT; ++u) {
+        const int i = tid * PT + u;
+        cnt[u] = 0;
+        if (i >= n) continue;
+        const unsigned run = (unsigned)(sk[i] >> 32);
+        int lo = 0, hi = i;  // the run's first position
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if ((unsigned)(sk[mid] >> 32) < run) lo = mid + 1; else hi = mid;
+        }
+        if ((i - lo) % DR_GR == 0) cnt[u] = (rows[(unsigned)sk[i]].L + DR_CH - 1) / DR_CH;
+        tot += cnt[u];
+    }
+    const int inc = wave_incl_scan_dpp(tot);
+    if (lane == 63) red[wv] = inc;
+    __syncthreads();
+    int o = inc - tot, all = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        o += w < wv ? red[w] : 0;
+        all += red[w];
+    }
+#pragma unroll
+    for (int u = 0; u < PT; ++u) {
+        const int i = tid * PT + u;
+        if (i < n) ord[i] = (int)(unsigned)sk[i];
+        if (!cnt[u]) continue;
+        const unsigned run = (unsigned)(sk[i] >> 32);
+        int lo = 0, hi = i;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if ((unsigned)(sk[mid] >> 32) < run) lo = mid + 1; else hi = mid;
+        }
+        int e = i + 1, eh = n;  // past the run's last position
+        while (e < eh) {
+            const int mid = (e + eh) >> 1;
+            if ((unsigned)(sk[mid] >> 32) <= run) e = mid + 1; else eh = mid;
+        }
+        const int R = cnt[u], S = (e - lo + DR_GR - 1) / DR_GR, sb = (i - lo) / DR_GR;
+        const int gbase = o - sb * R;
+        const int nr = min(DR_GR, e - i);
+        for (int c = 0; c < R; ++c) chunks[gbase + c * S + sb] = make_int4(i, nr, c * DR_CH, 0);
+        o += R;
+    }
+    if (tid == 0) *nchunk = all;
+}
+
+// a chunk: DR_CH elements of one run, held in registers, written for each of
+// the chunk's rows (consecutive in ord, all of that run); a persistent grid
+// (the chunk count is known on the device only)
+constexpr int DR_FU = DR_CH / DR_NT;
 __global__ __launch_bounds__(DR_NT) void k_rows_dr_fill(RowsArgs g, const int *Crp, int *Ccol, double *Cval,
-                                                        const DrRow *rows, const DrEnt *ents,
-                                                        const int2 *chunks, const int *nchunk) {
-    __shared__ int sp[DR_SMAX];   // the chunk's S entries: insertion points
+                                                        const DrRow *rows, const DrEnt *ents, const int *ord,
+                                                        const int4 *chunks, const int *nchunk) {
+    __shared__ int sp[DR_SMAX];   // a row's S entries in the range: insertion points
     __shared__ int snd[DR_SMAX];  // inserted columns before each
     __shared__ unsigned char sdup[DR_SMAX];
     __shared__ double sval[DR_SMAX];
-    __shared__ int s_lo, s_hi;
+    __shared__ int r_lo[DR_GR], r_hi[DR_GR], r_nd0[DR_GR], r_h[DR_GR], r_out[DR_GR];
+    __shared__ double r_a[DR_GR];
     const int tid = threadIdx.x;
-    if ((int)blockIdx.x >= *nchunk) return;  // (workgroup-uniform)
-    const int2 ch = chunks[blockIdx.x];
-    const DrRow d = rows[ch.x];
-    const DrEnt *const E8 = ents + (long)ch.x * DR_SMAX;
-    const int i0 = ch.y, i1 = min(d.L, i0 + DR_CH);
-    const bool last = i1 == d.L;
-    // the S entries with insertion point in [i0, i1) (the last chunk: [i0, L])
-    if (tid < 2) {
-        const int key = tid == 0 ? i0 : (last ? d.L + 1 : i1);
-        int lo = 0, hi = d.nu;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (E8[mid].p < key) lo = mid + 1; else hi = mid;
-        }
-        if (tid == 0) s_lo = lo; else s_hi = lo;
-    }
-    __syncthreads();
-    const int elo = s_lo, ne = s_hi - s_lo;
-    const int nd0 = elo < d.nu ? E8[elo].nd : (d.nu ? E8[d.nu - 1].nd + !E8[d.nu - 1].dup : 0);
-    for (int t = tid; t < ne; t += DR_NT) {
-        const DrEnt e = E8[elo + t];
-        sp[t] = e.p;
-        snd[t] = e.nd;
-        sdup[t] = e.dup;
-        sval[t] = e.val;
-    }
-    __syncthreads();
-    int *const Ocol = Ccol + Crp[d.r];
-    double *const Oval = Cval + Crp[d.r];
-    // the run streamed: DR_U elements per thread with every load issued first,
-    // C written with streaming (nontemporal) stores -- this call never reads it
-    constexpr int DR_U = 4;
-    for (int ib = i0 + tid; ib < i1; ib += DR_U * DR_NT) {
-        int c[DR_U];
-        double v[DR_U];
+    const int nck = *nchunk;
+    for (int q = blockIdx.x; q < nck; q += gridDim.x) {  // (workgroup-uniform)
+        const int4 ch = chunks[q];  // {first position in ord, rows, range start, -}
+        const int nr = ch.y, i0 = ch.z;
+        const DrRow d0 = rows[ord[ch.x]];
+        const int i1 = min(d0.L, i0 + DR_CH);
+        const bool last = i1 == d0.L;
+        // the range, loads issued first (read once for the chunk's rows)
+        int c[DR_FU];
+        double v[DR_FU];
 #pragma unroll
-        for (int u = 0; u < DR_U; ++u) {
-            const int i = ib + u * DR_NT;
-            c[u] = i < i1 ? g.Bcol[d.bs + i] : 0;
-            v[u] = i < i1 ? g.Bval[d.bs + i] : 0.0;
+        for (int u = 0; u < DR_FU; ++u) {
+            const int i = i0 + u * DR_NT + tid;
+            c[u] = i < i1 ? g.Bcol[d0.bs + i] : 0;
+            v[u] = i < i1 ? g.Bval[d0.bs + i] : 0.0;
         }
-#pragma unroll
-        for (int u = 0; u < DR_U; ++u) {
-            const int i = ib + u * DR_NT;
-            if (i >= i1) break;
-            double x = d.aL * v[u];
-            // entries with p <= i: the count t; the inserted ones before i = nd of entry t
-            int lo = 0, hi = ne;
+        // per row, two lanes: its S entries with insertion point in [i0, i1)
+        // (the last range: [i0, L]), the inserted columns before the range
+        if (tid < 2 * nr) {
+            const int j = tid >> 1, hi_side = tid & 1;
+            const int h = ord[ch.x + j];
+            const DrRow d = rows[h];
+            const DrEnt *const E8 = ents + (long)h * DR_SMAX;
+            const int key = hi_side ? (last ? d.L + 1 : i1) : i0;
+            int lo = 0, hi = d.nu;
             while (lo < hi) {
                 const int mid = (lo + hi) >> 1;
-                if (sp[mid] <= i) lo = mid + 1; else hi = mid;
+                if (E8[mid].p < key) lo = mid + 1; else hi = mid;
             }
-            const int ins = lo < ne ? snd[lo] : (ne ? snd[ne - 1] + !sdup[ne - 1] : nd0);
-            if (lo > 0 && sp[lo - 1] == i && sdup[lo - 1]) x += sval[lo - 1];
-            __builtin_nontemporal_store(c[u], Ocol + i + ins);
-            __builtin_nontemporal_store(x, Oval + i + ins);
+            if (hi_side) {
+                r_hi[j] = lo;
+            } else {
+                r_lo[j] = lo;
+                r_h[j] = h;
+                r_out[j] = Crp[d.r];
+                r_a[j] = d.aL;
+                r_nd0[j] = lo < d.nu ? E8[lo].nd : (d.nu ? E8[d.nu - 1].nd + !E8[d.nu - 1].dup : 0);
+            }
         }
+        __syncthreads();
+        for (int j = 0; j < nr; ++j) {
+            const int elo = r_lo[j], ne = r_hi[j] - elo, nd0 = r_nd0[j];
+            int *const Ocol = Ccol + r_out[j];
+            double *const Oval = Cval + r_out[j];
+            const double aL = r_a[j];
+            // (plain stores: nontemporal ones 0.8 ms slower on mawi's 19 GB of C, r5r)
+            if (ne == 0) {  // (most rows' ranges: the run shifted by the inserted columns before it)
+#pragma unroll
+                for (int u = 0; u < DR_FU; ++u) {
+                    const int i = i0 + u * DR_NT + tid;
+                    if (i < i1) {
+                        Ocol[i + nd0] = c[u];
+                        Oval[i + nd0] = aL * v[u];
+                    }
+                }
+                continue;
+            }
+            const DrEnt *const E8 = ents + (long)r_h[j] * DR_SMAX;
+            for (int t = tid; t < ne; t += DR_NT) {
+                const DrEnt e = E8[elo + t];
+                sp[t] = e.p;
+                snd[t] = e.nd;
+                sdup[t] = e.dup;
+                sval[t] = e.val;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < DR_FU; ++u) {
+                const int i = i0 + u * DR_NT + tid;
+                if (i >= i1) break;
+                double x = aL * v[u];
+                // entries with p <= i: the count t; the inserted ones before i = nd of entry t
+                int lo = 0, hi = ne;
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (sp[mid] <= i) lo = mid + 1; else hi = mid;
+                }
+                const int ins = lo < ne ? snd[lo] : snd[ne - 1] + !sdup[ne - 1];
+                if (lo > 0 && sp[lo - 1] == i && sdup[lo - 1]) x += sval[lo - 1];
+                Ocol[i + ins] = c[u];
+                Oval[i + ins] = x;
+            }
+            for (int t = tid; t < ne; t += DR_NT)
+                if (!sdup[t]) {
+                    const DrEnt e = E8[elo + t];
+                    Ocol[e.p + e.nd] = e.col;
+                    Oval[e.p + e.nd] = e.val;
+                }
+            __syncthreads();  // (the LDS tables: the next row's)
+        }
+        __syncthreads();  // (the row tables: the next chunk's)
     }
-    for (int t = tid; t < ne; t += DR_NT)
-        if (!sdup[t]) {
-            const DrEnt e = E8[elo + t];
-            Ocol[e.p + e.nd] = e.col;
-            Oval[e.p + e.nd] = e.val;
-        }
 }
 
 // chunks of CP_CH output positions (a workgroup each, consecutive lanes on
@@ -2352,7 +2473,8 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
     double *Ox = nullptr;
     DrRow *drows = nullptr;
     DrEnt *dents = nullptr;
-    int2 *dchunks = nullptr;
+    int4 *dchunks = nullptr;
+    int *dord = nullptr;
     // windowed (W) rows' arrays: per class-H row, per unit, per chunk
     int *wnw = nullptr, *wnch = nullptr, *wlo = nullptr, *wwb = nullptr, *umap = nullptr;
     int *ucnt = nullptr, *ubo = nullptr, *ucount = nullptr, *uoff = nullptr, *Wc = nullptr;
@@ -2455,8 +2577,16 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
             TSG_TRY(cx.get(&drows, (size_t)ndr));
             TSG_TRY(cx.get(&dents, (size_t)ndr * DR_SMAX));
             TSG_TRY(cx.get(&dchunks, (size_t)nch));
-            k_rows_dr_prep<<<n7, DR_NT, 0, s>>>(g, soff, drows, dents, dchunks, p.cls + 20, p.cls + 21);
+            TSG_TRY(cx.get(&dord, (size_t)ndr));
+            // (TSG_DR_PER_ROW: the per-row chunks also below DR_GMAX rows -- a test of that path)
+            const bool grouped = ndr <= DR_GMAX && !getenv("TSG_DR_PER_ROW");
+            k_rows_dr_prep<<<n7, DR_NT, 0, s>>>(g, soff, drows, dents, dord, dchunks, p.cls + 20, p.cls + 21,
+                                                !grouped);
             TSG_HIP(hipGetLastError());
+            if (grouped) {
+                k_rows_dr_group<<<1, DR_NT, 0, s>>>(drows, p.cls + 21, dord, dchunks, p.cls + 20);
+                TSG_HIP(hipGetLastError());
+            }
             drnch = nch;
         }
     }
@@ -2538,8 +2668,9 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
             TSG_HIP(hipGetLastError());
         }
         if (drnch > 0) {
-            k_rows_dr_fill<<<(unsigned)drnch, DR_NT, 0, s>>>(g7, C.rowpointer, C.columnindex, C.value, drows, dents,
-                                                              dchunks, p.cls + 20);
+            // (persistent: the grouped chunk count, under drnch, is known on the device only)
+            k_rows_dr_fill<<<(unsigned)std::min<long long>(drnch, 1024), DR_NT, 0, s>>>(
+                g7, C.rowpointer, C.columnindex, C.value, drows, dents, dord, dchunks, p.cls + 20);
             TSG_HIP(hipGetLastError());
         }
         return TSG_OK;
@@ -2604,6 +2735,7 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
     cx.put(drows);
     cx.put(dents);
     cx.put(dchunks);
+    cx.put(dord);
     if (st) {
         st->nnzC = C.nnz;
         st->tile_products = products;

@@ -286,6 +286,45 @@ def test_rows_hub_rows_windowed_and_dominant_run():
     _check(A, B, real=True, seed=43)
 
 
+@pytest.mark.parametrize("per_row", [False, True])
+def test_rows_dominant_run_rows_grouped_by_run(monkeypatch, per_row):
+    """Many dominant-run rows sharing a run (the mawi pattern: every hub
+    neighbour's C row holds the hub's whole B row): k_rows_dr_group sorts them
+    by run and cuts each run's rows into blocks of DR_GR = 32 whose chunks of
+    DR_CH = 16,384 elements read the run once for the block.  71 + 32 rows on
+    two runs of 120,000 / 70,001 columns (blocks of 32, 32, 7 and 32), their
+    inserted columns before, inside (some L holds: a sum) and past the run, in
+    one range or many; with TSG_DR_PER_ROW the per-row chunks instead."""
+    if per_row:
+        monkeypatch.setenv("TSG_DR_PER_ROW", "1")
+    rng = np.random.default_rng(61)
+    n = 1_500_000
+    nb = 4000
+    Brows = [np.sort(rng.choice(n, size=int(rng.integers(1, 40)), replace=False)) for _ in range(nb - 4)]
+    h1 = np.sort(rng.choice(np.arange(1000, n - 1000), size=120_000, replace=False))
+    h2 = np.sort(rng.choice(n, size=70_001, replace=False))
+    Brows += [h1, h2, np.array([0, 1, 2]), np.array([n - 3, n - 2, n - 1])]  # (before / past h1)
+    B = _csr(nb, n, Brows)
+    arows = []
+    for i in range(70):
+        extra = rng.choice(nb - 4, size=int(rng.integers(0, 6)), replace=False)
+        if i % 7 == 0:
+            extra = np.concatenate([extra, [nb - 2, nb - 1]])
+        arows.append(np.sort(np.concatenate([extra, [nb - 4]])))
+    arows.append(np.sort(np.concatenate([rng.choice(nb - 4, size=120, replace=False), [nb - 4]])))  # many ranges
+    for i in range(32):
+        arows.append(np.sort(np.concatenate([rng.choice(nb - 4, size=int(rng.integers(0, 4)), replace=False),
+                                             [nb - 3]])))
+    arows += [np.sort(rng.choice(nb - 4, size=5, replace=False)) for _ in range(20)]  # ordinary rows
+    order = rng.permutation(len(arows))  # (the runs' rows interleaved)
+    arows = [arows[i] for i in order]
+    A = _csr(len(arows), nb, arows)
+    blen = np.diff(B[2].astype(np.int64))
+    P = np.array([blen[r].sum() for r in arows])
+    assert (P > 65536).sum() == 103
+    _check(A, B, real=True, seed=67)
+
+
 def test_rows_mawi_prefix_hub_rows():
     """The mawi stand-in at 1e-2 scale (hub degree 1e5): a row prefix holding
     hub-neighbour rows (each C row receives the hub's whole row) through the
