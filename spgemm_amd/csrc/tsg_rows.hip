@@ -51,6 +51,7 @@ constexpr int M1_CAP = 512, M1_RUNS = 124, M1_NT = 128;    // 10,208 B
 constexpr int M2_CAP = 1024, M2_RUNS = 248, M2_NT = 256;   // 20,400 B
 constexpr int M3_CAP = 2048, M3_RUNS = 504, M3_NT = 512;   // 40,912 B
 constexpr int M4_CAP = 4096, M4_RUNS = 512, M4_NT = 1024;  // 72 KB
+constexpr int W_CH = 32768;           // windowed rows: products per chunk (k_rows_wcount / wscatter)
 constexpr int NCLS = 8;               // S16, S64, M0..M4, H
 constexpr int DR_SMAX = 4096;         // hub rows: products outside the dominant run (the DR kernels)
 constexpr int DR_CH = 16384;          // DR fill: dominant-run elements per chunk
@@ -1030,43 +1031,64 @@ __device__ __forceinline__ void batch_runmap(const WalkTab &tb, int nb, int qb, 
 // products [q0, q1) of a batch whose run table tb holds (rows_batch; nb runs),
 // U per thread at a time: each product's column (and with VAL its a*b) to
 // f(column, value, valid), called by every lane (consecutive lanes hold
-// consecutive products; the invalid ones are a suffix of the wave).
-// With rmap (4 * RH_NT u16 + red: every thread must call), each step's runs come
-// from batch_runmap; else a binary search of the run table per product.
+// consecutive products; the invalid ones are a suffix of the wave).  Each
+// step's runs come from batch_runmap (rmap: two maps of 4 * RH_NT u16, red:
+// every thread must call).  Software-pipelined: step s + 1's map is built and
+// its B loads issued before f runs on step s, so the loads are in flight
+// through f (its LDS atomics and stores); the maps alternate, so a map is
+// rebuilt only after a barrier past its last reads.  (One step at a time --
+// map, loads, wait, f -- left the memory pipe idle through the map's barriers
+// and f: 856 us of k_rows_wscatter on the LiveJournal block, r5p.)
 template <bool VAL, class F>
 __device__ __forceinline__ void batch_walk(const RowsArgs &g, int nb, int q0, int q1, const WalkTab &tb, F &&f,
-                                           unsigned short *rmap = nullptr, int *red = nullptr) {
+                                           unsigned short *rmap, int *red) {  // (q1 - q0 <= W_CH)
     constexpr int U = 4;
     const int tid = threadIdx.x;
-    for (int qb = q0; qb < q1; qb += U * RH_NT) {
-        int b[U], len2[U], q[U], c[U];
-        double x[U];
+    if (q0 >= q1) return;  // (workgroup-uniform)
+    int c[U], cn[U];
+    double x[U], xn[U];
+    // step qb's products: its map into rm, then every load issued -- unconditional
+    // (invalid lanes read B's first entry) and raw, the a*b product taken at use:
+    // a load under a branch, or arithmetic on it here, makes hipcc wait for it here
+    auto fetch = [&](int qb, unsigned short *rm, int (&cc)[U], double (&xx)[U]) {
+        __syncthreads();  // (the last use of the map rm held, two steps back, done everywhere)
+        batch_runmap(tb, nb, qb, rm, red);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            q[u] = qb + u * RH_NT + tid;
-            b[u] = 0;
-            len2[u] = q[u] < q1 ? nb : 0;
-            c[u] = 0;
-            x[u] = 0.0;
+            const int q = qb + u * RH_NT + tid;
+            const int r = q < q1 ? rm[u * RH_NT + tid] : 0;
+            const int bs = tb.bs[r], pre = tb.pre[r];
+            const int pp = q < q1 ? bs + q - pre : 0;
+            cc[u] = g.Bcol[pp];
+            if (VAL) xx[u] = g.Bval[pp];
         }
-        if (rmap) {
-            batch_runmap(tb, nb, qb, rmap, red);
+    };
+    // the run of each product read again from its step's map at use (the map is
+    // rebuilt only by the fetch after this use): no register set of runs
+    auto use = [&](int qb, const unsigned short *rm, const int (&cc)[U], const double (&xx)[U]) {
 #pragma unroll
-            for (int u = 0; u < U; ++u) b[u] = q[u] < q1 ? rmap[q[u] - qb] + 1 : 1;
-        } else {
-            const bool ub[U] = {true, true, true, true};
-            search_ilp(tb.pre, b, len2, q, ub);  // b - 1 = the run holding product q
+        for (int u = 0; u < U; ++u) {  // (every lane: f may use wave operations)
+            const bool ok = qb + u * RH_NT + tid < q1;
+            f(cc[u], VAL && ok ? tb.av[rm[u * RH_NT + tid]] * xx[u] : 0.0, ok);
         }
+    };
+    constexpr int STEP = U * RH_NT;
+    // two register sets, fully unrolled over the at most W_CH / STEP steps of a
+    // chunk: straight-line code, where hipcc counts the waits exactly (in a loop,
+    // its register moves on the back edge waited for the set still loading); each
+    // fetch unconditional -- past q1 its lanes all read B's first entry -- so that
+    // no path leaves a set's loads the latest
+    unsigned short *const rm0 = rmap, *const rm1 = rmap + 4 * RH_NT;
+    fetch(q0, rm0, c, x);
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (q[u] < q1) {
-                const int pp = tb.bs[b[u] - 1] + q[u] - tb.pre[b[u] - 1];
-                c[u] = g.Bcol[pp];
-                if (VAL) x[u] = tb.av[b[u] - 1] * g.Bval[pp];
-            }
-#pragma unroll
-        for (int u = 0; u < U; ++u) f(c[u], x[u], q[u] < q1);  // (every lane: f may use wave operations)
-        if (rmap) __syncthreads();  // (the map read before the next step rebuilds it)
+    for (int st = 0; st < W_CH / STEP; st += 2) {  // (workgroup-uniform)
+        const int qb = q0 + st * STEP;
+        if (qb >= q1) break;
+        fetch(qb + STEP, rm1, cn, xn);
+        use(qb, rm0, c, x);
+        if (qb + STEP >= q1) break;
+        fetch(qb + 2 * STEP, rm0, c, x);
+        use(qb + STEP, rm1, cn, xn);
     }
 }
 
@@ -1379,7 +1401,6 @@ __device__ __forceinline__ long long row_longest_run(const long long *E, int a0,
 // product, and a hub row's work is spread over as many workgroups as it has
 // chunks and units.
 constexpr int W_NT = RH_NT;        // (the run-batch tables are RH_NT wide)
-constexpr int W_CH = 32768;        // products per chunk
 constexpr int W_UNIT = 8192;       // products per unit, the target of wb
 constexpr int W_MAXW = 8192;       // windows per row
 constexpr int W_WBMIN = 8, W_WBMAX = 18;
@@ -1388,6 +1409,7 @@ constexpr int W_BLK = 512;                    // words per rank block
 constexpr int W_NBLK = W_WORDS / W_BLK;
 constexpr int W_VCAP = 4096;                  // a unit's values per LDS pass
 constexpr int W_RPT = 8;                      // a unit's products per thread held in registers
+constexpr int WU_NT = 1024;                   // the unit kernel's workgroup (W_RPT * WU_NT >= W_UNIT)
 constexpr int W_SPANK = 8192;                 // plan: rows past so many runs span all of B's columns
 
 __device__ __forceinline__ int ceil_log2_ll(long long v) {
@@ -1573,7 +1595,7 @@ __global__ __launch_bounds__(W_NT) void k_rows_wcount(RowsArgs g, const int4 *ch
                                                      int *cbo) {
     __shared__ int hist[W_MAXW];
     __shared__ WalkTab wt;
-    __shared__ __align__(16) unsigned short rmap[4 * RH_NT];
+    __shared__ __align__(16) unsigned short rmap[8 * RH_NT];  // (two maps: batch_walk)
     __shared__ int red[RH_NT / 64];
     const int4 ch = chunks[blockIdx.x];
     const int u0 = ubase[ch.x], nw = ubase[ch.x + 1] - u0;
@@ -1648,11 +1670,11 @@ __global__ __launch_bounds__(W_NT) void k_rows_wscan(RowsArgs g, const int *ubas
 // Each product is stored at its window's LDS cursor.  (Binning each sub-batch
 // by window in LDS first, then writing it out in window order, measured no
 // faster on the LiveJournal block: 2.744 vs 2.746 ms; removed.)
-__global__ __launch_bounds__(W_NT) void k_rows_wscatter(RowsArgs g, const int4 *chunks, const long long *cmoff,
+__global__ __launch_bounds__(W_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_rows_wscatter(RowsArgs g, const int4 *chunks, const long long *cmoff,
                                                        const int *wlo, const int *wwb, const int *ubase,
                                                        const int *ubo, const int *cbo) {
     // cursors of up to W_MAXW windows, the run map above them
-    __shared__ __align__(16) unsigned char lds[W_MAXW * 4 + 4 * RH_NT * 2];
+    __shared__ __align__(16) unsigned char lds[W_MAXW * 4 + 8 * RH_NT * 2];  // (two run maps: batch_walk)
     __shared__ WalkTab wt;
     __shared__ int red[W_NT / 64];
     int *const cur = reinterpret_cast<int *>(lds);  // row-relative slots (windows not reached: unused)
@@ -1703,9 +1725,9 @@ __device__ __forceinline__ int w_rank(const u64 *bm, const u16 *g4, const int *b
 // a workgroup per unit u (row i = umap[u], window u - ubase[i]): its bucket
 // (ucnt[u] products at E[a0] + ubo[u]) -> its nonzeros, column-sorted, at
 // Ocol/Oval + wpre[i] + ubo[u]; ucount[u] = their number
-__global__ __launch_bounds__(W_NT) void k_rows_wunit(RowsArgs g, const WUnit *urec, int *ucount, int *Ocol,
+__global__ __launch_bounds__(WU_NT) void k_rows_wunit(RowsArgs g, const WUnit *urec, int *ucount, int *Ocol,
                                                     double *Oval) {
-    constexpr int NW = W_NT / 64;
+    constexpr int NW = WU_NT / 64;
     __shared__ __align__(16) u64 bm[W_WORDS];
     __shared__ u16 g4[W_WORDS / 4];
     __shared__ int blk[W_NBLK];
@@ -1724,13 +1746,13 @@ __global__ __launch_bounds__(W_NT) void k_rows_wunit(RowsArgs g, const WUnit *ur
     const long long wlo0 = R.wlo0;
     const long long s0 = R.s0;
     const int nwd = 1 << (wb - 6);
-    for (int w = tid; w < nwd; w += W_NT) bm[w] = 0ull;
-    // the first W_RPT * W_NT products in registers (the rest read again below)
+    for (int w = tid; w < nwd; w += WU_NT) bm[w] = 0ull;
+    // the first W_RPT * WU_NT products in registers (the rest read again below)
     int cc[W_RPT];
     double xx[W_RPT];
 #pragma unroll
     for (int t = 0; t < W_RPT; ++t) {
-        const int q = t * W_NT + tid;
+        const int q = t * WU_NT + tid;
         cc[t] = q < n ? (int)(g.Scol[s0 + q] - wlo0) : -1;
         xx[t] = q < n ? g.Sval[s0 + q] : 0.0;
     }
@@ -1739,7 +1761,7 @@ __global__ __launch_bounds__(W_NT) void k_rows_wunit(RowsArgs g, const WUnit *ur
 #pragma unroll
     for (int t = 0; t < W_RPT; ++t)
         if (cc[t] >= 0) atomicOr(&bm[cc[t] >> 6], 1ull << (cc[t] & 63));
-    for (int q = W_RPT * W_NT + tid; q < n; q += W_NT) {
+    for (int q = W_RPT * WU_NT + tid; q < n; q += WU_NT) {
         const int c = (int)(g.Scol[s0 + q] - wlo0);
         atomicOr(&bm[c >> 6], 1ull << (c & 63));
     }
@@ -1774,8 +1796,8 @@ __global__ __launch_bounds__(W_NT) void k_rows_wunit(RowsArgs g, const WUnit *ur
 #pragma unroll
     for (int t = 0; t < W_RPT; ++t) rk[t] = cc[t] >= 0 ? w_rank(bm, g4, blk, cc[t]) : 0;
     const long long o0 = R.o0;
-    static_assert(2 * W_WORDS >= W_RPT * W_NT, "the bitmap's LDS holds a column per rank (wn <= n)");
-    if (n <= W_RPT * W_NT) {  // (workgroup-uniform) every product in registers
+    static_assert(2 * W_WORDS >= W_RPT * WU_NT, "the bitmap's LDS holds a column per rank (wn <= n)");
+    if (n <= W_RPT * WU_NT) {  // (workgroup-uniform) every product in registers
         // the bitmap is done with once the ranks are: its LDS takes each rank's
         // column (a column's products store the same one), the values are
         // summed at their ranks W_VCAP at a time, and both go out coalesced
@@ -1789,14 +1811,14 @@ __global__ __launch_bounds__(W_NT) void k_rows_wunit(RowsArgs g, const WUnit *ur
         RP(3);
         for (int r0 = 0; r0 < wn; r0 += W_VCAP) {  // (workgroup-uniform)
             const int r1 = min(wn, r0 + W_VCAP);
-            for (int j = tid; j < r1 - r0; j += W_NT) vals[j] = 0.0;
+            for (int j = tid; j < r1 - r0; j += WU_NT) vals[j] = 0.0;
             __syncthreads();
 #pragma unroll
             for (int t = 0; t < W_RPT; ++t)
                 if (cc[t] >= 0 && (unsigned)(rk[t] - r0) < (unsigned)W_VCAP) atomicAdd(&vals[rk[t] - r0], xx[t]);
             __syncthreads();
             RP(4);
-            for (int j = tid; j < r1 - r0; j += W_NT) {
+            for (int j = tid; j < r1 - r0; j += WU_NT) {
                 Ocol[o0 + r0 + j] = (int)(wlo0 + cl[r0 + j]);
                 Oval[o0 + r0 + j] = vals[j];
             }
@@ -1809,19 +1831,19 @@ __global__ __launch_bounds__(W_NT) void k_rows_wunit(RowsArgs g, const WUnit *ur
     }
     for (int r0 = 0; r0 < wn; r0 += W_VCAP) {  // (workgroup-uniform; one pass unless wn > W_VCAP)
         const int r1 = min(wn, r0 + W_VCAP);
-        for (int j = tid; j < r1 - r0; j += W_NT) vals[j] = 0.0;
+        for (int j = tid; j < r1 - r0; j += WU_NT) vals[j] = 0.0;
         __syncthreads();
 #pragma unroll
         for (int t = 0; t < W_RPT; ++t)
             if (cc[t] >= 0 && (unsigned)(rk[t] - r0) < (unsigned)W_VCAP) atomicAdd(&vals[rk[t] - r0], xx[t]);
-        for (int q = W_RPT * W_NT + tid; q < n; q += W_NT) {
+        for (int q = W_RPT * WU_NT + tid; q < n; q += WU_NT) {
             const int c = (int)(g.Scol[s0 + q] - wlo0);
             const int rq = w_rank(bm, g4, blk, c) - r0;
             if ((unsigned)rq < (unsigned)W_VCAP) atomicAdd(&vals[rq], g.Sval[s0 + q]);
         }
         __syncthreads();
         // emit: a thread per bitmap word, its columns at their ranks
-        for (int w = tid; w < nwd; w += W_NT) {
+        for (int w = tid; w < nwd; w += WU_NT) {
             u64 word = bm[w];
             if (!word) continue;
             int r = w_rank(bm, g4, blk, w * 64);
@@ -2558,7 +2580,7 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
             TSG_HIP(hipGetLastError());
             k_rows_wscatter<<<nc, W_NT, 0, s>>>(g, wchunks, cmoff, wlo, wwb, ubase, ubo, cbo);
             TSG_HIP(hipGetLastError());
-            k_rows_wunit<<<nu, W_NT, 0, s>>>(g, urec, ucount, Wc, Wv);
+            k_rows_wunit<<<nu, WU_NT, 0, s>>>(g, urec, ucount, Wc, Wv);
             TSG_HIP(hipGetLastError());
             k_rows_wscan<<<n7, W_NT, 0, s>>>(g, ubase, ucount, uoff, g.rnnz);
             TSG_HIP(hipGetLastError());
