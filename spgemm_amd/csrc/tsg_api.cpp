@@ -935,7 +935,14 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
     tsg_stats st{};
     tsg_dev_tiles tA, tB, tC;
     auto h0 = std::chrono::steady_clock::now();
-    TSG_HIP(hipEventRecord(cx.ev[8], s));
+    // the stage events (ev 8, 9, 0, 1, 3) only on request: each marker on the
+    // stream cost ~2-3 us of GPU time (cant 0.707 -> 0.692 ms without them, r5e1);
+    // the kernel bracket (ev 4, 5) and the end (ev 10) always
+    {
+        const char *se = getenv("TSG_STAGE_EVENTS");
+        cx.stage_ev = se && se[0] == '1';
+    }
+    if (cx.stage_ev) TSG_HIP(hipEventRecord(cx.ev[8], s));
     // Element streaming (steps 2/3 straight from the CSR operands) needs B's rows
     // column-sorted.  Sparse tiles (few nonzeros per A tile, e.g. web graphs) then
     // need only the tile STRUCTURE of A and B; denser tiles keep the full
@@ -981,7 +988,7 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
             band = false;
         }
         long long path_id = -1;
-        TSG_HIP(hipEventRecord(cx.ev[9], s));
+        if (cx.stage_ev) TSG_HIP(hipEventRecord(cx.ev[9], s));
         if (band) {
             const int rc = dev_spgemm_band(cx, *A, *B, bw, *C, &st, s, cx.ev);
             cx.put(bw.win);
@@ -992,7 +999,7 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
         } else {
             // the row-merge setup and the sortedness flag: one host round trip
             // decides rows / tiles
-            TSG_HIP(hipEventRecord(cx.ev[0], s));
+            if (cx.stage_ev) TSG_HIP(hipEventRecord(cx.ev[0], s));
             RowsPlan plan;
             TSG_TRY(dev_rows_setup_async(cx, *A, *B, plan, s, shares.part ? &shares : nullptr));
             TSG_TRY(stream_wait(s));
@@ -1012,21 +1019,24 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
             st.numtileA = -1;
             st.numtileB = -1;
             st.path = path_id;
-            st.t_csr2tile_ms = ev_ms(cx.ev[8], cx.ev[9]);   // sortedness (+ band: window statistics; no csr2tile)
-            st.t_step1_ms = ev_ms(cx.ev[0], cx.ev[1]);      // entry table, classes / row windows / units
-            st.t_step2_ms = 0.0;                            // (structure and values together)
-            st.t_step3_ms = ev_ms(cx.ev[1], cx.ev[3]);      // the row / unit kernels, row pointers, compaction
+            // (stage times 0 without the stage events: unmeasured, not free)
+            const bool se = cx.stage_ev;
+            st.t_csr2tile_ms = se ? ev_ms(cx.ev[8], cx.ev[9]) : 0.0;  // sortedness (+ band: window statistics)
+            st.t_step1_ms = se ? ev_ms(cx.ev[0], cx.ev[1]) : 0.0;     // entry table, classes / row windows / units
+            st.t_step2_ms = 0.0;                                      // (structure and values together)
+            st.t_step3_ms = se ? ev_ms(cx.ev[1], cx.ev[3]) : 0.0;     // the row / unit kernels, scan, compaction
             st.t_step3_kernel_ms = ev_ms(cx.ev[4], cx.ev[5]);
-            st.t_tile2csr_ms = 0.0;                         // (fused)
-            st.t_kern_ms = ev_ms(cx.ev[0], cx.ev[3]);
+            st.t_tile2csr_ms = 0.0;                                   // (fused)
+            st.t_kern_ms = se ? ev_ms(cx.ev[0], cx.ev[3]) : 0.0;
             st.t_e2e_ms = std::chrono::duration<double, std::milli>(h1 - h0).count();
-            st.t_malloc_ms = st.t_e2e_ms - ev_ms(cx.ev[8], cx.ev[10]);
+            st.t_malloc_ms = se ? st.t_e2e_ms - ev_ms(cx.ev[8], cx.ev[10]) : 0.0;
             if (st.t_malloc_ms < 0) st.t_malloc_ms = 0;
             if (stats) *stats = st;
             return TSG_OK;
         }
     }
     TSG_TRY(dev_rows_sorted_finish(cx, shares, s));  // (forced tiles: the flag is still owed)
+    if (!cx.stage_ev) TSG_HIP(hipEventRecord(cx.ev[8], s));  // (the staged pipeline: its stage times always)
     const char *md = getenv("TSG_STEP2_MODE");
     const int forced = !md ? -1 : !strcmp(md, "elem") ? 1 : !strcmp(md, "tile") ? 0 : -1;
     const double skip = forced == 1 ? 1e300 : forced == 0 ? 0.0 : kStep2ElemMaxTileDensity;

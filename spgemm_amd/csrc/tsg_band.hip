@@ -419,7 +419,7 @@ int dev_spgemm_band(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, Ban
         else TSG_TRY(rc);
     }
     const long long *soff = fixed ? nullptr : bw.width;
-    if (ev) TSG_HIP(hipEventRecord(ev[1], s));
+    if (ev && cx.stage_ev) TSG_HIP(hipEventRecord(ev[1], s));
     if (ev) TSG_HIP(hipEventRecord(ev[4], s));
     if (m > 0) {
         BandArgs g{A.rowpointer, A.value, ebnd, bw.win, soff, B.columnindex, B.value, C.rowpointer, Scol, Sval, m};
@@ -460,7 +460,7 @@ int dev_spgemm_band(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, Ban
         k_band_compact<<<grid_for(m, WAVES, 16384), WG, 0, s>>>(m, soff, C.rowpointer, Scol, Sval, C.columnindex,
                                                                C.value);
     TSG_HIP(hipGetLastError());
-    if (ev) TSG_HIP(hipEventRecord(ev[3], s));
+    if (ev && cx.stage_ev) TSG_HIP(hipEventRecord(ev[3], s));
     TSG_TRY(stream_wait(s));
     if (fused) nnz = *hnnz;
     if (nnz > 0x7fffffffLL) return TSG_ERR_OVERFLOW;

@@ -61,6 +61,7 @@ struct Context {
     int *dpinned = nullptr;        // device views of the pinned scratch (kernels report
     long long *dpinned64 = nullptr; //   small results there by system-scope stores)
     hipEvent_t ev[16];
+    bool stage_ev = false;         // the stage events too (TSG_STAGE_EVENTS=1), not just the kernel bracket
     bool ev_ready = false;
     std::vector<void *> owned;    // outputs handed to the caller (released on reset)
     int init(int dev);

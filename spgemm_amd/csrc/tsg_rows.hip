@@ -1829,6 +1829,12 @@ __global__ __launch_bounds__(WU_NT) void k_rows_wunit(RowsArgs g, const WUnit *u
         RP_DONE(0);
         return;
     }
+#ifdef TSG_ROWS_PROF
+    for (int k = 0; k < 3; ++k) {  // (the large units' phases 0..2 as 6..8)
+        rp_acc[6 + k] += rp_acc[k];
+        rp_acc[k] = 0;
+    }
+#endif
     for (int r0 = 0; r0 < wn; r0 += W_VCAP) {  // (workgroup-uniform; one pass unless wn > W_VCAP)
         const int r1 = min(wn, r0 + W_VCAP);
         for (int j = tid; j < r1 - r0; j += WU_NT) vals[j] = 0.0;
@@ -1842,6 +1848,7 @@ __global__ __launch_bounds__(WU_NT) void k_rows_wunit(RowsArgs g, const WUnit *u
             if ((unsigned)rq < (unsigned)W_VCAP) atomicAdd(&vals[rq], g.Sval[s0 + q]);
         }
         __syncthreads();
+        RP(9);
         // emit: a thread per bitmap word, its columns at their ranks
         for (int w = tid; w < nwd; w += WU_NT) {
             u64 word = bm[w];
@@ -1859,8 +1866,11 @@ __global__ __launch_bounds__(WU_NT) void k_rows_wunit(RowsArgs g, const WUnit *u
             }
         }
         __syncthreads();  // (the pass's values read before the next pass zeroes them)
+        RP(10);
     }
     if (tid == 0) ucount[u] = wn;
+    RP(11);
+    RP_DONE(0);
 }
 
 // each unit's nonzeros from the output area to C at the row's pointer plus the
@@ -2457,7 +2467,7 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
     double *Sval = nullptr;
     TSG_TRY(cx.get(&Scol, (size_t)products + 1));
     TSG_TRY(cx.get(&Sval, (size_t)products + 1));
-    if (ev) TSG_HIP(hipEventRecord(ev[1], s));
+    if (ev && cx.stage_ev) TSG_HIP(hipEventRecord(ev[1], s));
     if (ev) TSG_HIP(hipEventRecord(ev[4], s));
 #ifdef TSG_ROWS_PROF
     unsigned long long *dprof = nullptr;
@@ -2738,7 +2748,7 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
     }
     if (small && !fused_scan)
         TSG_HIP(hipMemcpyAsync(cx.pinned64 + 15, C.rowpointer + m, sizeof(int), hipMemcpyDeviceToHost, s));
-    if (ev) TSG_HIP(hipEventRecord(ev[3], s));
+    if (ev && cx.stage_ev) TSG_HIP(hipEventRecord(ev[3], s));
     TSG_TRY(stream_wait(s));
     if (small) nnz = *hnnz;
     C.nnz = (int)nnz;
