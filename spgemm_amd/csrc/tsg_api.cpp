@@ -953,8 +953,17 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
     // (its last step -- the shares' sum into the flag -- rides on the row-merge
     // setup's binning kernel, or runs before the first read-back of another route)
     SortedShares shares;
+    // (A referencing at most 1/64 of B's rows -- the mawi prefix: 6,828 entries
+    // against 226 M rows -- only the B rows A references are checked, 0.88 ->
+    // 0.12 ms there; a LiveJournal hub block's 125 K entries reach hub rows
+    // whose entries outweigh the whole-B sweep: 0.19 vs 0.10 ms, so it keeps
+    // the sweep.  The staged tile pipeline, which reads whole B tile rows,
+    // re-checks all of B below.)
+    const bool ref_check = b_sorted != 1 && (long long)A->nnz * 64 < (long long)B->m;
     if (b_sorted == 1)
         cx.pinned[1] = 0;  // (known: no check, no shares for the binning kernel to sum)
+    else if (ref_check)
+        TSG_TRY(dev_rows_sorted_shares_ref(cx, *A, *B, cx.pinned + 1, &shares, s));
     else
         TSG_TRY(dev_rows_sorted_shares(cx, *B, cx.pinned + 1, &shares, s));
     // Routing, B's rows column-sorted:
@@ -1036,6 +1045,10 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
         }
     }
     TSG_TRY(dev_rows_sorted_finish(cx, shares, s));  // (forced tiles: the flag is still owed)
+    if (ref_check) {  // (the referenced rows' flag: the tile pipeline needs all of B's)
+        bool all_sorted = false;
+        TSG_TRY(dev_rows_sorted(cx, *B, &all_sorted, s));
+    }
     if (!cx.stage_ev) TSG_HIP(hipEventRecord(cx.ev[8], s));  // (the staged pipeline: its stage times always)
     const char *md = getenv("TSG_STEP2_MODE");
     const int forced = !md ? -1 : !strcmp(md, "elem") ? 1 : !strcmp(md, "tile") ? 0 : -1;

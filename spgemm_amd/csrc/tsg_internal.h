@@ -131,6 +131,9 @@ struct SortedShares {
 };
 int dev_rows_sorted_shares(Context &cx, const tsg_dev_csr &M, int *host_flag, SortedShares *sh, hipStream_t s);
 int dev_rows_sorted_finish(Context &cx, SortedShares &sh, hipStream_t s);
+// the same for the B rows A references only (row-merge / band paths)
+int dev_rows_sorted_shares_ref(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, int *host_flag,
+                               SortedShares *sh, hipStream_t s);
 int dev_tile2csr(Context &cx, const tsg_dev_tiles &C, tsg_dev_csr &out, hipStream_t s);
 // banded path (tsg_band.hip): every C row's reachable columns within one
 // window of <= 2,048 columns, the windows holding at least as many products as

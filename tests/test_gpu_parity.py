@@ -475,3 +475,47 @@ def test_tiled_csr_disagreeing_with_tiles_takes_the_payload_route(which):
         np.testing.assert_array_equal(ct[k], want[k], err_msg=f"C {k} ({which}'s CSR disagrees)")
     T.tile2csr(Cm, 16, 16)
     assert_csr_equal(Cm.csr(), O.gustavson(oA, oB).csr())
+
+
+@pytest.mark.parametrize("where", ["unreferenced", "referenced", "long_row_tail", "none"])
+def test_row_block_checks_only_referenced_b_rows(monkeypatch, where):
+    """A row block far smaller than B (nnz(A) * 64 < B's rows: the mawi prefix)
+    checks the column order of the B rows A references only
+    (dev_rows_sorted_shares_ref).  An out-of-order B row that A never reads
+    leaves the row-merge path in place; one that A reads -- a short row, or the
+    tail of a row of 10,000 entries (three queued chunks of 4,096 pairs) --
+    sends the product to the staged tile pipeline, which re-checks all of B.
+    Each C against the oracle."""
+    monkeypatch.delenv("TSG_PATH", raising=False)
+    rng = np.random.default_rng(71)
+    nb, n = 40000, 30000
+    brows = [np.sort(rng.choice(n, size=int(rng.integers(1, 12)), replace=False)) for _ in range(nb)]
+    brows[7] = np.sort(rng.choice(n, size=10000, replace=False))  # a long row
+    bad = {"unreferenced": 12345, "referenced": 3, "long_row_tail": 7, "none": None}[where]
+    if bad is not None:
+        r = brows[bad]
+        if len(r) < 2:
+            r = np.array([5, 9])
+        r = r.copy()
+        k = len(r) - 2 if where == "long_row_tail" else 0
+        r[k], r[k + 1] = r[k + 1], r[k]  # two neighbours swapped
+        brows[bad] = r
+    lens = [len(r) for r in brows]
+    brp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    bci = np.concatenate(brows).astype(np.int32)
+    bvv = rng.uniform(-1, 1, len(bci))
+    arows = [np.array([3, 7, 100 + i]) for i in range(40)]  # rows 3, 7 and 100..139 of B
+    arp = np.concatenate([[0], np.cumsum([len(r) for r in arows])]).astype(np.int32)
+    aci = np.concatenate(arows).astype(np.int32)
+    avv = rng.uniform(-1, 1, len(aci))
+    assert len(aci) * 64 < nb
+    A = T.Matrix.from_csr(40, nb, arp, aci, avv)
+    B = T.Matrix.from_csr(nb, n, brp, bci, bvv)
+    Cm, st = T.spgemm(A, B)
+    ref = O.gustavson(O.OMat.from_csr(40, nb, arp, aci, avv), O.OMat.from_csr(nb, n, brp, bci, bvv)).csr()
+    got = Cm.csr()
+    np.testing.assert_array_equal(got[2], ref[2])
+    np.testing.assert_array_equal(got[3], ref[3])
+    np.testing.assert_allclose(got[4], ref[4], rtol=1e-10, atol=1e-12)
+    expect = T.PATH_TILES if where in ("referenced", "long_row_tail") else T.PATH_ROWS
+    assert st["path"] == expect
