@@ -269,10 +269,10 @@ __device__ __forceinline__ int row_class(long long P, int k) {
 __global__ __launch_bounds__(WG) void k_rows_bin(const int *rpA, int m, const long long *E, const long long *Etot,
                                                  int *rnnz, int4 *lists, int *cls, long long *soff,
                                                  unsigned long long *hst, const int *spart, int snb, int *sflag) {
-    __shared__ int wc[NCLS][WAVES];
     __shared__ int gb[NCLS];
     __shared__ long long red64[WAVES];
-    __shared__ signed char rc[BIN_ROWS];  // each row's class, for the second sweep
+    constexpr int RPT = BIN_ROWS / WG;  // rows per thread: every load of a sweep issued together
+    __shared__ int wcu[RPT][NCLS][WAVES];  // per (row slot, class, wave): count, then exclusive prefix
     const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
     const int r0 = blockIdx.x * BIN_ROWS, r1 = min(m, r0 + BIN_ROWS);
     if (blockIdx.x == 0 && tid == 0) {
@@ -286,9 +286,8 @@ __global__ __launch_bounds__(WG) void k_rows_bin(const int *rpA, int m, const lo
         v = block_sum(v, red64);
         if (tid == 0 && v != 0) __hip_atomic_store(sflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    int n[NCLS] = {};
     long long hp = 0, pmax = 0, drp = 0, hubr = 0, hbig = 0;
-    constexpr int RPT = BIN_ROWS / WG;  // rows per thread: every load of a sweep issued together
+    int cu[RPT];  // each of the thread's rows' class (-1: none)
     int ra0[RPT], ra1[RPT];
 #pragma unroll
     for (int u = 0; u < RPT; ++u) {
@@ -305,14 +304,13 @@ __global__ __launch_bounds__(WG) void k_rows_bin(const int *rpA, int m, const lo
 #pragma unroll
     for (int u = 0; u < RPT; ++u) {
         const int r = r0 + u * WG + tid;
+        cu[u] = -1;
         if (r >= r1) continue;
         const long long P = e1[u] - e0[u];
         const int c = row_class(P, ra1[u] - ra0[u]);
         soff[r] = e0[u];  // the row's staging offset
-        rc[r - r0] = (signed char)c;
+        cu[u] = c;
         if (c < 0) rnnz[r] = 0;
-#pragma unroll
-        for (int t = 0; t < NCLS; ++t) n[t] += c == t;
         hp += c == NCLS - 1 ? P : 0;
         hbig += c == NCLS - 1 && P <= kRowsHubProducts && P > OW_CH ? P - OW_CH : 0;
         pmax = max(pmax, P);
@@ -337,46 +335,40 @@ __global__ __launch_bounds__(WG) void k_rows_bin(const int *rpA, int m, const lo
         if (hubr) atomicAdd(&hst[4], (unsigned long long)hubr);
         if (hbig) atomicAdd(&hst[8], (unsigned long long)hbig);
     }
+    // the list slots with two barriers (one sweep per row slot u had cost two
+    // each: 16 on a workgroup of 8 row slots): per (u, class) each wave's count
+    // by a ballot; eight threads turn them into exclusive prefixes in (u, wave)
+    // order and reserve each class's run of slots with one atomic
+    u64 mine[RPT];  // the ballot of this lane's class, per row slot
 #pragma unroll
-    for (int t = 0; t < NCLS; ++t) {
-        const int v = wave_sum(n[t]);
-        if (lane == 0) wc[t][wv] = v;
+    for (int u = 0; u < RPT; ++u) {
+        mine[u] = 0;
+#pragma unroll
+        for (int t = 0; t < NCLS; ++t) {
+            const u64 bt = __ballot(cu[u] == t);
+            if (cu[u] == t) mine[u] = bt;
+            if (lane == 0) wcu[u][t][wv] = __popcll(bt);
+        }
     }
     __syncthreads();
     if (tid < NCLS) {
-        int v = 0;
-        for (int w = 0; w < WAVES; ++w) v += wc[tid][w];
-        gb[tid] = v ? atomicAdd(&cls[tid], v) : 0;
+        int run = 0;
+        for (int u = 0; u < RPT; ++u)
+            for (int w = 0; w < WAVES; ++w) {
+                const int v = wcu[u][tid][w];
+                wcu[u][tid][w] = run;
+                run += v;
+            }
+        gb[tid] = run ? atomicAdd(&cls[tid], run) : 0;
     }
     __syncthreads();
-    int run[NCLS];
-#pragma unroll
-    for (int t = 0; t < NCLS; ++t) run[t] = gb[t];
 #pragma unroll
     for (int u = 0; u < RPT; ++u) {
-        const int rb = r0 + u * WG;
-        if (rb >= r1) break;  // (workgroup-uniform)
-        const int r = rb + tid;
-        const int c = r < r1 ? rc[r - r0] : -1;
-        u64 bt[NCLS];
-#pragma unroll
-        for (int t = 0; t < NCLS; ++t) {
-            bt[t] = __ballot(c == t);
-            if (lane == 0) wc[t][wv] = __popcll(bt[t]);
+        const int c = cu[u];
+        if (c >= 0) {
+            const int r = r0 + u * WG + tid;
+            lists[(long)c * m + gb[c] + wcu[u][c][wv] + lanes_below(mine[u])] = make_int4(r, ra0[u], ra1[u] - ra0[u], 0);
         }
-        __syncthreads();
-#pragma unroll
-        for (int t = 0; t < NCLS; ++t) {
-            int pre = 0, tot = 0;
-            for (int w = 0; w < WAVES; ++w) {
-                const int v = wc[t][w];
-                pre += w < wv ? v : 0;
-                tot += v;
-            }
-            if (c == t) lists[(long)t * m + run[t] + pre + lanes_below(bt[t])] = make_int4(r, ra0[u], ra1[u] - ra0[u], 0);
-            run[t] += tot;
-        }
-        __syncthreads();
     }
 }
 
