@@ -726,12 +726,16 @@ int tsg_tilespgemm(tsg_smatrix *A, tsg_smatrix *B, tsg_smatrix *C, unsigned int 
         Context &cx1 = aux.cx();
         hipStream_t s1 = aux.stream();
         int rc1 = TSG_OK;
+        // (the step times' markers only with TSG_STAGE_EVENTS=1: each cost a few
+        // us of GPU time on a ~1 ms call; the steps report 0 without them)
+        const char *sev = getenv("TSG_STAGE_EVENTS");
+        const bool se = sev && sev[0] == '1';
         auto step1 = [&] {
             long long tp = 0;
             rc1 = hipSetDevice(cx.device) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
-            if (rc1 == TSG_OK) rc1 = hipEventRecord(cx1.ev[11], s1) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
+            if (rc1 == TSG_OK && se) rc1 = hipEventRecord(cx1.ev[11], s1) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
             if (rc1 == TSG_OK) rc1 = dev_step1(cx1, dA, dB, dC, &tp, s1);
-            if (rc1 == TSG_OK) rc1 = hipEventRecord(cx1.ev[12], s1) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
+            if (rc1 == TSG_OK && se) rc1 = hipEventRecord(cx1.ev[12], s1) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
             if (rc1 == TSG_OK) rc1 = hipStreamSynchronize(s1) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
         };
         // step 1 from a host thread of its own; when the thread cannot be made
@@ -746,15 +750,15 @@ int tsg_tilespgemm(tsg_smatrix *A, tsg_smatrix *B, tsg_smatrix *C, unsigned int 
             step1();
         }
         tsg_dev_csr Cc{};
-        tsg_stats st2{};
-        rc = hipEventRecord(cx.ev[12], s) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
-        if (rc == TSG_OK) rc = dev_spgemm16(cx, &cA, &cB, s, &Cc, &st2, bsorted ? 1 : -1);
-        if (rc == TSG_OK) rc = hipEventRecord(cx.ev[13], s) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
+        rc = se && hipEventRecord(cx.ev[12], s) != hipSuccess ? TSG_ERR_HIP : TSG_OK;
+        if (rc == TSG_OK) rc = dev_spgemm16(cx, &cA, &cB, s, &Cc, nullptr, bsorted ? 1 : -1);
+        if (rc == TSG_OK && se) rc = hipEventRecord(cx.ev[13], s) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
         if (threaded) th.join();
         if (rc == TSG_OK) rc = rc1;
-        if (rc == TSG_OK) t_s1 = ev_ms(cx1.ev[11], cx1.ev[12]);
+        if (rc == TSG_OK) t_s1 = se ? ev_ms(cx1.ev[11], cx1.ev[12]) : 0.0;
         if (rc == TSG_OK) rc = dev_ctiles_from_csr(cx, Cc, dC, s);
-        if (rc == TSG_OK) rc = hipEventRecord(cx.ev[14], s) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
+        if (rc == TSG_OK && se) rc = hipEventRecord(cx.ev[14], s) == hipSuccess ? TSG_OK : TSG_ERR_HIP;
+        if (!se) evi[0] = evi[1] = evi[2] = evi[3] = -1;  // (no step times)
         if (rc == TSG_OK) TSG_HIP(hipStreamSynchronize(s));
         // a nonzero of the CSR product outside step 1's tiles, or tile totals that
         // miss nnz(C): the CSR disagrees with the tiles it was passed with
@@ -783,8 +787,10 @@ int tsg_tilespgemm(tsg_smatrix *A, tsg_smatrix *B, tsg_smatrix *C, unsigned int 
     if (rc != TSG_OK) return rc;
     // the reference's steps at every tile size: step 1 | step 2 + scan | step 3
     // (the CSR route: step 1 overlaps step 2, its own stream's duration)
-    const double t1 = t_s1 >= 0 ? t_s1 : ev_ms(cx.ev[evi[0]], cx.ev[evi[1]]),
-                 t2 = ev_ms(cx.ev[evi[1]], cx.ev[evi[2]]), t3 = ev_ms(cx.ev[evi[2]], cx.ev[evi[3]]);
+    const bool stepev = evi[0] >= 0;
+    const double t1 = t_s1 >= 0 ? t_s1 : (stepev ? ev_ms(cx.ev[evi[0]], cx.ev[evi[1]]) : 0.0),
+                 t2 = stepev ? ev_ms(cx.ev[evi[1]], cx.ev[evi[2]]) : 0.0,
+                 t3 = stepev ? ev_ms(cx.ev[evi[2]], cx.ev[evi[3]]) : 0.0;
     const double tk = std::chrono::duration<double, std::milli>(h1 - h0).count();
     if (time_step1) *time_step1 = t1;
     if (time_step2) *time_step2 = t2;
@@ -942,6 +948,9 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
         const char *se = getenv("TSG_STAGE_EVENTS");
         cx.stage_ev = se && se[0] == '1';
     }
+    // (no stats asked for -- the tiled route's product, a caller passing NULL:
+    // not even the numeric phase's bracket on the row-merge and banded paths)
+    hipEvent_t *const evp = stats || cx.stage_ev ? cx.ev : nullptr;
     if (cx.stage_ev) TSG_HIP(hipEventRecord(cx.ev[8], s));
     // Element streaming (steps 2/3 straight from the CSR operands) needs B's rows
     // column-sorted.  Sparse tiles (few nonzeros per A tile, e.g. web graphs) then
@@ -999,7 +1008,7 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
         long long path_id = -1;
         if (cx.stage_ev) TSG_HIP(hipEventRecord(cx.ev[9], s));
         if (band) {
-            const int rc = dev_spgemm_band(cx, *A, *B, bw, *C, &st, s, cx.ev);
+            const int rc = dev_spgemm_band(cx, *A, *B, bw, *C, &st, s, evp);
             cx.put(bw.win);
             cx.put(bw.width);
             cx.put(bw.ebnd);
@@ -1015,13 +1024,17 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
             dev_rows_setup_read(cx, plan);
             const bool bsorted0 = cx.pinned[1] == 0;
             if (bsorted0 && !force_band && (force_rows || dev_rows_accept(plan))) {
-                TSG_TRY(dev_rows_run(cx, *A, *B, plan, *C, &st, s, cx.ev));
+                TSG_TRY(dev_rows_run(cx, *A, *B, plan, *C, &st, s, evp));
                 path_id = TSG_PATH_ROWS;
             } else {
                 dev_rows_release(cx, plan);
             }
         }
         if (path_id >= 0) {
+            if (!evp) {  // (C complete on return, no marker)
+                TSG_TRY(stream_wait(s));
+                return TSG_OK;
+            }
             TSG_HIP(hipEventRecord(cx.ev[10], s));
             TSG_HIP(hipEventSynchronize(cx.ev[10]));
             auto h1 = std::chrono::steady_clock::now();

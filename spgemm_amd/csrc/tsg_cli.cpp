@@ -28,6 +28,9 @@ static FILE *open_csv(const std::string &dir, const char *name) {
 }
 
 int main(int argc, char **argv) {
+    // the reference prints each step's time: the step markers on (the library
+    // records them only on request; an explicit TSG_STAGE_EVENTS=0 wins)
+    setenv("TSG_STAGE_EVENTS", "1", 0);
     if (argc < 6) {
         printf("Run the code by './test -d 0 -aat 0 matrix.mtx tile_size_m tile_size_n'.\n");
         return 0;
