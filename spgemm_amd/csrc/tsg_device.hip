@@ -1430,7 +1430,7 @@ constexpr int SRT_CH = 4096;     // adjacent pairs per queued chunk of a long ro
 constexpr int SRT_SHORT = 64;    // rows of at most so many pairs: a thread's
 constexpr int SRT_REFB = 1024;   // k_ref_check's workgroups (its shares)
 __global__ __launch_bounds__(WG) void k_ref_mark(const int *ciA, int nnzA, const int *rpB, u32 *bits, int2 *items,
-                                                 int *shorts, int *cnt) {
+                                                 int *shorts, int *longs, int *cnt) {
     for (long a = (long)blockIdx.x * WG + threadIdx.x; a < nnzA; a += (long)gridDim.x * WG) {
         const int c = ciA[a];
         const u32 bit = 1u << (c & 31);
@@ -1441,16 +1441,27 @@ __global__ __launch_bounds__(WG) void k_ref_mark(const int *ciA, int nnzA, const
             shorts[atomicAdd(&cnt[1], 1)] = c;
             continue;
         }
-        const int nch = (np + SRT_CH - 1) / SRT_CH;
-        const int b = atomicAdd(&cnt[0], nch);
-        for (int j = 0; j < nch; ++j) items[b + j] = make_int2(c, j);
+        if (np <= SRT_CH) {
+            items[atomicAdd(&cnt[0], 1)] = make_int2(c, 0);
+            continue;
+        }
+        longs[atomicAdd(&cnt[2], 1)] = c;  // (its chunks spread over k_ref_check's workgroups: one
+                                           // thread queueing the mawi hub's 2,441 chunks took 73 us)
     }
 }
 __global__ __launch_bounds__(WG) void k_ref_check(const int *rpB, const int *ciB, const int2 *items,
-                                                  const int *shorts, const int *cnt, int *part) {
+                                                  const int *shorts, const int *longs, const int *cnt, int *part) {
     __shared__ int red[WAVES];
-    const int nl = cnt[0], ns = cnt[1];
+    const int nl = cnt[0], ns = cnt[1], ng = cnt[2];
     int v = 0;
+    for (int li = 0; li < ng; ++li) {  // (workgroup-uniform) rows past one chunk: chunk j on workgroup j mod grid
+        const int c = longs[li];
+        const int r0 = rpB[c], np = rpB[c + 1] - 1 - r0;
+        for (int j = blockIdx.x; j * SRT_CH < np; j += gridDim.x) {
+            const int p0 = r0 + j * SRT_CH, p1 = min(r0 + np, p0 + SRT_CH);
+            for (int p = p0 + (int)threadIdx.x; p < p1; p += WG) v += ciB[p + 1] <= ciB[p];
+        }
+    }
     for (int q = blockIdx.x; q < nl; q += gridDim.x) {  // (workgroup-uniform) long rows' chunks
         const int2 it = items[q];
         const int p0 = rpB[it.x] + it.y * SRT_CH, p1 = min(rpB[it.x + 1] - 1, p0 + SRT_CH);
@@ -1478,23 +1489,24 @@ int dev_rows_sorted_shares_ref(Context &cx, const tsg_dev_csr &A, const tsg_dev_
     TSG_HIP(hipHostGetDevicePointer((void **)&sh->dflag, host_flag, 0));
     u32 *bits = nullptr;
     int2 *items = nullptr;
-    int *shorts = nullptr;
+    int *shorts = nullptr, *longs = nullptr;
     const size_t nw = ((size_t)B.m + 31) / 32;
-    const size_t cap = (size_t)A.nnz + (size_t)B.nnz / SRT_CH + 1;  // (>= the queued long-row chunks)
-    TSG_TRY(cx.get(&bits, nw + 2));  // (+2: the two queue counts after the bits)
-    TSG_TRY(cx.get(&items, cap));
+    TSG_TRY(cx.get(&bits, nw + 3));  // (+3: the three queue counts after the bits)
+    TSG_TRY(cx.get(&items, (size_t)A.nnz));
     TSG_TRY(cx.get(&shorts, (size_t)A.nnz));
+    TSG_TRY(cx.get(&longs, (size_t)A.nnz));
     TSG_TRY(cx.get(&sh->part, (size_t)SRT_REFB));
     int *const cnt = reinterpret_cast<int *>(bits + nw);
-    TSG_HIP(hipMemsetAsync(bits, 0, (nw + 2) * sizeof(u32), s));
+    TSG_HIP(hipMemsetAsync(bits, 0, (nw + 3) * sizeof(u32), s));
     k_ref_mark<<<grid_for(A.nnz, WG, 16384), WG, 0, s>>>(A.columnindex, A.nnz, B.rowpointer, bits, items, shorts,
-                                                          cnt);
-    k_ref_check<<<SRT_REFB, WG, 0, s>>>(B.rowpointer, B.columnindex, items, shorts, cnt, sh->part);
+                                                          longs, cnt);
+    k_ref_check<<<SRT_REFB, WG, 0, s>>>(B.rowpointer, B.columnindex, items, shorts, longs, cnt, sh->part);
     TSG_HIP(hipGetLastError());
     sh->nb = SRT_REFB;
     cx.put(bits);  // (stream-ordered reuse)
     cx.put(items);
     cx.put(shorts);
+    cx.put(longs);
     return TSG_OK;
 }
 int dev_rows_sorted_finish(Context &cx, SortedShares &sh, hipStream_t s) {
