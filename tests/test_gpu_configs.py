@@ -11,7 +11,9 @@ mawi_201512020330 (config 5) at FULL scale (226 M rows, hub degree 10^7): the
 row prefix of ~2e8 products that `bench.py --matrix mawi` times a larger
 version of, through the default route (its hub-neighbour rows take the
 dominant-run kernels), against scipy's SpGEMM of the same rows (the oracle's
-dense row accumulator would need 226 M doubles per thread).
+dense row accumulator would need 226 M doubles per thread); and the benched
+prefix itself (1.49e9 nonzeros of C) whole, through the oracle's SPA pattern
+and per-row value sums by linearity.
 """
 import numpy as np
 import pytest
@@ -84,3 +86,43 @@ def test_mawi_full_scale_prefix_vs_scipy():
     np.testing.assert_array_equal(got[2], ref.indptr)
     np.testing.assert_array_equal(got[3], ref.indices)
     np.testing.assert_array_equal(got[4], ref.data)
+
+
+def test_mawi_bench_prefix_full_size_properties():
+    """The mawi prefix at the size bench.py times (the longest row prefix
+    within 1.5e9 products: 3,360 rows, C of 1.49e9 nonzeros, ~150 hub
+    neighbours on the grouped dominant-run fill), checked whole through
+    properties the oracle can afford: row pointers and every column against
+    the oracle's SPA (the reference's CPU symbolic, spgemm_serialref_spa_new.h:
+    7-105, restated in oracle/tsg_oracle.c), and each row's value sum against
+    linearity -- rowsum(C)_i = sum_k A_ik rowsum(B)_k, exact here (values
+    pos % 10 + 1: every sum an integer below 2^53)."""
+    m, n, rp, ci, _ = synth.mawi()
+    vv = (np.arange(len(ci)) % 10 + 1).astype(np.float64)
+    blen = np.diff(rp.astype(np.int64))
+    cum = np.concatenate([[0], np.cumsum(blen[ci])])[rp]
+    r = int(np.searchsorted(cum, 1.5e9, side="right") - 1)
+    assert cum[r] > 10 ** 9
+    A = T.Matrix.from_csr(r, n, rp[:r + 1].copy(), ci[:rp[r]].copy(), vv[:rp[r]].copy())
+    B = T.Matrix.from_csr(m, n, rp, ci, vv)
+    Cm, st = T.spgemm(A, B)
+    assert st["path"] == T.PATH_ROWS
+    got = Cm.csr()
+    del Cm, A, B
+    oA = O.OMat.from_csr(r, n, rp[:r + 1].copy(), ci[:rp[r]].copy(), vv[:rp[r]].copy())
+    oB = O.OMat.from_csr(m, n, rp, ci, vv)
+    srp, sci = O.spa(oA, oB, 0, r)
+    np.testing.assert_array_equal(got[2], srp)
+    assert len(got[3]) == len(sci) > 10 ** 9
+    assert np.array_equal(got[3], sci)
+    del sci
+    # (prefix sums of integer values: exact in fp64, and empty rows need no care)
+    cs = np.concatenate([[0.0], np.cumsum(vv)])
+    rowsum_b = cs[rp[1:].astype(np.int64)] - cs[rp[:-1].astype(np.int64)]
+    na = int(rp[r])
+    cs = np.concatenate([[0.0], np.cumsum(vv[:na] * rowsum_b[ci[:na]])])
+    expect = cs[rp[1:r + 1].astype(np.int64)] - cs[rp[:r].astype(np.int64)]
+    del cs
+    gc = np.concatenate([[0.0], np.cumsum(got[4])])
+    grp = got[2].astype(np.int64)
+    np.testing.assert_array_equal(gc[grp[1:]] - gc[grp[:-1]], expect)
