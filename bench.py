@@ -47,6 +47,8 @@ sys.path.insert(0, REPO)
 
 METRIC = "SpGEMM GFLOPS (fp64, C=A^2) + achieved HBM GB/s fraction, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+XGMI_LINK_GBS = 153.0  # one xGMI link, per direction (MI355X_MICROARCH.md)
+STAGE_STEPS = 3  # untimed steps with the stage events on (bench.py stage_ms)
 
 
 def log(*a):
@@ -229,6 +231,7 @@ def tiled_leg(m, n, rp, ci, vv, mb, nb, rpb, cib, vvb, aat, tm, nnzcub, reps=3, 
             del os.environ["TSG_STAGE_EVENTS"]
         steps = {k: float(info[k]) for k in steps}
         steps_src = "the second of two untimed calls after the timed ones, with TSG_STAGE_EVENTS=1"
+    calls = len(runs) + max(1, warmup) + (2 if steps_src != "the timed calls" else 0)  # tsg_tilespgemm calls made
     numblk, nnzc = int(runs[0][1]), int(runs[0][0]["nnzC"])
     # roofline of the timed region (steps 1-3): the reference's byte model
     # (B_alg) and, for context, the bytes of the reference LAYOUT the
@@ -243,7 +246,7 @@ def tiled_leg(m, n, rp, ci, vv, mb, nb, rpb, cib, vvb, aat, tm, nnzcub, reps=3, 
             "t_step1_ms": round(steps["time_step1"], 4), "t_step2_ms": round(steps["time_step2"], 4),
             "t_step3_ms": round(steps["time_step3"], 4), "t_malloc_ms": round(steps["time_malloc"], 4),
             "step_times_source": steps_src,
-            "numblkC": numblk, "nnzC": nnzc, "reps": reps, "tile": tm,
+            "numblkC": numblk, "nnzC": nnzc, "reps": reps, "tile": tm, "calls_made": calls,
             "step_times_overlap": tm == 16,
             "step_times_note": ("16x16 CSR route: step 1 runs on its own stream beside steps 2-3, so the three "
                                 "step times overlap and do not add up to t_kern_tiled_ms (t_malloc_ms, the "
@@ -394,7 +397,7 @@ def main():
                "config": {"workload": f"{name} C=A{'*A^T' if aat else '^2'} fp64, tsg_tilespgemm {tm}x{tm} "
                                       f"(tiles in -> tiled C out; the reference's timed region)",
                           "m": m, "nnzA": int(len(ci)), "nnzCub": cub, "nnzC": tl["nnzC"], "path": "tiled"},
-               "roofline": tl["roofline"], "tiled": tl}
+               "roofline": tl["roofline"], "tiled": tl, "calls_made": tl["calls_made"]}
         # HBM traffic of the call from a PMC summary of the same command (tools/profile.sh
         # --leg tiled): every kernel's bytes over the calls, which also spreads the
         # one-time csr2tile of A and B (outside the timed region) over the calls
@@ -470,6 +473,8 @@ def main():
 
     gathered = [None]
     gather_ms = []
+    compute_ms = []  # per step: this rank's pieces computed (before the gather's exposed wait)
+    calls_made = [0]  # device passes this process makes (one_step calls), for the PMC per-call accounting
     sg = None
     if gather:
         # one gatherer for every step: rank 0's C arrays are sized from the gathered
@@ -480,6 +485,8 @@ def main():
     def one_step():
         sts, nnz = [], 0
         c = None
+        calls_made[0] += 1
+        s0 = time.perf_counter()
         if gather:
             # the rounds in turn, each piece handed to the gather as soon as its C is
             # complete (the context keeps every piece's C until the step ends)
@@ -496,6 +503,7 @@ def main():
                 else:
                     sg.push(s, cv.rowptr, cv.col, cv.val, nnz=c.nnz)
             g0 = time.perf_counter()
+            compute_ms.append((g0 - s0) * 1e3)  # (ctx.spgemm returns with C complete: host time = compute)
             gathered[0] = sg.finish()
             if not host_coll:
                 torch.cuda.synchronize()
@@ -506,6 +514,7 @@ def main():
                 c, st = ctx.spgemm(dAb, dB, tm, tm)  # returns with C complete on the device
                 sts.append(st)
                 nnz += c.nnz
+            compute_ms.append((time.perf_counter() - s0) * 1e3)
         st = {k: sum(s[k] for s in sts) for k in sts[0]}
         # (labels, not sums: the path every block took, -1 for "no C tiles")
         paths = {int(s["path"]) for s in sts}
@@ -557,28 +566,81 @@ def main():
             work_share["max_row_over_mean"] = round(float(prow.max()) / mean, 6) if len(prow) else 0.0
     ms_per_step = elapsed * 1e3 / args.steps
     gflops = 2.0 * nnzcub_total * args.steps / elapsed / 1e9
+    scale_model = None
+    if dist:
+        # what bounds this N: every rank's compute time per step, the bytes each
+        # peer sends to rank 0 over its own xGMI link and, for the
+        # gather, the single-GPU time of the same product measured on rank 0
+        # (outside the timed region) -> the ceiling t_1 / max(compute_N, floor)
+        rows_mine = sum(b - a for a, b in my_pieces)
+        mine = torch.tensor([float(rows_mine), float(nnz_rank), float(np.median(compute_timed))],
+                            dtype=torch.float64, device=red_dev)
+        allm = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allm, mine)
+        rows_r = [int(x[0].item()) for x in allm]
+        nnz_r = [int(x[1].item()) for x in allm]
+        comp_r = [round(float(x[2].item()), 4) for x in allm]
+        t1_ms = None
+        if gather and rank == 0:
+            dA_full = DeviceCSR.from_host(m, n, rp, ci, vv)
+            ts = []
+            for _ in range(3):
+                ctx.reset()
+                q0 = time.perf_counter()
+                ctx.spgemm(dA_full, dB, tm, tm)  # (returns with C complete)
+                ts.append((time.perf_counter() - q0) * 1e3)
+            ctx.reset()
+            del dA_full
+            t1_ms = float(np.median(ts[1:]))  # (the first call grows the context's pool)
+        dist.barrier()
+        peer_bytes = [4.0 * (rows_r[r] + nsub) + 12.0 * nnz_r[r] for r in range(1, world)] if gather else []
+        floor_ms = max(peer_bytes) / (XGMI_LINK_GBS * 1e9) * 1e3 if peer_bytes else None
+        bound = max([max(comp_r)] + ([floor_ms] if floor_ms else []))
+        scale_model = {
+            "compute_ms": comp_r,
+            "compute_note": ("per rank, median over the timed steps: its pieces' device passes (host time to the "
+                             "last piece's C complete; ctx.spgemm is synchronous), without the exposed gather"),
+            "rows": rows_r, "nnzC": nnz_r,
+            "rank0_received_bytes": int(sum(peer_bytes)) if gather else None,
+            "max_peer_bytes": int(max(peer_bytes)) if peer_bytes else None,
+            "link_GBps": XGMI_LINK_GBS,
+            "gather_floor_ms": round(floor_ms, 4) if floor_ms is not None else None,
+            "gather_floor_note": ("the largest peer's C rows (4 B per row pointer + 12 B per nonzero) over one "
+                                  "xGMI link into rank 0; the peers send in parallel, each on its own link")
+                                 if gather else "no gather: C stays distributed",
+            "t1_ms": round(t1_ms, 4) if t1_ms is not None else None,
+            "t1_source": ("rank 0: the whole product on its own GPU after the timed steps (median of 2 "
+                          "calls after one warm call)") if t1_ms is not None else None,
+            "ceiling_speedup": round(t1_ms / bound, 3) if t1_ms and bound > 0 else None,
+            "ceiling_note": "t1_ms / max(max(compute_ms), gather_floor_ms): perfect overlap of the rounds",
+            "measured_speedup": round(t1_ms / ms_per_step, 3) if t1_ms else None,
+        }
 
     med = {k: float(np.median([s[k] for s in stats])) for k in stats[0]}
     mins = {k: float(np.min([s[k] for s in stats])) for k in ("t_e2e_ms", "t_kern_ms")}
-    # the stage breakdown from two untimed steps with the stage events on
+    compute_timed = compute_ms[-args.steps:]
+    # the stage breakdown from untimed steps with the stage events on
     # (TSG_STAGE_EVENTS=1): the timed steps record only the kernel bracket (its
     # time is the roofline's kernel_ms) -- each stage marker on the stream cost
-    # ~2-3 us of GPU time, which the timed steps do not pay
+    # ~2-3 us of GPU time, which the timed steps do not pay.  The median over
+    # STAGE_STEPS such steps (the first of them is not dropped: warm by then).
     stage_src = "timed steps (TSG_STAGE_EVENTS=1 set by the caller)"
     if os.environ.get("TSG_STAGE_EVENTS") != "1":
         n_gm = len(gather_ms)
         os.environ["TSG_STAGE_EVENTS"] = "1"
+        st_stages = []
         try:
-            for _ in range(2):
-                _, st_stage, _ = one_step()
+            for _ in range(STAGE_STEPS):
+                st_stages.append(one_step()[1])
         finally:
             del os.environ["TSG_STAGE_EVENTS"]
         del gather_ms[n_gm:]
         for k in ("t_csr2tile_ms", "t_step1_ms", "t_step2_ms", "t_step3_ms", "t_tile2csr_ms", "t_kern_ms",
                   "t_malloc_ms"):
-            med[k] = float(st_stage[k])
-        mins["t_kern_ms"] = float(st_stage["t_kern_ms"])
-        stage_src = "the second of two untimed steps after the timed ones, with TSG_STAGE_EVENTS=1"
+            med[k] = float(np.median([x[k] for x in st_stages]))
+        mins["t_kern_ms"] = float(np.min([x["t_kern_ms"] for x in st_stages]))
+        stage_src = (f"median of {STAGE_STEPS} untimed steps after the timed ones, with TSG_STAGE_EVENTS=1 "
+                     "(t_kern_ms and gflops_kern included)")
     dev_ms = med["t_csr2tile_ms"] + med["t_step1_ms"] + med["t_step2_ms"] + med["t_step3_ms"] + med["t_tile2csr_ms"]
     # SURVEY §8d algorithmic bytes (src/external/cusparse/main.cu:205-208), this rank's share
     mrank = sum(b - a for a, b in my_pieces)
@@ -635,6 +697,7 @@ def main():
         # row pointers summed as the one global CSR would hold them
         acc = np.zeros(4)
         off = 0
+        calls_made[0] += 1
         for (_, _, dAb) in dA_blocks:
             ctx.reset()
             cb, _ = ctx.spgemm(dAb, dB, tm, tm)
@@ -665,6 +728,7 @@ def main():
             chk = acc
             chk[1] += off
     if args.dump and world == 1 and not blocked:
+        calls_made[0] += 1
         ctx.reset()
         cb, _ = ctx.spgemm(dA_blocks[0][2], dB, tm, tm)
         g_rp, g_ci, g_vv = ctx.to_host(cb)[2:]
@@ -739,6 +803,8 @@ def main():
             "gather_note": ("rank 0: the gather's exposed part (after the last sub-block's compute; the "
                             "earlier sub-blocks travel while the next ones compute)") if gather_ms else None,
             "work_share": work_share,
+            "scale_model": scale_model,
+            "calls_made": calls_made[0],
             "gflops_kern": (round(2.0 * nnzcub_total / (med["t_kern_ms"] * 1e-3) / 1e9, 3)
                             if world == 1 and med["t_kern_ms"] > 0 else None),
             "tiled": tiled,

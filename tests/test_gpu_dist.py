@@ -57,6 +57,16 @@ def test_two_ranks_gather_equals_single_rank(name, aat):
     assert two["check"] == one["check"]
     assert two["config"]["nnzC"] == one["config"]["nnzC"]
     assert two["work_share"]["max_over_mean"] >= 1.0
+    # the line reads itself against the link bound: per-rank compute,
+    # the largest peer's bytes over one xGMI link, the single-GPU time of the
+    # same product and the ceiling they give
+    sm = two["scale_model"]
+    assert len(sm["compute_ms"]) == 2 and all(x > 0 for x in sm["compute_ms"])
+    assert sm["gather_floor_ms"] > 0 and sm["max_peer_bytes"] > 0
+    assert sm["rank0_received_bytes"] == sm["max_peer_bytes"]
+    assert sum(sm["nnzC"]) == one["config"]["nnzC"]
+    assert sm["t1_ms"] > 0 and sm["ceiling_speedup"] > 0 and sm["measured_speedup"] > 0
+    assert one["scale_model"] is None
 
 
 @pytest.mark.parametrize("name,aat", [("x_powerlaw_400", 1)])

@@ -23,9 +23,9 @@ timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fe
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- "${BENCH_PMC[@]}" \
   > "$OUT/pmc_write.log" 2>&1
 cd "$ROOT"
-python3 tools/pmc_summary.py "$OUT" "$TAG" $((PS + 2))
+python3 tools/pmc_summary.py "$OUT" "$TAG"
 cd /tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run -- "${BENCH_STATS[@]}" \
   > "$OUT/stats.log" 2>&1
 cd "$ROOT"
-python3 tools/pmc_summary.py "$OUT" "$TAG" $((PS + 2))
+python3 tools/pmc_summary.py "$OUT" "$TAG"
