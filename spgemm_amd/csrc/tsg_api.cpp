@@ -334,7 +334,11 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
 // A's and B's nnz equal their tiles' totals (tile_nnz[numtile], an exclusive
 // scan) and every A tile row holds as many nonzeros as the CSR rows it covers.
 // Otherwise the tile payloads are used (the payload route), so a caller whose
-// CSR and tiles disagree gets C of the tiles, as from the reference.
+// CSR and tiles disagree IN THESE COUNTS gets C of the tiles, as from the
+// reference.  Only counts are compared: a CSR with the same counts but other
+// columns is caught only if one of its products falls outside step 1's tiles
+// (the call then returns TSG_ERR_INVALID), and one with the same pattern but
+// other values gives C of the CSR's values.
 static bool csr_matches_tiles(const tsg_smatrix *A, const tsg_smatrix *B, int tm) {
     for (const tsg_smatrix *M : {A, B}) {
         if (!M->rowpointer || !M->columnindex || !M->value || !M->tile_nnz || !M->tile_ptr) return false;
@@ -691,8 +695,7 @@ int tsg_tilespgemm(tsg_smatrix *A, tsg_smatrix *B, tsg_smatrix *C, unsigned int 
         if (sq16 && allow && csr_matches_tiles(A, B, tm)) {
             TSG_TRY(upload_csr(cx, A, cA, s));
             TSG_TRY(upload_csr(cx, B, cB, s));
-            TSG_TRY(dev_rows_sorted(cx, cB, &bsorted, s));
-            use_csr = bsorted;
+            use_csr = true;  // (if B's rows turn out column-sorted: checked inside the timed region)
         }
     }
     if (use_csr) {
@@ -705,6 +708,19 @@ int tsg_tilespgemm(tsg_smatrix *A, tsg_smatrix *B, tsg_smatrix *C, unsigned int 
     TSG_HIP(hipStreamSynchronize(s));
     tsg_stats st{};
     auto h0 = std::chrono::steady_clock::now();
+    if (use_csr) {
+        // B's sortedness decides the route: work of the call, so inside the timed
+        // region.  Unsorted rows (rare) take the tile payloads after all, whose
+        // copies then fall inside it too (the pool keeps the structures until
+        // the call's end).
+        TSG_TRY(dev_rows_sorted(cx, cB, &bsorted, s));
+        use_csr = bsorted;
+        if (!use_csr) {
+            TSG_TRY(upload_tiles(cx, A, tm, tn, false, dA, s));
+            TSG_TRY(upload_tiles(cx, B, tn, tm, true, dB, s));
+            TSG_HIP(hipStreamSynchronize(s));
+        }
+    }
     int rc;
     int evi[4] = {0, 1, 2, 3};  // the events bracketing steps 1 | 2 | 3
     HostLease aux;  // the CSR route's step 1: its own context and stream (outlives the download)

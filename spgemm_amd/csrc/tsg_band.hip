@@ -406,9 +406,10 @@ int dev_spgemm_band(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, Ban
         if (A.nnz > 0) k_band_ebnd<<<grid_for(A.nnz, WG, 16384), WG, 0, s>>>(A.columnindex, A.nnz, B.rowpointer, ebnd);
         TSG_HIP(hipGetLastError());
     }
-    // staging: BD_SPAN slots per row while that stays within 2 GiB (no scan of
-    // the window widths: two launches fewer), else the widths' prefix
-    const bool fixed = (long long)m * BD_SPAN * 12 <= (2LL << 30);
+    // staging: BD_SPAN slots per row while that stays within 2 GiB and within 4x
+    // the window columns (no scan of the window widths: two launches fewer; cant:
+    // 1.9x), else the widths' prefix (narrow windows: no near-2 GiB staging)
+    const bool fixed = (long long)m * BD_SPAN * 12 <= (2LL << 30) && (long long)m * BD_SPAN <= 4 * bw.wcols;
     const long long slots = fixed ? (long long)m * BD_SPAN : bw.wcols;
     TSG_TRY(cx.get(&Scol, (size_t)slots + 1));
     TSG_TRY(cx.get(&Sval, (size_t)slots + 1));

@@ -290,9 +290,10 @@ def test_rows_hub_rows_windowed_and_dominant_run():
 def test_rows_dominant_run_rows_grouped_by_run(monkeypatch, per_row):
     """Many dominant-run rows sharing a run (the mawi pattern: every hub
     neighbour's C row holds the hub's whole B row): k_rows_dr_group sorts them
-    by run and cuts each run's rows into blocks of DR_GR = 32 whose chunks of
+    by run and cuts each run's rows into blocks of DR_GR = 16 whose chunks of
     DR_CH = 16,384 elements read the run once for the block.  71 + 32 rows on
-    two runs of 120,000 / 70,001 columns (blocks of 32, 32, 7 and 32), their
+    two runs of 120,000 / 70,001 columns (blocks of 16, 16, 16, 16, 7 and 16,
+    16: a partial last block on the first run), their
     inserted columns before, inside (some L holds: a sum) and past the run, in
     one range or many; with TSG_DR_PER_ROW the per-row chunks instead."""
     if per_row:
