@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of library variants (spgemm_amd/lib/variants/libtsg_<name>.so, tools/build_variant.sh)
-# against the main build: bash tools/r4_ab.sh TAG "variant ..." bench args...
+# against the main build: bash tools/ab.sh TAG "variant ..." bench args...
 set -uo pipefail
 TAG=$1; VARS=$2; shift 2
 mkdir -p gpurun_out

@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B of an environment setting: bash tools/r4_abenv.sh TAG "VAR=VALUE" bench-args
+# A/B of an environment setting: bash tools/abenv.sh TAG "VAR=VALUE" bench-args
 set -uo pipefail
 TAG=$1; ENVSET=$2; shift 2
 mkdir -p gpurun_out

@@ -13,13 +13,13 @@ if [ -n "${TESTS:-}" ]; then
   [ $rc -eq 0 ] || { grep -E "^(FAILED|ERROR)|Error|assert" gpurun_out/${TAG}_tests.log | head -20; exit 1; }
 fi
 for ab in ${AB:-}; do  # matrix:variant (spgemm_amd/lib/variants/libtsg_<variant>.so)
-  bash tools/r4_ab.sh ${TAG}_${ab%%:*} "${ab#*:}" --matrix ${ab%%:*} || exit 1
+  bash tools/ab.sh ${TAG}_${ab%%:*} "${ab#*:}" --matrix ${ab%%:*} || exit 1
 done
 for ab in ${TAB:-}; do  # matrix:variant, the tiled drop-in leg (tsg_tilespgemm)
-  bash tools/r4_ab.sh ${TAG}_tiled_${ab%%:*} "${ab#*:}" --matrix ${ab%%:*} --leg tiled --steps 5 || exit 1
+  bash tools/ab.sh ${TAG}_tiled_${ab%%:*} "${ab#*:}" --matrix ${ab%%:*} --leg tiled --steps 5 || exit 1
 done
 for ab in ${ENVAB:-}; do  # matrix:VAR=VALUE
-  bash tools/r4_abenv.sh ${TAG}_${ab%%:*} "${ab#*:}" --matrix ${ab%%:*} || exit 1
+  bash tools/abenv.sh ${TAG}_${ab%%:*} "${ab#*:}" --matrix ${ab%%:*} || exit 1
 done
 for m in ${PROF:-}; do  # kernel trace + stats of one bench command
   ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \

@@ -1,7 +1,7 @@
 #!/bin/bash
-# round 4: the GPU test suite + smoke (log under gpurun_out/$1_tests.log)
+# the GPU test suite + smoke (log under gpurun_out/$1_tests.log)
 set -uo pipefail
-TAG=${1:-r4}
+TAG=${1:-r6}
 mkdir -p gpurun_out
 timeout -k 10 900 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests > gpurun_out/${TAG}_tests.log 2>&1; rc=$?
 tail -4 gpurun_out/${TAG}_tests.log

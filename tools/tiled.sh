@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 4: the drop-in tiled path (tsg_tilespgemm): its tests, then webbase and cant lines
+# the drop-in tiled path (tsg_tilespgemm): its tests, then webbase and cant lines
 set -uo pipefail
 TAG=${1:-r4t}
 mkdir -p gpurun_out
