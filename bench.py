@@ -538,6 +538,7 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    compute_timed = compute_ms[-args.steps:]  # (the timed steps' compute times)
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -618,7 +619,6 @@ def main():
 
     med = {k: float(np.median([s[k] for s in stats])) for k in stats[0]}
     mins = {k: float(np.min([s[k] for s in stats])) for k in ("t_e2e_ms", "t_kern_ms")}
-    compute_timed = compute_ms[-args.steps:]
     # the stage breakdown from untimed steps with the stage events on
     # (TSG_STAGE_EVENTS=1): the timed steps record only the kernel bracket (its
     # time is the roofline's kernel_ms) -- each stage marker on the stream cost
