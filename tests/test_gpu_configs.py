@@ -4,8 +4,9 @@ com-LiveJournal (config 4): the R-MAT stand-in's A^2 has 1.3e11 intermediate
 products -- past the reference's `int nnzC` (src/tilespgemm-cuda.h:2327) -- so
 the product runs as sequential tile-row blocks (spgemm_amd.dist.product_blocks,
 what `bench.py --matrix lj` times).  Here: the block with the most work (the
-hub rows, the load-imbalanced case) and two strided blocks, each C against the
+hub rows, the load-imbalanced case) and strided blocks, each C against the
 numeric Gustavson oracle at 1e8-product blocks (host-checkable sizes).
+(Here: the heaviest block and twenty strided ones.)
 
 mawi_201512020330 (config 5) at FULL scale (226 M rows, hub degree 10^7): the
 row prefix of ~2e8 products that `bench.py --matrix mawi` times a larger
@@ -13,7 +14,8 @@ version of, through the default route (its hub-neighbour rows take the
 dominant-run kernels), against scipy's SpGEMM of the same rows (the oracle's
 dense row accumulator would need 226 M doubles per thread); and the benched
 prefix itself (1.49e9 nonzeros of C) whole, through the oracle's SPA pattern
-and per-row value sums by linearity.
+and per-row value sums by linearity, plus every value of every 48th row
+against scipy.
 """
 import numpy as np
 import pytest
@@ -41,8 +43,8 @@ def test_lj_heaviest_and_strided_row_blocks_vs_oracle(lj):
     work = np.array([cum[b1] - cum[b0] for b0, b1 in blocks], dtype=np.float64)
     rows = np.array([b1 - b0 for b0, b1 in blocks])
     dens = work / rows
-    # the heaviest block and ten strided ones
-    pick = [int(np.argmax(dens))] + [k * len(blocks) // 11 for k in range(1, 11)]
+    # the heaviest block and twenty strided ones
+    pick = [int(np.argmax(dens))] + [k * len(blocks) // 21 for k in range(1, 21)]
     B = T.Matrix.from_csr(m, n, rp, ci, vv)
     oB = O.OMat.from_csr(m, n, rp, ci, vv)
     for k in pick:
@@ -96,7 +98,8 @@ def test_mawi_bench_prefix_full_size_properties():
     the oracle's SPA (the reference's CPU symbolic, spgemm_serialref_spa_new.h:
     7-105, restated in oracle/tsg_oracle.c), and each row's value sum against
     linearity -- rowsum(C)_i = sum_k A_ik rowsum(B)_k, exact here (values
-    pos % 10 + 1: every sum an integer below 2^53)."""
+    pos % 10 + 1: every sum an integer below 2^53); then every value of every
+    48th row element for element against scipy."""
     m, n, rp, ci, _ = synth.mawi()
     vv = (np.arange(len(ci)) % 10 + 1).astype(np.float64)
     blen = np.diff(rp.astype(np.int64))
@@ -126,3 +129,19 @@ def test_mawi_bench_prefix_full_size_properties():
     gc = np.concatenate([[0.0], np.cumsum(got[4])])
     grp = got[2].astype(np.int64)
     np.testing.assert_array_equal(gc[grp[1:]] - gc[grp[:-1]], expect)
+    del gc
+    # and every value of a strided sample of the rows (every 48th: ~70 rows, a
+    # few of them hub neighbours on the dominant-run fill) element for element
+    # against scipy's SpGEMM of those rows (exact: small integer sums)
+    import scipy.sparse as sp
+    rows = np.arange(0, r, 48)
+    lens = (rp[rows + 1] - rp[rows]).astype(np.int64)
+    idx = np.concatenate([np.arange(rp[i], rp[i + 1]) for i in rows])
+    As = sp.csr_matrix((vv[idx], ci[idx], np.concatenate([[0], np.cumsum(lens)])), shape=(len(rows), n))
+    ref = (As @ sp.csr_matrix((vv, ci, rp), shape=(m, n))).tocsr()
+    ref.sort_indices()
+    assert (np.diff(ref.indptr) > 65536).any()  # (hub neighbours among them)
+    for j, i in enumerate(rows):
+        a, b = int(grp[i]), int(grp[i + 1])
+        np.testing.assert_array_equal(got[3][a:b], ref.indices[ref.indptr[j]:ref.indptr[j + 1]])
+        np.testing.assert_array_equal(got[4][a:b], ref.data[ref.indptr[j]:ref.indptr[j + 1]])
