@@ -297,13 +297,17 @@ __global__ __launch_bounds__(BD_WG) void k_band_rows(BandArgs g) {
     __syncthreads();
     // ---- the row's columns and values, in column order, to the staging area
     if (r == 0 && tid == 0) g.rnnz[g.m] = 0;
+    // (the staging nontemporal, here and in k_band_compact: 208 MB on cant that
+    // no later walk reads, kept out of the L2s that hold the B rows -- cant
+    // 0.700 -> 0.651 ms, k_band_rows 500 -> 457 us; the same on the row-merge
+    // classes' scattered row segments measured 0.6 ms slower)
     const long long E = g.soff ? g.soff[r] : (long long)r * BD_SPAN;
     for (int i = tid; i < span; i += BD_WG) {
         const u32 word = bm[i >> 5], bit = 1u << (i & 31);
         if (word & bit) {
             const long long pos = E + wpre[i >> 5] + __popc(word & (bit - 1u));
-            g.Scol[pos] = lo + i;
-            g.Sval[pos] = acc[i];
+            __builtin_nontemporal_store(lo + i, g.Scol + pos);
+            __builtin_nontemporal_store(acc[i], g.Sval + pos);
         }
     }
 }
@@ -321,13 +325,13 @@ __global__ __launch_bounds__(WG) void k_band_compact(int m, const long long *sof
             double v[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                c[u] = Scol[s0 + i + 64 * u];
-                v[u] = Sval[s0 + i + 64 * u];
+                c[u] = __builtin_nontemporal_load(Scol + s0 + i + 64 * u);
+                v[u] = __builtin_nontemporal_load(Sval + s0 + i + 64 * u);
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                Ccol[d0 + i + 64 * u] = c[u];
-                Cval[d0 + i + 64 * u] = v[u];
+                __builtin_nontemporal_store(c[u], Ccol + d0 + i + 64 * u);
+                __builtin_nontemporal_store(v[u], Cval + d0 + i + 64 * u);
             }
         }
         for (; i < n; i += 64) {
