@@ -23,8 +23,8 @@
 namespace tsg {
 
 namespace {
-constexpr int CT_NT = 512, CT_NW = CT_NT / 64;
-constexpr int CT_TC = 992;                  // tiles per unit (LDS: 4 workgroups per CU)
+constexpr int CT_NT = 256, CT_NW = CT_NT / 64;
+constexpr int CT_TC = 496;                  // tiles per unit (LDS: 8 workgroups per CU; 992 tiles at 512 threads: +3 % on webbase)
 constexpr int CT_TPT = (CT_TC + CT_NT - 1) / CT_NT;  // tiles per thread in the tile phase
 constexpr int CT_EPT = 4;                   // nonzeros per thread held in registers (8: 1.91 vs 1.81 ms on webbase)
 constexpr int CT_EB = CT_EPT * CT_NT;       // ... a batch of the unit's nonzeros
