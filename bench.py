@@ -482,6 +482,10 @@ def main():
         meta = dist.new_group(backend="gloo")
         sg = tdist.RoundGather(rank, world, pieces, 0, device="cpu" if host_coll else "cuda", meta_group=meta)
 
+    # B's rows checked once (outside the timed steps; every step's first block
+    # checks again inside its own call): the later row blocks of a step skip it
+    b_ok = len(dA_blocks) > 1 and ctx.rows_sorted(dB)
+
     def one_step():
         sts, nnz = [], 0
         c = None
@@ -494,7 +498,7 @@ def main():
             gathered[0] = None
             sg.reset()
             for s, (_, _, dAb) in enumerate(dA_blocks):
-                c, st = ctx.spgemm(dAb, dB, tm, tm)
+                c, st = ctx.spgemm(dAb, dB, tm, tm, b_sorted=s > 0 and b_ok)
                 sts.append(st)
                 nnz += c.nnz
                 cv = ctx.view_torch(c)  # zero-copy views of the context-owned C
@@ -509,9 +513,11 @@ def main():
                 torch.cuda.synchronize()
             gather_ms.append((time.perf_counter() - g0) * 1e3)  # (the last round's, not hidden behind compute)
         else:
-            for (_, _, dAb) in dA_blocks:
+            for bi, (_, _, dAb) in enumerate(dA_blocks):
                 ctx.reset()
-                c, st = ctx.spgemm(dAb, dB, tm, tm)  # returns with C complete on the device
+                # (row blocks over one B: B's sortedness checked once per step, by the
+                # first block's call; the others skip it -- tsg_dev_spgemm_sorted_b)
+                c, st = ctx.spgemm(dAb, dB, tm, tm, b_sorted=bi > 0 and b_ok)  # returns with C complete
                 sts.append(st)
                 nnz += c.nnz
             compute_ms.append((time.perf_counter() - s0) * 1e3)

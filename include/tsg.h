@@ -204,6 +204,18 @@ int tsg_dev_transpose(tsg_context *ctx, const tsg_dev_csr *A, void *stream, tsg_
 int tsg_dev_spgemm(tsg_context *ctx, const tsg_dev_csr *A, const tsg_dev_csr *B,
                    int tile_size_m, int tile_size_n, void *stream, tsg_dev_csr *C,
                    tsg_stats *stats);
+/* Whether every row of M is strictly column-sorted (*sorted = 1, else 0): the
+ * check tsg_dev_spgemm makes on B on every call (the row-merge and banded
+ * routes need it), on its own. */
+int tsg_dev_csr_rows_sorted(tsg_context *ctx, const tsg_dev_csr *M, void *stream, int *sorted);
+/* tsg_dev_spgemm for a B whose rows the caller has found column-sorted
+ * (tsg_dev_csr_rows_sorted returned 1 and B has not changed since; the
+ * caller's contract -- an unsorted B passed here gives a wrong C): the
+ * per-call check of B is skipped, so a sequence of row blocks of A against one
+ * B checks B once.  b_checked_sorted = 0 is tsg_dev_spgemm itself. */
+int tsg_dev_spgemm_sorted_b(tsg_context *ctx, const tsg_dev_csr *A, const tsg_dev_csr *B,
+                            int b_checked_sorted, int tile_size_m, int tile_size_n, void *stream,
+                            tsg_dev_csr *C, tsg_stats *stats);
 /* Copies between host and device (stream-ordered, synchronous on return). */
 int tsg_memcpy_h2d(tsg_context *ctx, void *dst, const void *src, size_t bytes, void *stream);
 int tsg_memcpy_d2h(tsg_context *ctx, void *dst, const void *src, size_t bytes, void *stream);

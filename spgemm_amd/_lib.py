@@ -103,6 +103,9 @@ _SIGS = {
     "tsg_dev_transpose": ([C.c_void_p, C.POINTER(DevCSR), C.c_void_p, C.POINTER(DevCSR)], C.c_int),
     "tsg_dev_spgemm": ([C.c_void_p, C.POINTER(DevCSR), C.POINTER(DevCSR), C.c_int, C.c_int, C.c_void_p,
                         C.POINTER(DevCSR), C.POINTER(Stats)], C.c_int),
+    "tsg_dev_spgemm_sorted_b": ([C.c_void_p, C.POINTER(DevCSR), C.POINTER(DevCSR), C.c_int, C.c_int, C.c_int,
+                                 C.c_void_p, C.POINTER(DevCSR), C.POINTER(Stats)], C.c_int),
+    "tsg_dev_csr_rows_sorted": ([C.c_void_p, C.POINTER(DevCSR), C.c_void_p, C.POINTER(C.c_int)], C.c_int),
     "tsg_memcpy_h2d": ([C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p], C.c_int),
     "tsg_memcpy_d2h": ([C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p], C.c_int),
     "tsg_memcpy_d2d": ([C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p], C.c_int),

@@ -1156,6 +1156,21 @@ int tsg_dev_spgemm(tsg_context *ctx, const tsg_dev_csr *A, const tsg_dev_csr *B,
     return dev_spgemm16(ctx->cx, A, B, (hipStream_t)stream, C, stats);
 }
 
+int tsg_dev_spgemm_sorted_b(tsg_context *ctx, const tsg_dev_csr *A, const tsg_dev_csr *B, int b_checked_sorted,
+                            int tm, int tn, void *stream, tsg_dev_csr *C, tsg_stats *stats) {
+    if (!ctx || !A || !B || !C || !valid_tiles(tm, tn) || A->n != B->m) return TSG_ERR_INVALID;
+    if (!tile_side_supported(tm) || !tile_side_supported(tn)) return TSG_ERR_UNSUPPORTED;
+    return dev_spgemm16(ctx->cx, A, B, (hipStream_t)stream, C, stats, b_checked_sorted == 1 ? 1 : -1);
+}
+
+int tsg_dev_csr_rows_sorted(tsg_context *ctx, const tsg_dev_csr *M, void *stream, int *sorted) {
+    if (!ctx || !M || !sorted || M->m < 0 || M->nnz < 0) return TSG_ERR_INVALID;
+    bool ok = false;
+    TSG_TRY(dev_rows_sorted(ctx->cx, *M, &ok, (hipStream_t)stream));
+    *sorted = ok ? 1 : 0;
+    return TSG_OK;
+}
+
 int tsg_spgemm_csr(const tsg_smatrix *A, const tsg_smatrix *B, tsg_smatrix *C, int tm, int tn,
                    tsg_stats *stats) {
     if (!A || !B || !C || A->n != B->m || !valid_tiles(tm, tn)) return TSG_ERR_INVALID;

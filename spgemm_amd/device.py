@@ -59,14 +59,28 @@ class Context:
     def reset(self):
         check("tsg_context_reset", lib().tsg_context_reset(self.ptr))
 
-    def spgemm(self, A, B, tile_m=16, tile_n=16, stream=None):
+    def spgemm(self, A, B, tile_m=16, tile_n=16, stream=None, b_sorted=False):
         """C = A*B device CSR in -> device CSR out.  Returns (DevCSR struct with
-        context-owned pointers, stats dict).  Valid until the next reset()."""
+        context-owned pointers, stats dict).  Valid until the next reset().
+        b_sorted=True: the caller found B's rows column-sorted (rows_sorted) and B
+        has not changed since -- the per-call check is skipped
+        (tsg_dev_spgemm_sorted_b)."""
         a, b, c, st = A.struct(), B.struct(), DevCSR(), Stats()
         s = C.c_void_p(stream) if stream else None
-        check("tsg_dev_spgemm", lib().tsg_dev_spgemm(self.ptr, C.byref(a), C.byref(b), tile_m, tile_n, s,
-                                                     C.byref(c), C.byref(st)))
+        if b_sorted:
+            check("tsg_dev_spgemm_sorted_b", lib().tsg_dev_spgemm_sorted_b(
+                self.ptr, C.byref(a), C.byref(b), 1, tile_m, tile_n, s, C.byref(c), C.byref(st)))
+        else:
+            check("tsg_dev_spgemm", lib().tsg_dev_spgemm(self.ptr, C.byref(a), C.byref(b), tile_m, tile_n, s,
+                                                         C.byref(c), C.byref(st)))
         return c, st.as_dict()
+
+    def rows_sorted(self, M, stream=None):
+        """whether every row of the device CSR M is strictly column-sorted"""
+        m, out = M.struct(), C.c_int(0)
+        s = C.c_void_p(stream) if stream else None
+        check("tsg_dev_csr_rows_sorted", lib().tsg_dev_csr_rows_sorted(self.ptr, C.byref(m), s, C.byref(out)))
+        return bool(out.value)
 
     def transpose(self, A, stream=None):
         a, c = A.struct(), DevCSR()

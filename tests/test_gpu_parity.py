@@ -223,6 +223,23 @@ def test_device_api_matches_host_api():
         ctx.reset()
         c2, _ = ctx.spgemm(dA, dA)
         assert_csr_equal(ctx.to_host(c2), got)
+    # B's sortedness checked once, then the calls that skip it
+    # (tsg_dev_csr_rows_sorted, tsg_dev_spgemm_sorted_b): the same C
+    assert ctx.rows_sorted(dA)
+    ctx.reset()
+    c3, st3 = ctx.spgemm(dA, dA, b_sorted=True)
+    assert_csr_equal(ctx.to_host(c3), got)
+    assert st3["path"] == st["path"]
+    # an unsorted B is reported as such, and the checking call routes it to the
+    # staged tile pipeline with the right C
+    mu, nu_, rpu, ciu, vvu = synth.random_csr(3000, 3000, density=0.003, seed=12, unsorted=True)
+    dU = DeviceCSR.from_host(mu, nu_, rpu, ciu, vvu)
+    assert not ctx.rows_sorted(dU)
+    ctx.reset()
+    c4, st4 = ctx.spgemm(dA, dU)
+    oU = O.OMat.from_csr(mu, nu_, rpu, ciu, vvu)
+    assert_csr_equal(ctx.to_host(c4), O.gustavson(oA, oU).csr())
+    assert st4["path"] == T.PATH_TILES
     ctx.close()
 
 
