@@ -1382,12 +1382,18 @@ __device__ __forceinline__ long long row_longest_run(const long long *E, int a0,
 //   k_rows_wscatter a workgroup per chunk: each product's (column, a*b) to its
 //                  window's bucket in the row's staging, at the chunk's place
 //                  plus an LDS cursor;
-//   k_rows_wunit   a workgroup per unit: the bucket's columns ORed into an LDS
-//                  bitmap of the window, ranks by popcount prefixes, the values
-//                  added at their ranks in LDS, the unit's nonzeros out in
-//                  column order (to a second area: the bucket is still read);
-//   k_rows_wgather each unit's nonzeros to the row's staging slots at the
-//                  unit's output offset (then the common compaction).
+//   k_rows_wunit<0> a workgroup per unit: the bucket's columns ORed into an
+//                  LDS bitmap of the window; its popcount is the unit's nnz;
+//   k_rows_wunit<1> after the row scan (every count known): the bitmap again,
+//                  ranks by popcount prefixes, the values added at their ranks
+//                  in LDS, the unit's nonzeros straight into C in column order
+//                  at the row's pointer + the unit's offset.  (Until round 6
+//                  one unit kernel wrote them to an output area that a gather
+//                  then copied into C, 24 B per nonzero; the split reads the
+//                  bucket's columns twice, 4 B per product: a 60,000-row
+//                  LiveJournal block 29.6 -> 29.2 ms.  Storing the count
+//                  kernel's bitmaps for the fill to load, 2^wb bits per unit,
+//                  measured 31.1 ms.)
 // Every product is read from B once for its column (counts) and once with its
 // value (scatter), then through its bucket once; no global atomic per
 // product, and a hub row's work is spread over as many workgroups as it has
@@ -1425,10 +1431,10 @@ __device__ __forceinline__ long long w_block_sum(long long x, long long *red) {
 }
 
 // a workgroup per class-H row i.  Outputs (zero unless a W row): wnw[i] units,
-// wnch[i] chunks, wlo[i] first column, wwb[i] window bits, wpre[i] products;
+// wnch[i] chunks, wlo[i] first column, wwb[i] window bits;
 // wst[0] += W rows' products, wst[1] / wst[2] += DR rows' products / rows.
 __global__ __launch_bounds__(W_NT) void k_rows_wplan(RowsArgs g, int bn, long long unit, int *wnw, int *wnch,
-                                                    int *wlo, int *wwb, long long *wpre, long long *wmat,
+                                                    int *wlo, int *wwb, long long *wmat,
                                                     unsigned long long *wst, long long *soff) {
     constexpr int NW = W_NT / 64;
     __shared__ int red[2 * NW];
@@ -1507,9 +1513,8 @@ __global__ __launch_bounds__(W_NT) void k_rows_wplan(RowsArgs g, int bn, long lo
         wnch[i] = nch;
         wlo[i] = lo;
         wwb[i] = wb;
-        wpre[i] = pw;
         wmat[i] = (long long)nch * nw;
-        if (nw) soff[le.x] = -1;  // (the compaction skips the row: k_rows_wgather writes it)
+        if (nw) soff[le.x] = -1;  // (the compaction skips the row: k_rows_wunit<1> writes it)
         if (pw) atomicAdd(&wst[0], (unsigned long long)pw);
         if (dr) {
             atomicAdd(&wst[1], (unsigned long long)P);
@@ -1603,19 +1608,18 @@ __global__ __launch_bounds__(W_NT) void k_rows_wcount(RowsArgs g, const int4 *ch
 // list -> E first cost three round trips per unit)
 struct WUnit {
     long long s0;   // its bucket in the row's staging slots
-    long long o0;   // its output slots
     int wlo0;       // its window's first column
     int wb;         // window bits
     int n;          // its bucket's products
-    int pad;
+    int row;        // its C row
 };
 
 // per W row (a workgroup per class-H row): out[u] = exclusive scan of in[u]
 // over the row's units; rnnz (optional) gets the row's total; rec (optional,
-// with wlo, wwb, wpre) the units' work records
+// with wlo, wwb) the units' work records
 __global__ __launch_bounds__(W_NT) void k_rows_wscan(RowsArgs g, const int *ubase, const int *in, int *out,
                                                     int *rnnz, WUnit *rec = nullptr, const int *wlo = nullptr,
-                                                    const int *wwb = nullptr, const long long *wpre = nullptr) {
+                                                    const int *wwb = nullptr) {
     constexpr int NW = W_NT / 64, PT = W_MAXW / W_NT;
     __shared__ int red[NW];
     const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
@@ -1637,11 +1641,12 @@ __global__ __launch_bounds__(W_NT) void k_rows_wscan(RowsArgs g, const int *ubas
         off += w < wv ? red[w] : 0;
         tot += red[w];
     }
-    long long rb = 0, ob = 0;
-    int lo = 0, wb = 0;
+    long long rb = 0;
+    int lo = 0, wb = 0, row = 0;
     if (rec) {  // (kernel-uniform)
-        rb = g.E[g.list[blockIdx.x].y];
-        ob = wpre[blockIdx.x];
+        const int4 le = g.list[blockIdx.x];
+        rb = g.E[le.y];
+        row = le.x;
         lo = wlo[blockIdx.x];
         wb = wwb[blockIdx.x];
     }
@@ -1650,7 +1655,7 @@ __global__ __launch_bounds__(W_NT) void k_rows_wscan(RowsArgs g, const int *ubas
         const int w = tid * PT + t;
         if (w < nw) {
             out[u0 + w] = off;
-            if (rec) rec[u0 + w] = WUnit{rb + off, ob + off, lo + (w << wb), wb, v[t], 0};
+            if (rec) rec[u0 + w] = WUnit{rb + off, lo + (w << wb), wb, v[t], row};
         }
         off += v[t];
     }
@@ -1714,11 +1719,17 @@ __device__ __forceinline__ int w_rank(const u64 *bm, const u16 *g4, const int *b
     return rk;
 }
 
-// a workgroup per unit u (row i = umap[u], window u - ubase[i]): its bucket
-// (ucnt[u] products at E[a0] + ubo[u]) -> its nonzeros, column-sorted, at
-// Ocol/Oval + wpre[i] + ubo[u]; ucount[u] = their number
-__global__ __launch_bounds__(WU_NT) void k_rows_wunit(RowsArgs g, const WUnit *urec, int *ucount, int *Ocol,
-                                                    double *Oval) {
+// a workgroup per unit u (its record R: bucket of R.n products at R.s0, window
+// of 2^R.wb columns from R.wlo0, C row R.row).
+//   MODE 0 (count): the bucket's columns ORed into an LDS bitmap of the window;
+//     ucount[u] = its popcount.
+//   MODE 1 (fill, after the row scan): the bitmap again, ranks by popcount
+//     prefixes (u16 per 4-word group, int per 512-word block), the values added
+//     at their ranks in LDS, the unit's nonzeros written in column order into C
+//     at Crp[R.row] + uoff[u].
+template <int MODE>
+__global__ __launch_bounds__(WU_NT) void k_rows_wunit(RowsArgs g, const WUnit *urec, int *ucount, const int *uoff,
+                                                    const int *Crp, int *Ccol, double *Cval) {
     constexpr int NW = WU_NT / 64;
     __shared__ __align__(16) u64 bm[W_WORDS];
     __shared__ u16 g4[W_WORDS / 4];
@@ -1731,15 +1742,47 @@ __global__ __launch_bounds__(WU_NT) void k_rows_wunit(RowsArgs g, const WUnit *u
     const WUnit R = urec[u];
     const int n = R.n;
     if (n == 0) {  // (workgroup-uniform)
-        if (tid == 0) ucount[u] = 0;
+        if (MODE == 0 && tid == 0) ucount[u] = 0;
         return;
     }
     const int wb = R.wb;
     const long long wlo0 = R.wlo0;
     const long long s0 = R.s0;
     const int nwd = 1 << (wb - 6);
+    if constexpr (MODE == 0) {
+        for (int w = tid; w < nwd; w += WU_NT) bm[w] = 0ull;
+        int cc[W_RPT];
+#pragma unroll
+        for (int t = 0; t < W_RPT; ++t) {
+            const int q = t * WU_NT + tid;
+            cc[t] = q < n ? (int)(g.Scol[s0 + q] - wlo0) : -1;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < W_RPT; ++t)
+            if (cc[t] >= 0) atomicOr(&bm[cc[t] >> 6], 1ull << (cc[t] & 63));
+        for (int q = W_RPT * WU_NT + tid; q < n; q += WU_NT) {
+            const int c = (int)(g.Scol[s0 + q] - wlo0);
+            atomicOr(&bm[c >> 6], 1ull << (c & 63));
+        }
+        __syncthreads();
+        int cnt = 0;
+        for (int w = tid; w < nwd; w += WU_NT) cnt += __popcll(bm[w]);
+        cnt = wave_sum(cnt);
+        if (lane == 0) red[wv] = cnt;
+        __syncthreads();
+        if (tid == 0) {
+            int t = 0;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) t += red[w];
+            ucount[u] = t;
+        }
+        RP_DONE(0);
+        return;
+    }
+    // (fill) the first W_RPT * WU_NT products in registers (the rest read again
+    // below), the bitmap again, the unit's place in C
     for (int w = tid; w < nwd; w += WU_NT) bm[w] = 0ull;
-    // the first W_RPT * WU_NT products in registers (the rest read again below)
     int cc[W_RPT];
     double xx[W_RPT];
 #pragma unroll
@@ -1748,8 +1791,8 @@ __global__ __launch_bounds__(WU_NT) void k_rows_wunit(RowsArgs g, const WUnit *u
         cc[t] = q < n ? (int)(g.Scol[s0 + q] - wlo0) : -1;
         xx[t] = q < n ? g.Sval[s0 + q] : 0.0;
     }
+    const long long o0 = (long long)Crp[R.row] + uoff[u];
     __syncthreads();
-    RP(0);
 #pragma unroll
     for (int t = 0; t < W_RPT; ++t)
         if (cc[t] >= 0) atomicOr(&bm[cc[t] >> 6], 1ull << (cc[t] & 63));
@@ -1787,7 +1830,6 @@ __global__ __launch_bounds__(WU_NT) void k_rows_wunit(RowsArgs g, const WUnit *u
     int rk[W_RPT];
 #pragma unroll
     for (int t = 0; t < W_RPT; ++t) rk[t] = cc[t] >= 0 ? w_rank(bm, g4, blk, cc[t]) : 0;
-    const long long o0 = R.o0;
     static_assert(2 * W_WORDS >= W_RPT * WU_NT, "the bitmap's LDS holds a column per rank (wn <= n)");
     if (n <= W_RPT * WU_NT) {  // (workgroup-uniform) every product in registers
         // the bitmap is done with once the ranks are: its LDS takes each rank's
@@ -1811,13 +1853,12 @@ __global__ __launch_bounds__(WU_NT) void k_rows_wunit(RowsArgs g, const WUnit *u
             __syncthreads();
             RP(4);
             for (int j = tid; j < r1 - r0; j += WU_NT) {
-                Ocol[o0 + r0 + j] = (int)(wlo0 + cl[r0 + j]);
-                Oval[o0 + r0 + j] = vals[j];
+                Ccol[o0 + r0 + j] = (int)(wlo0 + cl[r0 + j]);
+                Cval[o0 + r0 + j] = vals[j];
             }
             __syncthreads();  // (the pass's values read before the next pass zeroes them)
             RP(5);
         }
-        if (tid == 0) ucount[u] = wn;
         RP_DONE(0);
         return;
     }
@@ -1851,8 +1892,8 @@ __global__ __launch_bounds__(WU_NT) void k_rows_wunit(RowsArgs g, const WUnit *u
                 const int bit = __builtin_ctzll(word);
                 word &= word - 1ull;
                 if (r >= r0 && r < r1) {
-                    Ocol[o0 + r] = (int)(wlo0 + w * 64 + bit);
-                    Oval[o0 + r] = vals[r - r0];
+                    Ccol[o0 + r] = (int)(wlo0 + w * 64 + bit);
+                    Cval[o0 + r] = vals[r - r0];
                 }
                 ++r;
             }
@@ -1860,24 +1901,8 @@ __global__ __launch_bounds__(WU_NT) void k_rows_wunit(RowsArgs g, const WUnit *u
         __syncthreads();  // (the pass's values read before the next pass zeroes them)
         RP(10);
     }
-    if (tid == 0) ucount[u] = wn;
     RP(11);
     RP_DONE(0);
-}
-
-// each unit's nonzeros from the output area to C at the row's pointer plus the
-// unit's output offset (uoff, from k_rows_wscan of ucount); after the row scan
-__global__ __launch_bounds__(WG) void k_rows_wgather(RowsArgs g, const int *umap, const long long *wpre,
-                                                    const int *ubo, const int *uoff, const int *ucount,
-                                                    const int *Ocol, const double *Oval, const int *Crp, int *Ccol,
-                                                    double *Cval) {
-    const int u = blockIdx.x, i = umap[u];
-    const long long src = wpre[i] + ubo[u], dst = (long long)Crp[g.list[i].x] + uoff[u];
-    const int n = ucount[u];
-    for (int j = threadIdx.x; j < n; j += WG) {
-        Ccol[dst + j] = Ocol[src + j];
-        Cval[dst + j] = Oval[src + j];
-    }
 }
 
 // ---- hub rows dominated by one run (mawi: a hub neighbour's C row is the
@@ -2303,7 +2328,7 @@ __global__ __launch_bounds__(WG) void k_rows_compact(int m, const int *cfirst, c
     for (int u = 0; u < PT; ++u) rowof[tid * PT + u] = max(carry, loc[u]);
     __syncthreads();
     // each thread's PT positions: their rows' offsets, then every load, then
-    // every store (a windowed row's positions, soff < 0, are k_rows_wgather's)
+    // every store (a windowed row's positions, soff < 0, are k_rows_wunit<1>'s)
     long long src[PT];
     bool ok[PT];
 #pragma unroll
@@ -2501,13 +2526,12 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
     int *dord = nullptr;
     // windowed (W) rows' arrays: per class-H row, per unit, per chunk
     int *wnw = nullptr, *wnch = nullptr, *wlo = nullptr, *wwb = nullptr, *umap = nullptr;
-    int *ucnt = nullptr, *ubo = nullptr, *ucount = nullptr, *uoff = nullptr, *Wc = nullptr;
+    int *ucnt = nullptr, *ubo = nullptr, *ucount = nullptr, *uoff = nullptr;
     WUnit *urec = nullptr;
-    long long *wpre = nullptr, *wmat = nullptr, *cmoff = nullptr;
+    long long *wmat = nullptr, *cmoff = nullptr;
     int *cbo = nullptr;
     unsigned long long *wst = nullptr;
     int4 *wchunks = nullptr;
-    double *Wv = nullptr;
     int nu = 0;
     long long drnch = 0;  // the dominant-run rows' fill chunks (launched after the row scan)
     RowsArgs g7 = g;  // (class H's list, for the windowed rows' gather after the row scan)
@@ -2528,21 +2552,18 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
             TSG_TRY(cx.get(&wnch, (size_t)n7 + 1));
             TSG_TRY(cx.get(&wlo, (size_t)n7));
             TSG_TRY(cx.get(&wwb, (size_t)n7));
-            TSG_TRY(cx.get(&wpre, (size_t)n7 + 1));
             TSG_TRY(cx.get(&wmat, (size_t)n7 + 1));
             TSG_TRY(cx.get(&wst, 4));
             TSG_HIP(hipMemsetAsync(wst, 0, 4 * sizeof(unsigned long long), s));
             // (W_UNIT products per unit: 4,096 measured equal, 16,384 / 32,768 slower)
-            k_rows_wplan<<<n7, W_NT, 0, s>>>(g, B.n, W_UNIT, wnw, wnch, wlo, wwb, wpre, wmat,
+            k_rows_wplan<<<n7, W_NT, 0, s>>>(g, B.n, W_UNIT, wnw, wnch, wlo, wwb, wmat,
                                              wst, soff);
             TSG_HIP(hipGetLastError());
             TSG_HIP(hipMemsetAsync(wnw + n7, 0, sizeof(int), s));
             TSG_HIP(hipMemsetAsync(wnch + n7, 0, sizeof(int), s));
-            TSG_HIP(hipMemsetAsync(wpre + n7, 0, sizeof(long long), s));
             TSG_HIP(hipMemsetAsync(wmat + n7, 0, sizeof(long long), s));
             TSG_TRY(scan_exclusive_i32(cx, wnw, (long)n7 + 1, s));   // -> ubase
             TSG_TRY(scan_exclusive_i32(cx, wnch, (long)n7 + 1, s));  // -> cbase
-            TSG_TRY(scan_exclusive_i64(cx, wpre, (long)n7 + 1, s));  // -> output-area offsets
             TSG_TRY(scan_exclusive_i64(cx, wmat, (long)n7 + 1, s));  // -> chunk x window offset matrix
             TSG_HIP(hipMemcpyAsync(cx.pinned64 + 16, wst, 3 * sizeof(long long), hipMemcpyDeviceToHost, s));
             TSG_HIP(hipMemcpyAsync(reinterpret_cast<int *>(cx.pinned64 + 20), wnw + n7, sizeof(int),
@@ -2569,8 +2590,6 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
             TSG_TRY(cx.get(&ucount, (size_t)nu));
             TSG_TRY(cx.get(&uoff, (size_t)nu));
             TSG_TRY(cx.get(&urec, (size_t)nu));
-            TSG_TRY(cx.get(&Wc, (size_t)wprod + 1));
-            TSG_TRY(cx.get(&Wv, (size_t)wprod + 1));
             TSG_HIP(hipMemsetAsync(ucnt, 0, (size_t)nu * sizeof(int), s));
             // (the run map of each walk step, not a binary search of the run table
             // per product: 2.75 vs 3.25 ms on the LiveJournal block)
@@ -2578,11 +2597,11 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
             TSG_HIP(hipGetLastError());
             k_rows_wcount<<<nc, W_NT, 0, s>>>(g, wchunks, cmoff, wlo, wwb, ubase, ucnt, cbo);
             TSG_HIP(hipGetLastError());
-            k_rows_wscan<<<n7, W_NT, 0, s>>>(g, ubase, ucnt, ubo, nullptr, urec, wlo, wwb, wpre);
+            k_rows_wscan<<<n7, W_NT, 0, s>>>(g, ubase, ucnt, ubo, nullptr, urec, wlo, wwb);
             TSG_HIP(hipGetLastError());
             k_rows_wscatter<<<nc, W_NT, 0, s>>>(g, wchunks, cmoff, wlo, wwb, ubase, ubo, cbo);
             TSG_HIP(hipGetLastError());
-            k_rows_wunit<<<nu, WU_NT, 0, s>>>(g, urec, ucount, Wc, Wv);
+            k_rows_wunit<0><<<nu, WU_NT, 0, s>>>(g, urec, ucount, nullptr, nullptr, nullptr, nullptr);
             TSG_HIP(hipGetLastError());
             k_rows_wscan<<<n7, W_NT, 0, s>>>(g, ubase, ucount, uoff, g.rnnz);
             TSG_HIP(hipGetLastError());
@@ -2687,8 +2706,7 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
     // and the dominant-run rows' (their counts exact since k_rows_dr_prep)
     auto wgather = [&]() -> int {
         if (nu > 0) {
-            k_rows_wgather<<<nu, WG, 0, s>>>(g7, umap, wpre, ubo, uoff, ucount, Wc, Wv, C.rowpointer,
-                                             C.columnindex, C.value);
+            k_rows_wunit<1><<<nu, WU_NT, 0, s>>>(g7, urec, ucount, uoff, C.rowpointer, C.columnindex, C.value);
             TSG_HIP(hipGetLastError());
         }
         if (drnch > 0) {
@@ -2749,8 +2767,7 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
     cx.put(Scol);
     cx.put(Sval);
     {
-        void *ws[] = {wnw, wnch, wlo, wwb, wpre, wmat, wst, wchunks, cmoff, cbo, umap, ucnt, ubo, ucount, uoff, Wc, Wv,
-                      urec};
+        void *ws[] = {wnw, wnch, wlo, wwb, wmat, wst, wchunks, cmoff, cbo, umap, ucnt, ubo, ucount, uoff, urec};
         for (void *q : ws) cx.put(q);
     }
     cx.put(Oc);

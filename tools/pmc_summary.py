@@ -101,7 +101,7 @@ def main():
                     spans.append(cur[1] - cur[0])
                 cur = None
             elif any(k.endswith(c) or c + "<" in k for c in ("k_rows_small", "k_rows_merge", "k_rows_bitmap",
-                                                             "k_rows_wcount", "k_rows_wscatter", "k_rows_wunit", "k_rows_wgather", "k_rows_dr_prep", "k_rows_dr_fill")):
+                                                             "k_rows_wcount", "k_rows_wscatter", "k_rows_wunit", "k_rows_dr_prep", "k_rows_dr_fill")):
                 s0, e0 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
                 cur = [min(cur[0], s0), max(cur[1], e0)] if cur else [s0, e0]
         if cur:
