@@ -1407,7 +1407,8 @@ constexpr int W_BLK = 512;                    // words per rank block
 constexpr int W_NBLK = W_WORDS / W_BLK;
 constexpr int W_VCAP = 4096;                  // a unit's values per LDS pass
 constexpr int W_RPT = 8;                      // a unit's products per thread held in registers
-constexpr int WU_NT = 1024;                   // the unit kernel's workgroup (W_RPT * WU_NT >= W_UNIT)
+constexpr int WU_NT = 1024;                   // the unit fill's workgroup (W_RPT * WU_NT >= W_UNIT)
+constexpr int WU_NT0 = 512;                   // the unit count's (its LDS: the bitmap alone)
 constexpr int W_SPANK = 8192;                 // plan: rows past so many runs span all of B's columns
 
 __device__ __forceinline__ int ceil_log2_ll(long long v) {
@@ -1727,10 +1728,10 @@ __device__ __forceinline__ int w_rank(const u64 *bm, const u16 *g4, const int *b
 //     prefixes (u16 per 4-word group, int per 512-word block), the values added
 //     at their ranks in LDS, the unit's nonzeros written in column order into C
 //     at Crp[R.row] + uoff[u].
-template <int MODE>
-__global__ __launch_bounds__(WU_NT) void k_rows_wunit(RowsArgs g, const WUnit *urec, int *ucount, const int *uoff,
+template <int MODE, int NT>
+__global__ __launch_bounds__(NT) void k_rows_wunit(RowsArgs g, const WUnit *urec, int *ucount, const int *uoff,
                                                     const int *Crp, int *Ccol, double *Cval) {
-    constexpr int NW = WU_NT / 64;
+    constexpr int NW = NT / 64;
     __shared__ __align__(16) u64 bm[W_WORDS];
     __shared__ u16 g4[W_WORDS / 4];
     __shared__ int blk[W_NBLK];
@@ -1750,24 +1751,24 @@ __global__ __launch_bounds__(WU_NT) void k_rows_wunit(RowsArgs g, const WUnit *u
     const long long s0 = R.s0;
     const int nwd = 1 << (wb - 6);
     if constexpr (MODE == 0) {
-        for (int w = tid; w < nwd; w += WU_NT) bm[w] = 0ull;
+        for (int w = tid; w < nwd; w += NT) bm[w] = 0ull;
         int cc[W_RPT];
 #pragma unroll
         for (int t = 0; t < W_RPT; ++t) {
-            const int q = t * WU_NT + tid;
+            const int q = t * NT + tid;
             cc[t] = q < n ? (int)(g.Scol[s0 + q] - wlo0) : -1;
         }
         __syncthreads();
 #pragma unroll
         for (int t = 0; t < W_RPT; ++t)
             if (cc[t] >= 0) atomicOr(&bm[cc[t] >> 6], 1ull << (cc[t] & 63));
-        for (int q = W_RPT * WU_NT + tid; q < n; q += WU_NT) {
+        for (int q = W_RPT * NT + tid; q < n; q += NT) {
             const int c = (int)(g.Scol[s0 + q] - wlo0);
             atomicOr(&bm[c >> 6], 1ull << (c & 63));
         }
         __syncthreads();
         int cnt = 0;
-        for (int w = tid; w < nwd; w += WU_NT) cnt += __popcll(bm[w]);
+        for (int w = tid; w < nwd; w += NT) cnt += __popcll(bm[w]);
         cnt = wave_sum(cnt);
         if (lane == 0) red[wv] = cnt;
         __syncthreads();
@@ -1780,14 +1781,14 @@ __global__ __launch_bounds__(WU_NT) void k_rows_wunit(RowsArgs g, const WUnit *u
         RP_DONE(0);
         return;
     }
-    // (fill) the first W_RPT * WU_NT products in registers (the rest read again
+    // (fill) the first W_RPT * NT products in registers (the rest read again
     // below), the bitmap again, the unit's place in C
-    for (int w = tid; w < nwd; w += WU_NT) bm[w] = 0ull;
+    for (int w = tid; w < nwd; w += NT) bm[w] = 0ull;
     int cc[W_RPT];
     double xx[W_RPT];
 #pragma unroll
     for (int t = 0; t < W_RPT; ++t) {
-        const int q = t * WU_NT + tid;
+        const int q = t * NT + tid;
         cc[t] = q < n ? (int)(g.Scol[s0 + q] - wlo0) : -1;
         xx[t] = q < n ? g.Sval[s0 + q] : 0.0;
     }
@@ -1796,7 +1797,7 @@ __global__ __launch_bounds__(WU_NT) void k_rows_wunit(RowsArgs g, const WUnit *u
 #pragma unroll
     for (int t = 0; t < W_RPT; ++t)
         if (cc[t] >= 0) atomicOr(&bm[cc[t] >> 6], 1ull << (cc[t] & 63));
-    for (int q = W_RPT * WU_NT + tid; q < n; q += WU_NT) {
+    for (int q = W_RPT * NT + tid; q < n; q += NT) {
         const int c = (int)(g.Scol[s0 + q] - wlo0);
         atomicOr(&bm[c >> 6], 1ull << (c & 63));
     }
@@ -1830,8 +1831,8 @@ __global__ __launch_bounds__(WU_NT) void k_rows_wunit(RowsArgs g, const WUnit *u
     int rk[W_RPT];
 #pragma unroll
     for (int t = 0; t < W_RPT; ++t) rk[t] = cc[t] >= 0 ? w_rank(bm, g4, blk, cc[t]) : 0;
-    static_assert(2 * W_WORDS >= W_RPT * WU_NT, "the bitmap's LDS holds a column per rank (wn <= n)");
-    if (n <= W_RPT * WU_NT) {  // (workgroup-uniform) every product in registers
+    static_assert(2 * W_WORDS >= W_RPT * NT, "the bitmap's LDS holds a column per rank (wn <= n)");
+    if (n <= W_RPT * NT) {  // (workgroup-uniform) every product in registers
         // the bitmap is done with once the ranks are: its LDS takes each rank's
         // column (a column's products store the same one), the values are
         // summed at their ranks W_VCAP at a time, and both go out coalesced
@@ -1845,14 +1846,14 @@ __global__ __launch_bounds__(WU_NT) void k_rows_wunit(RowsArgs g, const WUnit *u
         RP(3);
         for (int r0 = 0; r0 < wn; r0 += W_VCAP) {  // (workgroup-uniform)
             const int r1 = min(wn, r0 + W_VCAP);
-            for (int j = tid; j < r1 - r0; j += WU_NT) vals[j] = 0.0;
+            for (int j = tid; j < r1 - r0; j += NT) vals[j] = 0.0;
             __syncthreads();
 #pragma unroll
             for (int t = 0; t < W_RPT; ++t)
                 if (cc[t] >= 0 && (unsigned)(rk[t] - r0) < (unsigned)W_VCAP) atomicAdd(&vals[rk[t] - r0], xx[t]);
             __syncthreads();
             RP(4);
-            for (int j = tid; j < r1 - r0; j += WU_NT) {
+            for (int j = tid; j < r1 - r0; j += NT) {
                 Ccol[o0 + r0 + j] = (int)(wlo0 + cl[r0 + j]);
                 Cval[o0 + r0 + j] = vals[j];
             }
@@ -1870,12 +1871,12 @@ __global__ __launch_bounds__(WU_NT) void k_rows_wunit(RowsArgs g, const WUnit *u
 #endif
     for (int r0 = 0; r0 < wn; r0 += W_VCAP) {  // (workgroup-uniform; one pass unless wn > W_VCAP)
         const int r1 = min(wn, r0 + W_VCAP);
-        for (int j = tid; j < r1 - r0; j += WU_NT) vals[j] = 0.0;
+        for (int j = tid; j < r1 - r0; j += NT) vals[j] = 0.0;
         __syncthreads();
 #pragma unroll
         for (int t = 0; t < W_RPT; ++t)
             if (cc[t] >= 0 && (unsigned)(rk[t] - r0) < (unsigned)W_VCAP) atomicAdd(&vals[rk[t] - r0], xx[t]);
-        for (int q = W_RPT * WU_NT + tid; q < n; q += WU_NT) {
+        for (int q = W_RPT * NT + tid; q < n; q += NT) {
             const int c = (int)(g.Scol[s0 + q] - wlo0);
             const int rq = w_rank(bm, g4, blk, c) - r0;
             if ((unsigned)rq < (unsigned)W_VCAP) atomicAdd(&vals[rq], g.Sval[s0 + q]);
@@ -1883,7 +1884,7 @@ __global__ __launch_bounds__(WU_NT) void k_rows_wunit(RowsArgs g, const WUnit *u
         __syncthreads();
         RP(9);
         // emit: a thread per bitmap word, its columns at their ranks
-        for (int w = tid; w < nwd; w += WU_NT) {
+        for (int w = tid; w < nwd; w += NT) {
             u64 word = bm[w];
             if (!word) continue;
             int r = w_rank(bm, g4, blk, w * 64);
@@ -2601,10 +2602,33 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
             TSG_HIP(hipGetLastError());
             k_rows_wscatter<<<nc, W_NT, 0, s>>>(g, wchunks, cmoff, wlo, wwb, ubase, ubo, cbo);
             TSG_HIP(hipGetLastError());
-            k_rows_wunit<0><<<nu, WU_NT, 0, s>>>(g, urec, ucount, nullptr, nullptr, nullptr, nullptr);
+            k_rows_wunit<0, WU_NT0><<<nu, WU_NT0, 0, s>>>(g, urec, ucount, nullptr, nullptr, nullptr, nullptr);
             TSG_HIP(hipGetLastError());
             k_rows_wscan<<<n7, W_NT, 0, s>>>(g, ubase, ucount, uoff, g.rnnz);
             TSG_HIP(hipGetLastError());
+#ifdef TSG_W_DUMP
+            {  // (diagnostic) the units by window bits and products
+                std::vector<WUnit> hr(nu);
+                std::vector<int> hc(nu);
+                TSG_HIP(hipMemcpyAsync(hr.data(), urec, sizeof(WUnit) * nu, hipMemcpyDeviceToHost, s));
+                TSG_HIP(hipMemcpyAsync(hc.data(), ucount, sizeof(int) * nu, hipMemcpyDeviceToHost, s));
+                TSG_TRY(stream_wait(s));
+                long long cnt[19][8] = {}, pr[19][8] = {}, nz[19][8] = {};
+                for (int u = 0; u < nu; ++u) {
+                    int b = 0;
+                    while (b < 7 && hr[u].n >= (64 << (2 * b))) ++b;
+                    cnt[hr[u].wb][b]++;
+                    pr[hr[u].wb][b] += hr[u].n;
+                    nz[hr[u].wb][b] += hc[u];
+                }
+                fprintf(stderr, "W rows %d units %d chunks %d products %lld\n", n7, nu, nc, wprod);
+                for (int w = 0; w < 19; ++w)
+                    for (int b = 0; b < 8; ++b)
+                        if (cnt[w][b])
+                            fprintf(stderr, "  wb %2d n<%7d units %7lld products %10lld nnz %10lld\n", w,
+                                    b < 7 ? (64 << (2 * b)) : -1, cnt[w][b], pr[w][b], nz[w][b]);
+            }
+#endif
         }
         if (p.hprod > wprod + drprod) {  // rows of the one-walk bitmap kernel
             if (p.hbig > 0) {  // one-walk rows past OW_CH products: their scratch
@@ -2706,7 +2730,7 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
     // and the dominant-run rows' (their counts exact since k_rows_dr_prep)
     auto wgather = [&]() -> int {
         if (nu > 0) {
-            k_rows_wunit<1><<<nu, WU_NT, 0, s>>>(g7, urec, ucount, uoff, C.rowpointer, C.columnindex, C.value);
+            k_rows_wunit<1, WU_NT><<<nu, WU_NT, 0, s>>>(g7, urec, ucount, uoff, C.rowpointer, C.columnindex, C.value);
             TSG_HIP(hipGetLastError());
         }
         if (drnch > 0) {
