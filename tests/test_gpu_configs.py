@@ -6,7 +6,9 @@ the product runs as sequential tile-row blocks (spgemm_amd.dist.product_blocks,
 what `bench.py --matrix lj` times).  Here: the block with the most work (the
 hub rows, the load-imbalanced case) and strided blocks, each C against the
 numeric Gustavson oracle at 1e8-product blocks (host-checkable sizes).
-(Here: the heaviest block and twenty strided ones.)
+(Here: the heaviest block and twenty strided ones.)  And the whole product,
+every one of the 90 row blocks bench.py times, through size-independent
+properties: C x = A_b (B x) for random x, rows strictly column-sorted.
 
 mawi_201512020330 (config 5) at FULL scale (226 M rows, hub degree 10^7): the
 row prefix of ~2e8 products that `bench.py --matrix mawi` times a larger
@@ -59,6 +61,59 @@ def test_lj_heaviest_and_strided_row_blocks_vs_oracle(lj):
         np.testing.assert_allclose(got[4], ref[4], rtol=1e-10, atol=0)
         assert st["nnzCub"] == 0 or st["nnzCub"] == cum[b1] - cum[b0]
         del Cm, A
+
+
+def _spmv(rowptr, col, val, x):
+    """y = M x for a device CSR (torch; a checker, not the product path)"""
+    import torch
+    return torch.segment_reduce(val * x[col.long()], "sum", offsets=rowptr.long())
+
+
+def test_lj_every_row_block_by_random_vectors(lj):
+    """The WHOLE LiveJournal stand-in (every row block bench.py times, 1.3e11
+    products; the oracle cannot hold them): per block, C x = A_b (B x) for two
+    random x, and every C row strictly column-sorted within [0, n).  The values
+    are positive, so no sum cancels: a missing, extra, doubled or misplaced
+    column moves C x far past the tolerance (1e-10 relative, fp64 sums in other
+    orders).  (The stand-in's values hold zeros: here every value is replaced
+    by a positive one, same structure.)"""
+    import torch
+    from spgemm_amd.device import Context, DeviceCSR
+    m, n, rp, ci, _, cum = lj
+    vv = (np.arange(len(ci)) % 7 + 1) / 4.0
+    blocks = tdist.product_blocks(cum, 0, m, 1.5e9, 16)  # (bench.py's --block-products)
+    assert len(blocks) >= 80
+    dB = DeviceCSR.from_host(m, n, rp, ci, vv)
+    ctx = Context(0)
+    assert ctx.rows_sorted(dB)
+    g = torch.Generator(device="cuda").manual_seed(7)
+    xs = [torch.rand(n, dtype=torch.float64, device="cuda", generator=g) + 0.5 for _ in range(2)]
+    bxs = [_spmv(dB.rowptr, dB.col, dB.val, x) for x in xs]
+    total = 0
+    for bi, (b0, b1) in enumerate(blocks):
+        mb, rpb, cib, vvb = tdist.slice_rows(m, rp, ci, vv, b0, b1)
+        dA = DeviceCSR.from_host(mb, n, rpb, cib, vvb)
+        ctx.reset()
+        c, st = ctx.spgemm(dA, dB, 16, 16, b_sorted=bi > 0)
+        assert st["nnzCub"] == 0 or st["nnzCub"] == cum[b1] - cum[b0]
+        C = ctx.view_torch(c)
+        assert C.m == mb and int(C.rowptr[0]) == 0 and int(C.rowptr[-1]) == c.nnz
+        if c.nnz:
+            assert int(C.col.min()) >= 0 and int(C.col.max()) < n
+            asc = C.col[1:] > C.col[:-1]
+            starts = C.rowptr[1:-1].long()
+            starts = starts[(starts > 0) & (starts < c.nnz)]
+            asc[starts - 1] = True  # (a row's first entry against the previous row's last)
+            assert bool(asc.all()), f"block {bi}: a C row not strictly column-sorted"
+        for x, bx in zip(xs, bxs):
+            got = _spmv(C.rowptr, C.col, C.val, x)
+            ref = _spmv(dA.rowptr, dA.col, dA.val, bx)
+            err = float(((got - ref).abs() / ref.clamp_min(1e-300)).max()) if mb else 0.0
+            assert err <= 1e-10, f"block {bi} rows [{b0}, {b1}): C x off by {err:.3g}"
+        total += c.nnz
+        del C, dA
+    ctx.reset()
+    assert total > 6e10  # (nnz(C) of the whole product: 6.5e10)
 
 
 def test_mawi_full_scale_prefix_vs_scipy():
