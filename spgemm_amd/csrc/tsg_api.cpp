@@ -335,10 +335,11 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
 // scan) and every A tile row holds as many nonzeros as the CSR rows it covers.
 // Otherwise the tile payloads are used (the payload route), so a caller whose
 // CSR and tiles disagree IN THESE COUNTS gets C of the tiles, as from the
-// reference.  Only counts are compared: a CSR with the same counts but other
-// columns is caught only if one of its products falls outside step 1's tiles
-// (the call then returns TSG_ERR_INVALID), and one with the same pattern but
-// other values gives C of the CSR's values.
+// reference.  Only counts are compared up front: a CSR with the same counts but
+// other columns is caught when one of its products falls outside step 1's tiles
+// (or C's tile totals miss its nnz), and the call then reruns on the payload
+// route; one whose products all land in step 1's tiles, or with the same
+// pattern but other values, gives C of the CSR.
 static bool csr_matches_tiles(const tsg_smatrix *A, const tsg_smatrix *B, int tm) {
     for (const tsg_smatrix *M : {A, B}) {
         if (!M->rowpointer || !M->columnindex || !M->value || !M->tile_nnz || !M->tile_ptr) return false;
@@ -777,8 +778,18 @@ int tsg_tilespgemm(tsg_smatrix *A, tsg_smatrix *B, tsg_smatrix *C, unsigned int 
         if (!se) evi[0] = evi[1] = evi[2] = evi[3] = -1;  // (no step times)
         if (rc == TSG_OK) TSG_HIP(hipStreamSynchronize(s));
         // a nonzero of the CSR product outside step 1's tiles, or tile totals that
-        // miss nnz(C): the CSR disagrees with the tiles it was passed with
-        if (rc == TSG_OK && cx.pinned[8] != 0) rc = TSG_ERR_INVALID;
+        // miss nnz(C): the CSR disagrees with the tiles it was passed with (same
+        // counts, other columns) -- C of the tile payloads after all, as from the
+        // reference, the payloads' copies inside the timed region (this call's work)
+        if (rc == TSG_OK && cx.pinned[8] != 0) {
+            use_csr = false;
+            evi[0] = 0, evi[1] = 1, evi[2] = 2, evi[3] = 3;
+            t_s1 = -1.0;
+            rc = upload_tiles(cx, A, tm, tn, false, dA, s);
+            if (rc == TSG_OK) rc = upload_tiles(cx, B, tn, tm, true, dB, s);
+            dC = tsg_dev_tiles{};
+            if (rc == TSG_OK) rc = dev_tilespgemm(cx, dA, dB, dC, &st, s, cx.ev, nullptr, nullptr, nullptr, false);
+        }
     } else if (sq16) {
         rc = dev_tilespgemm(cx, dA, dB, dC, &st, s, cx.ev, nullptr, nullptr, nullptr, false);
     } else {

@@ -494,6 +494,52 @@ def test_tiled_csr_disagreeing_with_tiles_takes_the_payload_route(which):
     assert_csr_equal(Cm.csr(), O.gustavson(oA, oB).csr())
 
 
+def test_tiled_csr_with_other_columns_reruns_on_the_payload_route():
+    """A CSR with the tiles' counts but another column (so csr_matches_tiles
+    passes): one A entry moved to a column c2 whose B row reaches a C tile
+    that step 1's structure (from the tiles) does not hold.  The CSR route
+    finds a product outside step 1's tiles and the call reruns on the tile
+    payloads: C is the tiles' product, every C tile field equal to the
+    oracle's (it used to return TSG_ERR_INVALID)."""
+    m, n, rp, ci, vv = synth.random_csr(1200, 1200, density=0.0015, seed=23)
+    A = T.Matrix.from_csr(m, n, rp, ci, vv)
+    B = T.Matrix.from_csr(m, n, rp.copy(), ci.copy(), vv.copy())
+    T.csr2tile_row_major(A, 16, 16)
+    T.csr2tile_col_major(B, 16, 16)
+    oA = O.OMat.from_csr(m, n, rp, ci, vv)
+    oB = O.OMat.from_csr(m, n, rp, ci, vv)
+    O.csr2tile_row_major(oA, 16, 16)
+    O.csr2tile_col_major(oB, 16, 16)
+    want = O.c_tiles(O.tilespgemm(oA, oB, 16, 16), 16)
+    # C's tile structure per tile row (step 1's, empty tiles included)
+    tp, tc = want["tile_ptr"], want["tile_columnidx"]
+    have = [set(tc[tp[i]:tp[i + 1]].tolist()) for i in range(len(tp) - 1)]
+    pick = None
+    for r in range(m):
+        if rp[r + 1] == rp[r]:
+            continue
+        for c2 in range(n):
+            if c2 in ci[rp[r]:rp[r + 1]] or rp[c2 + 1] == rp[c2]:
+                continue
+            if any(int(j) // 16 not in have[r // 16] for j in ci[rp[c2]:rp[c2 + 1]]):
+                pick = (r, c2)
+                break
+        if pick:
+            break
+    assert pick, "no column reaching outside C's tiles"
+    r, c2 = pick
+    ci2 = ci.astype(np.int32).copy()
+    ci2[rp[r]] = c2  # (same counts everywhere; A's rows need not stay sorted)
+    A._keep += [ci2]
+    A.s.columnindex = ci2.ctypes.data_as(ctypes.POINTER(ctypes.c_int))
+    Cm, _ = T.tilespgemm(A, B, 16, 16)
+    ct = Cm.tiles(16, 1)
+    for k in C_KEYS:
+        np.testing.assert_array_equal(ct[k], want[k], err_msg=f"C {k}")
+    T.tile2csr(Cm, 16, 16)
+    assert_csr_equal(Cm.csr(), O.gustavson(oA, oB).csr())
+
+
 @pytest.mark.parametrize("where", ["unreferenced", "referenced", "long_row_tail", "none"])
 def test_row_block_checks_only_referenced_b_rows(monkeypatch, where):
     """A row block far smaller than B (nnz(A) * 64 < B's rows: the mawi prefix)
