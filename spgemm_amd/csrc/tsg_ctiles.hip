@@ -69,8 +69,9 @@ __global__ __launch_bounds__(WG) void k_ct_bounds(int m, const int *Crp, const i
 //   * the unit's nonzeros, flat over its 16 row segments, CT_EPT per thread in
 //     registers (columns, values, rows; every load independent), in batches
 //     past CT_EB;
-//   * pass A: each nonzero's tile by a binary search of tcl in LDS; the (tile,
-//     row) masks by LDS atomicOr (bit 15 - c, the reference's mask);
+//   * pass A: each nonzero's tile by a binary search of tcl in LDS (kept in
+//     registers for pass B when the unit is one batch); the (tile, row) masks
+//     by LDS atomicOr (bit 15 - c, the reference's mask);
 //   * tile totals = popcounts of the mask words, a workgroup scan -> the tiles'
 //     offsets; then a thread per tile, consecutive tiles on consecutive lanes:
 //     tile_nnz, Ptr and mask (2 x 16 B each; zeros for the empty tiles);
@@ -146,18 +147,19 @@ __global__ __launch_bounds__(CT_NT) void k_ctiles(int m, const int *Crp, const i
         return tcl[a] == tc ? a : -1;
     };
     if (nbat == 1) load_batch(0);
+    int tk[CT_EPT];  // (one batch: each nonzero's unit tile, kept for pass B)
     // pass A: the masks
     for (int bb = 0; bb < nbat; ++bb) {  // (workgroup-uniform)
         if (nbat > 1) load_batch(bb);
 #pragma unroll
-        for (int k = 0; k < CT_EPT; ++k)
-            if (cc[k] >= 0) {
-                const int tl = tile_of(cc[k]);
-                if (tl >= 0)
-                    atomicOr(&mk[tl * 8 + (rr[k] >> 1)], (0x8000u >> (cc[k] & 15)) << (16 * (rr[k] & 1)));
-                else
-                    atomicExch(fail, 1);  // (never expected: a nonzero outside step 1's tiles)
-            }
+        for (int k = 0; k < CT_EPT; ++k) {
+            const int tl = cc[k] >= 0 ? tile_of(cc[k]) : -1;
+            tk[k] = tl;
+            if (tl >= 0)
+                atomicOr(&mk[tl * 8 + (rr[k] >> 1)], (0x8000u >> (cc[k] & 15)) << (16 * (rr[k] & 1)));
+            else if (cc[k] >= 0)
+                atomicExch(fail, 1);  // (never expected: a nonzero outside step 1's tiles)
+        }
     }
     __syncthreads();
     {  // tile totals (a thread's tiles consecutive), scanned into the offsets
@@ -219,7 +221,7 @@ __global__ __launch_bounds__(CT_NT) void k_ctiles(int m, const int *Crp, const i
         if (nbat > 1) load_batch(bb);
 #pragma unroll
         for (int k = 0; k < CT_EPT; ++k) {
-            const int tl = cc[k] >= 0 ? tile_of(cc[k]) : -1;
+            const int tl = nbat == 1 ? tk[k] : cc[k] >= 0 ? tile_of(cc[k]) : -1;
             if (tl >= 0) {
                 const int r = rr[k], c = cc[k] & 15;
                 const uint4 a = reinterpret_cast<const uint4 *>(mk)[2 * tl];
