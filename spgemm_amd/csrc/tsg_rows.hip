@@ -1394,6 +1394,8 @@ __device__ __forceinline__ long long row_longest_run(const long long *E, int a0,
 //                  LiveJournal block 29.6 -> 29.2 ms.  Storing the count
 //                  kernel's bitmaps for the fill to load, 2^wb bits per unit,
 //                  measured 31.1 ms.)
+//   k_rows_wsort   on the checked-scan path (list sizes read back with nnz(C)),
+//                  units of at most WS_CAP products instead: a sort, no bitmap.
 // Every product is read from B once for its column (counts) and once with its
 // value (scatter), then through its bucket once; no global atomic per
 // product, and a hub row's work is spread over as many workgroups as it has
@@ -1409,6 +1411,8 @@ constexpr int W_VCAP = 4096;                  // a unit's values per LDS pass
 constexpr int W_RPT = 8;                      // a unit's products per thread held in registers
 constexpr int WU_NT = 1024;                   // the unit fill's workgroup (W_RPT * WU_NT >= W_UNIT)
 constexpr int WU_NT0 = 512;                   // the unit count's (its LDS: the bitmap alone)
+constexpr int WS_NT = 256, WS_CAP = 4 * WS_NT;  // units of at most WS_CAP products: the sort fill
+constexpr int WS_MAX = WS_CAP;                   // (the sort fill's units: 1 .. WS_MAX products)
 constexpr int W_SPANK = 8192;                 // plan: rows past so many runs span all of B's columns
 
 __device__ __forceinline__ int ceil_log2_ll(long long v) {
@@ -1617,10 +1621,15 @@ struct WUnit {
 
 // per W row (a workgroup per class-H row): out[u] = exclusive scan of in[u]
 // over the row's units; rnnz (optional) gets the row's total; rec (optional,
-// with wlo, wwb) the units' work records
+// with wlo, wwb) the units' work records, and the fill lists: units of 1 ..
+// WS_CAP products appended to ulist (lcnt[0]: the sort fill's); for the
+// bitmap fill, units past W_RPT * WU_NT products to the back of ulist2,
+// ulist2[nu - 1 - i] (lcnt[1]), the others to its front (lcnt[2]) -- the
+// longest units dispatched first, so that none starts at the fill's end
 __global__ __launch_bounds__(W_NT) void k_rows_wscan(RowsArgs g, const int *ubase, const int *in, int *out,
                                                     int *rnnz, WUnit *rec = nullptr, const int *wlo = nullptr,
-                                                    const int *wwb = nullptr) {
+                                                    const int *wwb = nullptr, int *ulist = nullptr,
+                                                    int *ulist2 = nullptr, int *lcnt = nullptr, int nu = 0) {
     constexpr int NW = W_NT / 64, PT = W_MAXW / W_NT;
     __shared__ int red[NW];
     const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
@@ -1661,6 +1670,31 @@ __global__ __launch_bounds__(W_NT) void k_rows_wscan(RowsArgs g, const int *ubas
         off += v[t];
     }
     if (rnnz && tid == 0) rnnz[g.list[blockIdx.x].x] = tot;
+    if (ulist) {  // (kernel-uniform) the fill lists, one atomic per wave and list
+        constexpr int HEAVY = W_RPT * WU_NT;
+        int ns = 0, nh = 0, nm = 0;
+#pragma unroll
+        for (int t = 0; t < PT; ++t) {
+            ns += v[t] > 0 && v[t] <= WS_MAX;
+            nh += v[t] > HEAVY;
+            nm += v[t] > WS_MAX && v[t] <= HEAVY;
+        }
+        const int is = wave_incl_scan_dpp(ns), ih = wave_incl_scan_dpp(nh), im = wave_incl_scan_dpp(nm);
+        int bs = 0, bh = 0, bm = 0;
+        if (lane == 63) {
+            bs = is ? atomicAdd(&lcnt[0], is) : 0;
+            bh = ih ? atomicAdd(&lcnt[1], ih) : 0;
+            bm = im ? atomicAdd(&lcnt[2], im) : 0;
+        }
+        int ps = __shfl(bs, 63, 64) + is - ns, ph = __shfl(bh, 63, 64) + ih - nh, pm = __shfl(bm, 63, 64) + im - nm;
+#pragma unroll
+        for (int t = 0; t < PT; ++t) {
+            const int w = tid * PT + t;
+            if (v[t] > 0 && v[t] <= WS_MAX) ulist[ps++] = u0 + w;
+            else if (v[t] > HEAVY) ulist2[nu - 1 - ph++] = u0 + w;
+            else if (v[t] > WS_MAX) ulist2[pm++] = u0 + w;
+        }
+    }
 }
 
 // the chunk's products to their windows' buckets in the row's staging slots
@@ -1730,7 +1764,9 @@ __device__ __forceinline__ int w_rank(const u64 *bm, const u16 *g4, const int *b
 //     at Crp[R.row] + uoff[u].
 template <int MODE, int NT>
 __global__ __launch_bounds__(NT) void k_rows_wunit(RowsArgs g, const WUnit *urec, int *ucount, const int *uoff,
-                                                    const int *Crp, int *Ccol, double *Cval) {
+                                                    const int *Crp, int *Ccol, double *Cval,
+                                                    const int *ulist = nullptr, int ulast = 0,
+                                                    int nheavy = 0) {
     constexpr int NW = NT / 64;
     __shared__ __align__(16) u64 bm[W_WORDS];
     __shared__ u16 g4[W_WORDS / 4];
@@ -1739,7 +1775,8 @@ __global__ __launch_bounds__(NT) void k_rows_wunit(RowsArgs g, const WUnit *urec
     __shared__ int red[NW];
     RP_INIT
     const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
-    const int u = blockIdx.x;
+    const int b = blockIdx.x;  // (with a list: its heavy units from the back first, then the rest from the front)
+    const int u = ulist ? ulist[b < nheavy ? ulast - b : b - nheavy] : b;
     const WUnit R = urec[u];
     const int n = R.n;
     if (n == 0) {  // (workgroup-uniform)
@@ -1904,6 +1941,96 @@ __global__ __launch_bounds__(NT) void k_rows_wunit(RowsArgs g, const WUnit *urec
     }
     RP(11);
     RP_DONE(0);
+}
+
+// a workgroup per unit of 1 .. WS_CAP products (the front of the fill list):
+// the unit's nonzeros into C by a sort, not a window bitmap.  A sparse row's
+// unit (LiveJournal: 2^18-column windows of ~600 products, nearly every column
+// once) spent its time on the 32 KB bitmap's clear, sweeps and barriers at two
+// workgroups per CU; here 16 KB of LDS, eight workgroups per CU.  Keys
+// (column - wlo0) << 10 | position, unique: each wave sorts its 256 in
+// registers, a bitonic merge over the waves' segments through LDS (only as
+// many as the unit fills), then each run of equal columns is summed in
+// position order by its first element and written at its rank.
+__global__ __launch_bounds__(WS_NT) void k_rows_wsort(RowsArgs g, const WUnit *urec, const int *ulist,
+                                                    const int *uoff, const int *Crp, int *Ccol, double *Cval) {
+    constexpr int NW = WS_NT / 64, SEG = 256, IB = WS_CAP == 1024 ? 10 : WS_CAP == 2048 ? 11 : 12;
+    static_assert((1 << IB) == WS_CAP && (W_WBMAX + IB) < 32, "keys: window column and position in a u32");
+    __shared__ __align__(16) u32 kb[2][WS_CAP];
+    __shared__ __align__(16) double V[WS_CAP];
+    __shared__ int red[NW];
+    const int u = ulist[blockIdx.x];
+    const WUnit R = urec[u];
+    const int n = R.n;  // (1 .. WS_CAP)
+    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    const int e0 = 4 * tid;  // (= 256 wv + 4 lane: a wave's segment of positions)
+    u32 x[4];
+    double xv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int q = e0 + k;
+        x[k] = q < n ? ((u32)(g.Scol[R.s0 + q] - R.wlo0) << IB) | (u32)q : ~0u;
+        xv[k] = q < n ? g.Sval[R.s0 + q] : 0.0;
+    }
+    const long long o0 = (long long)Crp[R.row] + uoff[u];
+    int npow = SEG;  // the sort's length: n padded to a power of two (~0u keys)
+    while (npow < n) npow <<= 1;
+    const bool act = wv * SEG < npow;  // (wave-uniform)
+    if (e0 < n) reinterpret_cast<double4 *>(V)[tid] = make_double4(xv[0], xv[1], xv[2], xv[3]);
+    if (wv * SEG < n) wave_sort256(x, lane);
+    if (act) *reinterpret_cast<uint4 *>(kb[0] + e0) = make_uint4(x[0], x[1], x[2], x[3]);
+    __syncthreads();
+    int src = 0;
+    auto cmpx = [&](const uint4 y, bool rev, bool keep_min) {
+        const u32 yy[4] = {rev ? y.w : y.x, rev ? y.z : y.y, rev ? y.y : y.z, rev ? y.x : y.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = keep_min ? min(x[k], yy[k]) : max(x[k], yy[k]);
+    };
+    for (int K = 2 * SEG; K <= npow; K <<= 1) {  // (workgroup-uniform)
+        if (act) cmpx(*reinterpret_cast<const uint4 *>(kb[src] + (e0 ^ (K - 4))), true, (e0 & (K >> 1)) == 0);
+        for (int J = K >> 2; J >= SEG; J >>= 1) {
+            src ^= 1;
+            if (act) *reinterpret_cast<uint4 *>(kb[src] + e0) = make_uint4(x[0], x[1], x[2], x[3]);
+            __syncthreads();
+            if (act) cmpx(*reinterpret_cast<const uint4 *>(kb[src] + (e0 ^ J)), false, (e0 & J) == 0);
+        }
+        if (act) bitonic_merge<256, 128>(x, lane);
+        src ^= 1;
+        if (act) *reinterpret_cast<uint4 *>(kb[src] + e0) = make_uint4(x[0], x[1], x[2], x[3]);
+        __syncthreads();
+    }
+    const u32 *const ks = kb[src];  // the sorted keys (positions >= n: ~0u)
+    // heads: the first position of each column; their ranks by a workgroup scan
+    u32 prev = e0 > 0 && e0 - 1 < n ? ks[e0 - 1] >> IB : ~0u;
+    bool hd[4];
+    int nh = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const u32 col = x[k] >> IB;
+        hd[k] = e0 + k < n && col != prev;
+        prev = col;
+        nh += hd[k];
+    }
+    const int inc = wave_incl_scan_dpp(nh);
+    if (lane == 63) red[wv] = inc;
+    __syncthreads();
+    int rk = inc - nh;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) rk += w < wv ? red[w] : 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (hd[k]) {
+            const u32 col = x[k] >> IB;
+            double sum = V[x[k] & (WS_CAP - 1)];
+            for (int p = e0 + k + 1; p < n; ++p) {  // (the column's other products, in position order)
+                const u32 y = ks[p];
+                if ((y >> IB) != col) break;
+                sum += V[y & (WS_CAP - 1)];
+            }
+            Ccol[o0 + rk] = (int)(R.wlo0 + (long long)col);
+            Cval[o0 + rk] = sum;
+            ++rk;
+        }
 }
 
 // ---- hub rows dominated by one run (mawi: a hub neighbour's C row is the
@@ -2527,7 +2654,8 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
     int *dord = nullptr;
     // windowed (W) rows' arrays: per class-H row, per unit, per chunk
     int *wnw = nullptr, *wnch = nullptr, *wlo = nullptr, *wwb = nullptr, *umap = nullptr;
-    int *ucnt = nullptr, *ubo = nullptr, *ucount = nullptr, *uoff = nullptr;
+    int *ucnt = nullptr, *ubo = nullptr, *ucount = nullptr, *uoff = nullptr, *ulist = nullptr, *ulist2 = nullptr,
+        *lcnt = nullptr;
     WUnit *urec = nullptr;
     long long *wmat = nullptr, *cmoff = nullptr;
     int *cbo = nullptr;
@@ -2591,14 +2719,18 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
             TSG_TRY(cx.get(&ucount, (size_t)nu));
             TSG_TRY(cx.get(&uoff, (size_t)nu));
             TSG_TRY(cx.get(&urec, (size_t)nu));
+            TSG_TRY(cx.get(&ulist, (size_t)nu));
+            TSG_TRY(cx.get(&ulist2, (size_t)nu));
+            TSG_TRY(cx.get(&lcnt, 3));
             TSG_HIP(hipMemsetAsync(ucnt, 0, (size_t)nu * sizeof(int), s));
+            TSG_HIP(hipMemsetAsync(lcnt, 0, 3 * sizeof(int), s));
             // (the run map of each walk step, not a binary search of the run table
             // per product: 2.75 vs 3.25 ms on the LiveJournal block)
             k_rows_wchunks<<<n7, WG, 0, s>>>(g, ubase, cbase, wmat, wchunks, cmoff, umap);
             TSG_HIP(hipGetLastError());
             k_rows_wcount<<<nc, W_NT, 0, s>>>(g, wchunks, cmoff, wlo, wwb, ubase, ucnt, cbo);
             TSG_HIP(hipGetLastError());
-            k_rows_wscan<<<n7, W_NT, 0, s>>>(g, ubase, ucnt, ubo, nullptr, urec, wlo, wwb);
+            k_rows_wscan<<<n7, W_NT, 0, s>>>(g, ubase, ucnt, ubo, nullptr, urec, wlo, wwb, ulist, ulist2, lcnt, nu);
             TSG_HIP(hipGetLastError());
             k_rows_wscatter<<<nc, W_NT, 0, s>>>(g, wchunks, cmoff, wlo, wwb, ubase, ubo, cbo);
             TSG_HIP(hipGetLastError());
@@ -2674,7 +2806,10 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
     // otherwise -- or when that allocation fails -- the checked scan reads nnz(C)
     // back first and C is sized exactly.
     long long nnz = 0;  // (C.rowpointer[m] = 0 from the binning kernel)
-    bool small = products <= 0x7fffffffLL && products * 12 <= kRowsProductSizedC;
+    // (TSG_ROWS_CHECKED_SCAN=1: the checked scan whatever the size -- tests take
+    // the large products' path, with its fill lists, on small ones)
+    const char *cs = getenv("TSG_ROWS_CHECKED_SCAN");
+    bool small = products <= 0x7fffffffLL && products * 12 <= kRowsProductSizedC && !(cs && cs[0] == '1');
     long long cap = 0;
     // small with at most RS_INLINE_MAX tiles of row counts: one launch of tile
     // sums, then one apply that also fills the compaction's chunk table and
@@ -2682,6 +2817,8 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
     const long rtile = ((long)m + 1 + RS_TILE - 1) / RS_TILE;
     const bool fused_scan = small && rtile <= RS_INLINE_MAX;
     int *const hnnz = reinterpret_cast<int *>(cx.pinned64 + 15);
+    int *const hl = reinterpret_cast<int *>(cx.pinned64 + 24);  // the fill lists' sizes (3 ints)
+    bool lknown = false;
     int *cfirst = nullptr;
     auto scan_alloc = [&]() -> int {
         if (small) {
@@ -2716,7 +2853,10 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
                 nnz = C.nnz;
             }
         } else {  // the checked scan (nnz(C) past int32 fails)
+            if (nu > 0)  // (the fill lists' sizes come back with the scan's total)
+                TSG_HIP(hipMemcpyAsync(hl, lcnt, 3 * sizeof(int), hipMemcpyDeviceToHost, s));
             TSG_TRY(scan_exclusive_i32_total(cx, C.rowpointer, (long)m + 1, s, &nnz));
+            lknown = nu > 0;
             if (nnz > 0x7fffffffLL) return TSG_ERR_OVERFLOW;
         }
         cap = small ? products : nnz;
@@ -2730,7 +2870,22 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
     // and the dominant-run rows' (their counts exact since k_rows_dr_prep)
     auto wgather = [&]() -> int {
         if (nu > 0) {
-            k_rows_wunit<1, WU_NT><<<nu, WU_NT, 0, s>>>(g7, urec, ucount, uoff, C.rowpointer, C.columnindex, C.value);
+            if (lknown) {
+                // the list sizes came back with the checked scan's total: the bitmap
+                // fill over its list (the longest units first), the sort fill over its
+                const int gs = hl[0], gh = hl[1], gb = hl[1] + hl[2];
+                if (gb > 0)
+                    k_rows_wunit<1, WU_NT><<<gb, WU_NT, 0, s>>>(g7, urec, ucount, uoff, C.rowpointer, C.columnindex,
+                                                               C.value, ulist2, nu - 1, gh);
+                if (gs > 0)
+                    k_rows_wsort<<<gs, WS_NT, 0, s>>>(g7, urec, ulist, uoff, C.rowpointer, C.columnindex, C.value);
+            } else {
+                // (no read-back on this path: a host round trip of its own for the list
+                // sizes, or grids of every unit with the surplus exiting, cost the
+                // heaviest LiveJournal block 0.12-0.18 ms -- the bitmap fill takes all)
+                k_rows_wunit<1, WU_NT><<<nu, WU_NT, 0, s>>>(g7, urec, ucount, uoff, C.rowpointer, C.columnindex,
+                                                           C.value);
+            }
             TSG_HIP(hipGetLastError());
         }
         if (drnch > 0) {
@@ -2791,7 +2946,8 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
     cx.put(Scol);
     cx.put(Sval);
     {
-        void *ws[] = {wnw, wnch, wlo, wwb, wmat, wst, wchunks, cmoff, cbo, umap, ucnt, ubo, ucount, uoff, urec};
+        void *ws[] = {wnw, wnch, wlo, wwb, wmat, wst, wchunks, cmoff, cbo, umap, ucnt, ubo, ucount, uoff, urec,
+                      ulist, ulist2, lcnt};
         for (void *q : ws) cx.put(q);
     }
     cx.put(Oc);

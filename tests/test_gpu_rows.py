@@ -183,11 +183,14 @@ def test_rows_aat_lj_prefix():
     _check((r, n, rp[:r + 1].copy(), ci[:e].copy(), vv[:e].copy()), aat=True)
 
 
-def test_default_routing_hub_rows_windowed(monkeypatch):
+@pytest.mark.parametrize("checked", [False, True])
+def test_default_routing_hub_rows_windowed(monkeypatch, checked):
     """A product with a hub row (past kRowsHubProducts = 65,536 products) that no
     single run dominates stays on the row-merge path: the windowed kernels
-    (k_rows_w*) take the hub row."""
+    (k_rows_w*) take the hub row (checked: through the fill lists, as above)."""
     monkeypatch.delenv("TSG_PATH", raising=False)
+    if checked:
+        monkeypatch.setenv("TSG_ROWS_CHECKED_SCAN", "1")
     n, nb = 300, 100_000
     rng = np.random.default_rng(21)
     # row 0 names every B row (300 runs of 300 columns spread over 100,000:
@@ -258,14 +261,20 @@ def test_rows_unpacked_wide_span(cls_products):
     _check(A, B, real=True, seed=cls_products)
 
 
-def test_rows_hub_rows_windowed_and_dominant_run():
+@pytest.mark.parametrize("checked", [False, True])
+def test_rows_hub_rows_windowed_and_dominant_run(monkeypatch, checked):
     """Hub rows (past 65,536 products): without a dominant run the windowed
     kernels ((row, window) units, products bucketed per unit, per-unit LDS
     bitmaps, LDS values) -- many runs over 1,500,000 columns with heavy collisions (several
     buckets, windows with more nonzeros than one LDS value chunk), two long
     colliding runs; with one (all but <= 4,096 products in one run) the DR
     kernels -- one long run with a few short ones (the mawi pattern) and a row
-    of one run -- beside ordinary rows."""
+    of one run -- beside ordinary rows.  checked: the large products' path
+    (TSG_ROWS_CHECKED_SCAN=1: nnz(C) read back first), where the windowed units
+    are filled from lists -- units of at most 1,024 products by the sort fill
+    (k_rows_wsort), the rest by the bitmap fill, longest first."""
+    if checked:
+        monkeypatch.setenv("TSG_ROWS_CHECKED_SCAN", "1")
     rng = np.random.default_rng(41)
     n = 1_500_000
     nb = 3000
@@ -278,6 +287,10 @@ def test_rows_hub_rows_windowed_and_dominant_run():
              np.array([5, 17, nb - 3]),                                # long run + short ones
              np.array([nb - 2, nb - 1]),                               # two long runs, colliding
              np.array([nb - 2])]                                       # one run, one window
+    # class-H rows of a few thousand products over the whole span: windows of
+    # 2^18 columns, units of ~700 / ~1,050 / ~2,300 products (the sort fill's
+    # and the bitmap fill's sizes on either side of 1,024)
+    arows += [np.sort(rng.choice(nb - 3, size=k, replace=False)) for k in (60, 90, 200)]
     arows += [np.sort(rng.choice(nb - 3, size=5, replace=False)) for _ in range(50)]
     A = _csr(len(arows), nb, arows)
     blen = np.diff(B[2].astype(np.int64))
