@@ -1622,14 +1622,15 @@ struct WUnit {
 // per W row (a workgroup per class-H row): out[u] = exclusive scan of in[u]
 // over the row's units; rnnz (optional) gets the row's total; rec (optional,
 // with wlo, wwb) the units' work records, and the fill lists: units of 1 ..
-// WS_CAP products appended to ulist (lcnt[0]: the sort fill's); for the
-// bitmap fill, units past W_RPT * WU_NT products to the back of ulist2,
-// ulist2[nu - 1 - i] (lcnt[1]), the others to its front (lcnt[2]) -- the
+// WS_CAP products appended to ulist (*lcnt64 bits 0..20: the sort fill's); for
+// the bitmap fill, units past W_RPT * WU_NT products to the back of ulist2,
+// ulist2[nu - 1 - i] (bits 21..41), the others to its front (bits 42..62) -- the
 // longest units dispatched first, so that none starts at the fill's end
 __global__ __launch_bounds__(W_NT) void k_rows_wscan(RowsArgs g, const int *ubase, const int *in, int *out,
                                                     int *rnnz, WUnit *rec = nullptr, const int *wlo = nullptr,
                                                     const int *wwb = nullptr, int *ulist = nullptr,
-                                                    int *ulist2 = nullptr, int *lcnt = nullptr, int nu = 0) {
+                                                    int *ulist2 = nullptr, unsigned long long *lcnt64 = nullptr,
+                                                    int nu = 0) {
     constexpr int NW = W_NT / 64, PT = W_MAXW / W_NT;
     __shared__ int red[NW];
     const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
@@ -1680,13 +1681,16 @@ __global__ __launch_bounds__(W_NT) void k_rows_wscan(RowsArgs g, const int *ubas
             nm += v[t] > WS_MAX && v[t] <= HEAVY;
         }
         const int is = wave_incl_scan_dpp(ns), ih = wave_incl_scan_dpp(nh), im = wave_incl_scan_dpp(nm);
-        int bs = 0, bh = 0, bm = 0;
-        if (lane == 63) {
-            bs = is ? atomicAdd(&lcnt[0], is) : 0;
-            bh = ih ? atomicAdd(&lcnt[1], ih) : 0;
-            bm = im ? atomicAdd(&lcnt[2], im) : 0;
-        }
-        int ps = __shfl(bs, 63, 64) + is - ns, ph = __shfl(bh, 63, 64) + ih - nh, pm = __shfl(bm, 63, 64) + im - nm;
+        // one atomic per wave for the three lists: 21-bit fields of a u64 (nu < 2^21,
+        // the host's condition); three same-address atomics per wave cost ~0.17 ms
+        // per LiveJournal block
+        unsigned long long old = 0;
+        if (lane == 63 && (is | ih | im))
+            old = atomicAdd(lcnt64, (unsigned long long)is | ((unsigned long long)ih << 21) |
+                                        ((unsigned long long)im << 42));
+        old = ((unsigned long long)__shfl((int)(old >> 32), 63, 64) << 32) | (u32)__shfl((int)old, 63, 64);
+        int ps = (int)(old & 0x1fffff) + is - ns, ph = (int)((old >> 21) & 0x1fffff) + ih - nh,
+            pm = (int)(old >> 42) + im - nm;
 #pragma unroll
         for (int t = 0; t < PT; ++t) {
             const int w = tid * PT + t;
@@ -2655,7 +2659,7 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
     // windowed (W) rows' arrays: per class-H row, per unit, per chunk
     int *wnw = nullptr, *wnch = nullptr, *wlo = nullptr, *wwb = nullptr, *umap = nullptr;
     int *ucnt = nullptr, *ubo = nullptr, *ucount = nullptr, *uoff = nullptr, *ulist = nullptr, *ulist2 = nullptr,
-        *lcnt = nullptr;
+        *lcnt = nullptr;  // (the lists' three sizes packed in one u64, 21 bits each)
     WUnit *urec = nullptr;
     long long *wmat = nullptr, *cmoff = nullptr;
     int *cbo = nullptr;
@@ -2721,16 +2725,18 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
             TSG_TRY(cx.get(&urec, (size_t)nu));
             TSG_TRY(cx.get(&ulist, (size_t)nu));
             TSG_TRY(cx.get(&ulist2, (size_t)nu));
-            TSG_TRY(cx.get(&lcnt, 3));
+            TSG_TRY(cx.get(&lcnt, 2));
             TSG_HIP(hipMemsetAsync(ucnt, 0, (size_t)nu * sizeof(int), s));
-            TSG_HIP(hipMemsetAsync(lcnt, 0, 3 * sizeof(int), s));
+            TSG_HIP(hipMemsetAsync(lcnt, 0, 2 * sizeof(int), s));
             // (the run map of each walk step, not a binary search of the run table
             // per product: 2.75 vs 3.25 ms on the LiveJournal block)
             k_rows_wchunks<<<n7, WG, 0, s>>>(g, ubase, cbase, wmat, wchunks, cmoff, umap);
             TSG_HIP(hipGetLastError());
             k_rows_wcount<<<nc, W_NT, 0, s>>>(g, wchunks, cmoff, wlo, wwb, ubase, ucnt, cbo);
             TSG_HIP(hipGetLastError());
-            k_rows_wscan<<<n7, W_NT, 0, s>>>(g, ubase, ucnt, ubo, nullptr, urec, wlo, wwb, ulist, ulist2, lcnt, nu);
+            k_rows_wscan<<<n7, W_NT, 0, s>>>(g, ubase, ucnt, ubo, nullptr, urec, wlo, wwb,
+                                             nu < (1 << 21) ? ulist : nullptr, ulist2,
+                                             reinterpret_cast<unsigned long long *>(lcnt), nu);
             TSG_HIP(hipGetLastError());
             k_rows_wscatter<<<nc, W_NT, 0, s>>>(g, wchunks, cmoff, wlo, wwb, ubase, ubo, cbo);
             TSG_HIP(hipGetLastError());
@@ -2817,7 +2823,7 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
     const long rtile = ((long)m + 1 + RS_TILE - 1) / RS_TILE;
     const bool fused_scan = small && rtile <= RS_INLINE_MAX;
     int *const hnnz = reinterpret_cast<int *>(cx.pinned64 + 15);
-    int *const hl = reinterpret_cast<int *>(cx.pinned64 + 24);  // the fill lists' sizes (3 ints)
+    int *const hl = reinterpret_cast<int *>(cx.pinned64 + 24);  // the fill lists' sizes (a packed u64)
     bool lknown = false;
     int *cfirst = nullptr;
     auto scan_alloc = [&]() -> int {
@@ -2853,10 +2859,10 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
                 nnz = C.nnz;
             }
         } else {  // the checked scan (nnz(C) past int32 fails)
-            if (nu > 0)  // (the fill lists' sizes come back with the scan's total)
-                TSG_HIP(hipMemcpyAsync(hl, lcnt, 3 * sizeof(int), hipMemcpyDeviceToHost, s));
+            if (nu > 0 && nu < (1 << 21))  // (the fill lists' sizes come back with the scan's total)
+                TSG_HIP(hipMemcpyAsync(hl, lcnt, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
             TSG_TRY(scan_exclusive_i32_total(cx, C.rowpointer, (long)m + 1, s, &nnz));
-            lknown = nu > 0;
+            lknown = nu > 0 && nu < (1 << 21);
             if (nnz > 0x7fffffffLL) return TSG_ERR_OVERFLOW;
         }
         cap = small ? products : nnz;
@@ -2873,7 +2879,8 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
             if (lknown) {
                 // the list sizes came back with the checked scan's total: the bitmap
                 // fill over its list (the longest units first), the sort fill over its
-                const int gs = hl[0], gh = hl[1], gb = hl[1] + hl[2];
+                const unsigned long long pk = *reinterpret_cast<const unsigned long long *>(hl);
+                const int gs = (int)(pk & 0x1fffff), gh = (int)((pk >> 21) & 0x1fffff), gb = gh + (int)(pk >> 42);
                 if (gb > 0)
                     k_rows_wunit<1, WU_NT><<<gb, WU_NT, 0, s>>>(g7, urec, ucount, uoff, C.rowpointer, C.columnindex,
                                                                C.value, ulist2, nu - 1, gh);
