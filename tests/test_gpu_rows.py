@@ -299,6 +299,37 @@ def test_rows_hub_rows_windowed_and_dominant_run(monkeypatch, checked):
     _check(A, B, real=True, seed=43)
 
 
+@pytest.mark.parametrize("pool", [None, 3000])
+def test_rows_windowed_sort_fill_unit_sizes(monkeypatch, pool):
+    """The checked-scan path's fill lists across unit sizes: class-H rows of
+    4,100 .. 20,000 products over a 1.5 M-column span (windows of 2^18
+    columns, units of ~700 .. ~3,300 products: the sort fill up to 1,024, the
+    bitmap fill past it), with B's columns drawn from the whole span (few
+    repeats) or from a pool of 3,000 columns (long runs of equal columns in
+    the sort fill's summing walk), plus the npow boundaries 256 / 257 and
+    1,024 / 1,025 of single-window rows.  Pattern exact, values within 1e-10
+    of |A||B|."""
+    monkeypatch.setenv("TSG_ROWS_CHECKED_SCAN", "1")
+    rng = np.random.default_rng(61 if pool is None else 62)
+    n, nb = 1_500_000, 3000
+    cols = np.arange(n) if pool is None else np.sort(rng.choice(n, size=pool, replace=False))
+    Brows = [np.sort(rng.choice(cols, size=int(rng.integers(50, 150)), replace=False)) for _ in range(nb - 4)]
+    # single-window rows: one B row each of 256 / 257 / 1,024 / 1,025 columns inside 2^18
+    for k in (256, 257, 1024, 1025):
+        Brows.append(np.sort(rng.choice(200_000, size=k, replace=False)))
+    B = _csr(nb, n, Brows)
+    blen = np.diff(B[2].astype(np.int64))
+    arows = []
+    for target in (4100, 5000, 6500, 9000, 13000, 20000):
+        k = int(target / blen[:nb - 4].mean())
+        arows.append(np.sort(rng.choice(nb - 4, size=k, replace=False)))
+    # (a row over the single-window B rows and a few short ones: class H by its products)
+    arows.append(np.array([nb - 4, nb - 3, nb - 2, nb - 1] + list(range(10, 40))))
+    arows += [np.sort(rng.choice(nb - 4, size=4, replace=False)) for _ in range(30)]
+    A = _csr(len(arows), nb, arows)
+    _check(A, B, real=True, seed=67)
+
+
 @pytest.mark.parametrize("per_row", [False, True])
 def test_rows_dominant_run_rows_grouped_by_run(monkeypatch, per_row):
     """Many dominant-run rows sharing a run (the mawi pattern: every hub
