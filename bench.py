@@ -262,7 +262,15 @@ def tiled_leg(m, n, rp, ci, vv, mb, nb, rpb, cib, vvb, aat, tm, nnzcub, reps=3, 
             "path": "tsg_tilespgemm (reference tiled layout in/out; the ./test CLI path)"}
 
 
-def pmc_file(workload, explicit=None):
+def profile_order(path):
+    """Sort key of a profiles/r<round><tag>_* file: the round, then the tag in
+    the order tags are handed out (a .. z, then aa .. zz: shorter first)."""
+    import re
+    mt = re.match(r"r(\d+)([A-Za-z]+)_", os.path.basename(path))
+    return (int(mt.group(1)), len(mt.group(2)), mt.group(2)) if mt else (-1, 0, os.path.basename(path))
+
+
+def pmc_file(workload, explicit=None, root=None):
     """The PMC summary the line's traffic comes from: `explicit` (--pmc-from: the
     profile run of the same build writes it right before its timed run), else the
     newest committed profiles/<round>_pmc.json of the same workload."""
@@ -275,7 +283,7 @@ def pmc_file(workload, explicit=None):
             return json.load(open(f)).get("_workload")
         except (OSError, ValueError, AttributeError):  # unreadable / partial summary
             return None
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc.json")))
+    files = sorted(glob.glob(os.path.join(root or REPO, "profiles", "r*_pmc.json")), key=profile_order)
     files = [f for f in files if workload_of(f) == workload]
     return files[-1] if files else None
 

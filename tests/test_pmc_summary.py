@@ -76,3 +76,16 @@ def test_bench_pmc_traffic_counts_dispatches_per_call(tmp_path):
                              "tsg::k_rows_merge": {"dispatches": 9, "hbm_bytes_per_dispatch": 10}}))
     unit, allk = bench.pmc_traffic(["k_rows_wunit", "k_rows_merge"], str(p))
     assert unit == 90 * 1000 + 10 and allk == 123
+
+
+def test_newest_profile_by_round_and_tag_order(tmp_path):
+    """bench.pmc_file's default: the newest summary of the workload by round,
+    then by tag in the order tags are handed out (x < aa < bf), not by name."""
+    import json
+    import bench
+    (tmp_path / "profiles").mkdir()
+    for tag in ("r5z", "r6x", "r6aa", "r6bf", "r6c"):
+        (tmp_path / "profiles" / f"{tag}_webbase_pmc.json").write_text(json.dumps({"_workload": "w"}))
+    (tmp_path / "profiles" / "r6zz_other_pmc.json").write_text(json.dumps({"_workload": "other"}))
+    got = bench.pmc_file("w", root=str(tmp_path))
+    assert os.path.basename(got) == "r6bf_webbase_pmc.json"
