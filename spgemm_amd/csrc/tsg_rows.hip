@@ -2874,7 +2874,7 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
     };
     // the windowed rows' nonzeros straight into C (the compaction skips those rows)
     // and the dominant-run rows' (their counts exact since k_rows_dr_prep)
-    auto wgather = [&]() -> int {
+    auto wfill = [&]() -> int {
         if (nu > 0) {
             if (lknown) {
                 // the list sizes came back with the checked scan's total: the bitmap
@@ -2929,7 +2929,7 @@ int dev_rows_run(Context &cx, const tsg_dev_csr &A, const tsg_dev_csr &B, RowsPl
         }
 #endif
         TSG_TRY(scan_alloc());
-        TSG_TRY(wgather());
+        TSG_TRY(wfill());
         if (ev && fills) TSG_HIP(hipEventRecord(ev[5], s));
         if (cap > 0) {
             const int nch = (int)((cap + CP_CH - 1) / CP_CH);
