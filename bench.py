@@ -506,7 +506,7 @@ def main():
             gathered[0] = None
             sg.reset()
             for s, (_, _, dAb) in enumerate(dA_blocks):
-                c, st = ctx.spgemm(dAb, dB, tm, tm, b_sorted=s > 0 and b_ok)
+                c, st = ctx.spgemm(dAb, dB, tm, tm, b_sorted=s > 0 and b_ok, raw=True)
                 sts.append(st)
                 nnz += c.nnz
                 cv = ctx.view_torch(c)  # zero-copy views of the context-owned C
@@ -525,10 +525,16 @@ def main():
                 ctx.reset()
                 # (row blocks over one B: B's sortedness checked once per step, by the
                 # first block's call; the others skip it -- tsg_dev_spgemm_sorted_b)
-                c, st = ctx.spgemm(dAb, dB, tm, tm, b_sorted=bi > 0 and b_ok)  # returns with C complete
+                c, st = ctx.spgemm(dAb, dB, tm, tm, b_sorted=bi > 0 and b_ok, raw=True)  # returns with C complete
                 sts.append(st)
                 nnz += c.nnz
             compute_ms.append((time.perf_counter() - s0) * 1e3)
+        # (the blocks' raw tsg_stats: merged by merge_stats after the timed steps,
+        # not inside them -- at mc2depi's 0.2 ms a step, the dict work was ~5 %)
+        return c, sts, nnz
+
+    def merge_stats(sts):
+        sts = [s.as_dict() for s in sts]
         st = {k: sum(s[k] for s in sts) for k in sts[0]}
         # (labels, not sums: the path every block took, -1 for "no C tiles")
         paths = {int(s["path"]) for s in sts}
@@ -536,7 +542,7 @@ def main():
         for k in ("numtileA", "numblkC"):
             if k in st and all(s[k] == -1 for s in sts):
                 st[k] = -1
-        return c, st, nnz
+        return st
 
     for _ in range(args.warmup):
         one_step()
@@ -549,6 +555,7 @@ def main():
         c, st, nnz_rank = one_step()
         stats.append(st)
     torch.cuda.synchronize()
+    stats = [merge_stats(x) for x in stats]  # (after the clock; see merge_stats)
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -645,7 +652,7 @@ def main():
         st_stages = []
         try:
             for _ in range(STAGE_STEPS):
-                st_stages.append(one_step()[1])
+                st_stages.append(merge_stats(one_step()[1]))
         finally:
             del os.environ["TSG_STAGE_EVENTS"]
         del gather_ms[n_gm:]

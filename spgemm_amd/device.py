@@ -27,8 +27,13 @@ class DeviceCSR:
         return cls(m, n, rp, ci, vv)
 
     def struct(self):
-        return DevCSR(self.m, self.n, self.nnz, self.rowpointer_ptr(), self.col.data_ptr(),
-                      self.val.data_ptr())
+        # (built once: the tensors are fixed for the object's life, and a timing
+        # loop should not pay for three data_ptr() calls and a ctypes struct per call)
+        s = getattr(self, "_struct", None)
+        if s is None:
+            s = self._struct = DevCSR(self.m, self.n, self.nnz, self.rowpointer_ptr(), self.col.data_ptr(),
+                                      self.val.data_ptr())
+        return s
 
     def rowpointer_ptr(self):
         return self.rowptr.data_ptr()
@@ -59,12 +64,13 @@ class Context:
     def reset(self):
         check("tsg_context_reset", lib().tsg_context_reset(self.ptr))
 
-    def spgemm(self, A, B, tile_m=16, tile_n=16, stream=None, b_sorted=False):
+    def spgemm(self, A, B, tile_m=16, tile_n=16, stream=None, b_sorted=False, raw=False):
         """C = A*B device CSR in -> device CSR out.  Returns (DevCSR struct with
         context-owned pointers, stats dict).  Valid until the next reset().
         b_sorted=True: the caller found B's rows column-sorted (rows_sorted) and B
         has not changed since -- the per-call check is skipped
-        (tsg_dev_spgemm_sorted_b)."""
+        (tsg_dev_spgemm_sorted_b).  raw=True: the stats as the tsg_stats struct
+        (its as_dict() later: a timing loop keeps the conversion out)."""
         a, b, c, st = A.struct(), B.struct(), DevCSR(), Stats()
         s = C.c_void_p(stream) if stream else None
         if b_sorted:
@@ -73,7 +79,7 @@ class Context:
         else:
             check("tsg_dev_spgemm", lib().tsg_dev_spgemm(self.ptr, C.byref(a), C.byref(b), tile_m, tile_n, s,
                                                          C.byref(c), C.byref(st)))
-        return c, st.as_dict()
+        return c, (st if raw else st.as_dict())
 
     def rows_sorted(self, M, stream=None):
         """whether every row of the device CSR M is strictly column-sorted"""
