@@ -1062,8 +1062,10 @@ static int dev_spgemm16(Context &cx, const tsg_dev_csr *A, const tsg_dev_csr *B,
                 TSG_TRY(stream_wait(s));
                 return TSG_OK;
             }
-            TSG_HIP(hipEventRecord(cx.ev[10], s));
-            TSG_HIP(hipEventSynchronize(cx.ev[10]));
+            // (the path returned with its stream drained; the end marker only for
+            // the stage times -- its record and synchronisation cost a few us a call)
+            if (cx.stage_ev) TSG_HIP(hipEventRecord(cx.ev[10], s));
+            TSG_TRY(stream_wait(s));
             auto h1 = std::chrono::steady_clock::now();
             st.numtileA = -1;
             st.numtileB = -1;
